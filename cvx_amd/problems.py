@@ -1,0 +1,106 @@
+"""Problem generators (synthetic inputs for the barrier path).
+
+Plain numpy arrays in the packing the engine consumes: objective r0 + a0.x + x'Px/2
+(P None => LinearObjectiveFunction), linear inequalities r_i + a_i.x <= ub_i with A row i = a_i in
+constraint LIST order, optional equalities Aeq x = beq.
+
+* ``random_qp`` — the seeded dense QP of SURVEY.md §8(d) used for configs C2/C3/C5, following the
+  reference generator patterns (Constraints.scala:158-171 random a_i in [-1,1]; ConstraintSets.scala:67-89;
+  MatrixUtils.scala:57-74): a_i ~ U[-1,1]^n, r_i = 0, ub_i ~ U[0.1,0.2], x0 = 0 strictly feasible,
+  P = R'R/n + I, a0 = -P x_tgt with x_tgt ~ 10 U[-1,1]^n.
+* known-answer problems of SimpleOptimizationProblems.scala that fit the linear-constraint engine.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+
+SEED_BASE = 20261015
+
+
+def random_qp(n: int, m: int, instance: int = 0, dtype=np.float64) -> Dict[str, np.ndarray]:
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + instance))
+    A = rng.uniform(-1.0, 1.0, size=(m, n)).astype(dtype)
+    ub = rng.uniform(0.1, 0.2, size=m)
+    R = rng.uniform(-1.0, 1.0, size=(n, n))
+    P = (R.T @ R) / n + np.eye(n)
+    P = 0.5 * (P + P.T)  # exactly symmetric (the reference's Breeze cholesky checks symmetry)
+    x_tgt = 10.0 * rng.uniform(-1.0, 1.0, size=n)
+    a0 = -(P @ x_tgt)
+    return dict(id=f"random_qp(n={n},m={m},instance={instance})", a0=a0, r0=0.0, P=P, A=A,
+                r=np.zeros(m), ub=ub, Aeq=None, beq=None, x0=np.zeros(n))
+
+
+def _positivity(n: int):
+    """Constraints.allCoordinatesPositive (Constraints.scala:26-69): -x_j <= 0, j = 0..n-1."""
+    return -np.eye(n), np.zeros(n), np.zeros(n)
+
+
+def _sum_to_one(n: int):
+    """Constraints.sumToOne (Constraints.scala:75-80)."""
+    return np.ones((1, n)), np.ones(1)
+
+
+def joptP2() -> Dict:
+    """SimpleOptimizationProblems.scala:384-414 — min x'Px (P=[[1,.4],[.4,1]]) on the simplex; x*=(1/2,1/2)."""
+    A, r, ub = _positivity(2)
+    Aeq, beq = _sum_to_one(2)
+    return dict(id="example_1.5", a0=np.zeros(2), r0=0.0, P=np.array([[1.0, 0.4], [0.4, 1.0]]), A=A, r=r,
+                ub=ub, Aeq=Aeq, beq=beq, x_where_defined=np.full(2, 2.0), x_opt=np.array([0.5, 0.5]))
+
+
+def rank_one_problem_simplex(dim: int) -> Dict:
+    """SimpleOptimizationProblems.scala:221-255 — f = x'(aa')x/2 form via QuadraticObjectiveFunction(P=aa'),
+    a = linspace(1,2,dim), x >= 0, sum x = 1; x* = e_1."""
+    a = np.linspace(1.0, 2.0, dim)
+    A, r, ub = _positivity(dim)
+    Aeq, beq = _sum_to_one(dim)
+    x_opt = np.zeros(dim)
+    x_opt[0] = 1.0
+    return dict(id="Simplicial rankOneProblem", a0=np.zeros(dim), r0=0.0, P=np.outer(a, a), A=A, r=r, ub=ub,
+                Aeq=Aeq, beq=beq, x_where_defined=np.full(dim, 1.0 / dim), x_opt=x_opt)
+
+
+def probability_simplex_problem(n: int) -> Dict:
+    """SimpleOptimizationProblems.scala:425-456 — f = 0.5 - 1'x + x'(11')x/2 on x >= 0; minimisers = simplex."""
+    A, r, ub = _positivity(n)
+    return dict(id="Probability_simplex_problem", a0=-np.ones(n), r0=0.5, P=np.ones((n, n)), A=A, r=r, ub=ub,
+                Aeq=None, beq=None, x_where_defined=np.full(n, 2.0), x_opt=np.full(n, 1.0 / n))
+
+
+def min_dot_product(a: np.ndarray) -> Dict:
+    """SimpleOptimizationProblems.scala:142-169 — min -a'x s.t. |x_j| <= |a_j|
+    (Constraints.absoluteValuesBoundedBy: +x_j <= |a_j| then -x_j <= |a_j|); x* = a."""
+    n = a.shape[0]
+    rows, ubs = [], []
+    for j in range(n):
+        e = np.zeros(n)
+        e[j] = 1.0
+        rows += [e, -e]
+        ubs += [abs(a[j]), abs(a[j])]
+    return dict(id="Min f(x)=a'x subject to |x_j|<=|a_j|", a0=-a, r0=0.0, P=None, A=np.array(rows),
+                r=np.zeros(2 * n), ub=np.array(ubs), Aeq=None, beq=None, x_where_defined=2.0 * a, x_opt=a.copy())
+
+
+def norm_squared_with_free_variables(dim: int) -> Dict:
+    """SimpleOptimizationProblems.scala:308-340 — 0.5||x||^2 s.t. x_0 <= -1; x* = (-1,0,...,0)."""
+    A = np.zeros((1, dim))
+    A[0, 0] = 1.0
+    x_opt = np.zeros(dim)
+    x_opt[0] = -1.0
+    return dict(id="normSquaredWithFreeVariables", a0=np.zeros(dim), r0=0.0, P=np.eye(dim), A=A, r=np.zeros(1),
+                ub=np.array([-1.0]), Aeq=None, beq=None, x_where_defined=np.ones(dim), x_opt=x_opt)
+
+
+def known_answer_zoo():
+    """The SimpleOptimizationProblems.standardProblems subset (:576-598) the linear engine covers."""
+    return [joptP2(), rank_one_problem_simplex(10), probability_simplex_problem(10),
+            min_dot_product(np.array([1.0, -2.0, 0.5, 3.0, -1.5])), norm_squared_with_free_variables(5)]
+
+
+def objective_value(spec: Dict, x: np.ndarray) -> float:
+    v = spec["r0"] + float(spec["a0"] @ x)
+    if spec.get("P") is not None:
+        v += float(x @ (spec["P"] @ x)) / 2
+    return v

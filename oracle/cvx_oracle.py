@@ -1,0 +1,738 @@
+"""CPU oracle for the barrier Newton-step path of spyqqqdia/cvx — TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product: only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import it.  The shipped path (``cvx_amd`` + ``libcvxg.so``)
+never calls into it and fails loudly when its HIP library is missing.
+
+What it is
+    A line-by-line numpy/scipy restatement of the reference's hot path (Scala 2.11 + Breeze 0.10):
+
+    * barrier value / gradient / Hessian fold ........ BarrierSolver.scala:280-315
+    * objective + linear constraint callbacks ......... QuadraticObjectiveFunction.scala:31-33,
+                                                        LinearObjectiveFunction.scala:19-21,
+                                                        LinearConstraint.scala:22-32
+    * strict feasibility (C.isInSet) .................. Constraint.scala:23, ConstraintSet.scala:32-40,
+                                                        ConvexSet.scala:63-72
+    * Ruiz equilibration ............................. MatrixUtils.scala:240-268
+    * regularized Cholesky ............................ MatrixUtils.scala:452-461 (+ Breeze `cholesky`)
+    * forward / back substitution ..................... MatrixUtils.scala:383-430
+    * triangularSolve (LAPACK dtrtrs) ................. MatrixUtils.scala:362-376
+    * relativeSize / choleskySolve .................... MatrixUtils.scala:437-442, 468-516
+    * symSolve / diagonalizationSolve (fallback) ...... MatrixUtils.scala:603-707, 734-751
+    * KKTSystem.solve chain ........................... KKTSystem.scala:43-66, 99-246, 253-310
+    * UnconstrainedSolver.solve (all quirks) .......... UnconstrainedSolver.scala:34-125
+    * EqualityConstrainedSolver.solve ................. EqualityConstrainedSolver.scala:37-107
+    * barrier t-loop .................................. BarrierSolver.scala:70-177 with
+                                                        CvxUtils.scala:61-87, SolverParams.scala:35-46
+    * phase-I feasibility (linear constraints) ........ ConstraintSet.scala:123-168, 326-395, 556-575,
+                                                        Constraint.scala:64-89, EqualityConstraint.scala:84-100
+
+Third-party arithmetic the reference reaches but does not vendor: Breeze 0.10 (`cholesky` = symmetry
+check + LAPACK dpotrf('L'); `eigSym` = LAPACK dsyevr), netlib-java 1.1.2 `LAPACK.dtrtrs`.  They are
+restated through scipy's LAPACK (the same routines; OpenBLAS 0.3.29 here), `numpy.linalg.eigh`
+(dsyevd: same eigen-decomposition, possibly different eigenvector signs — the solve is invariant).
+
+Pinning
+    The reference cannot be compiled or run here (no JVM/sbt), and its tests hold no
+    golden vectors.  This oracle is pinned by the reference's own KNOWN-ANSWER tests, replayed in
+    ``tests/test_oracle_known_answers.py``: the analytic minimisers of
+    SimpleOptimizationProblems.scala (joptP2, rankOneProblemSimplex, probabilitySimplexProblem,
+    minDotProduct, normSquaredWithFreeVariables), the known-solution KKT systems of KktTest.scala:117-272,
+    the LA known-solution tests of MatrixUtilsTests.scala:16-198 and the KL analytic optimum of
+    OptimizationProblems.scala:136-141.  Per-Newton-step golden vectors (``tests/golden/``) are outputs
+    of THIS restatement on seeded inputs (script: ``tests/golden/make_golden.py``).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Tuple
+
+import numpy as np
+from scipy.linalg import lapack
+
+# ----------------------------------------------------------------------------------------------
+# Exceptions mirroring the reference's failure modes
+# ----------------------------------------------------------------------------------------------
+
+
+class LinSolveException(Exception):
+    """LinSolveException.scala (thrown by choleskySolve / solveWithCholFactor residual checks)."""
+
+
+class NotConvergedException(Exception):
+    """breeze.linalg.NotConvergedException (dpotrf info>0, line-search failures)."""
+
+
+class UnsolvableSystemException(Exception):
+    """UnsolvableSystemException.scala (diagonalizationSolve)."""
+
+
+class NotStrictlyFeasible(ValueError):
+    """IllegalArgumentException thrown by the barrier oracles when d_i <= 0 (BarrierSolver.scala:284)."""
+
+
+# ----------------------------------------------------------------------------------------------
+# Parameters  (SolverParams.scala:24-46)
+# ----------------------------------------------------------------------------------------------
+
+
+@dataclass
+class SolverParams:
+    maxIter: int = 1000
+    alpha: float = 0.04
+    beta: float = 0.8
+    tolSolver: float = 1e-8
+    tolEqSolve: float = 1e-1
+    tolFeas: float = 1e-7
+    delta: float = 1e-6
+
+
+def standard_params() -> SolverParams:
+    return SolverParams()
+
+
+# ----------------------------------------------------------------------------------------------
+# Problem model (packing of the reference's callback objects)
+# ----------------------------------------------------------------------------------------------
+
+
+@dataclass
+class Problem:
+    """Quadratic (P given) or linear (P None) objective r0 + a0.x (+ x'Px/2) with linear
+    inequalities r_i + a_i.x <= ub_i (rows of A in constraint LIST order) and optional Aeq x = beq.
+    """
+
+    a0: np.ndarray
+    r0: float = 0.0
+    P: Optional[np.ndarray] = None
+    A: np.ndarray = None  # m x n, row i = a_i
+    r: np.ndarray = None
+    ub: np.ndarray = None
+    Aeq: Optional[np.ndarray] = None
+    beq: Optional[np.ndarray] = None
+
+    @property
+    def n(self) -> int:
+        return self.a0.shape[0]
+
+    @property
+    def m(self) -> int:
+        return self.A.shape[0]
+
+
+def objective_value(pb: Problem, x: np.ndarray) -> float:
+    """QuadraticObjectiveFunction.scala:31 — r + (a dot x) + (x dot (P*x))/2;
+    LinearObjectiveFunction.scala:19 — r + (a dot x)."""
+    v = pb.r0 + float(np.dot(pb.a0, x))
+    if pb.P is not None:
+        v = v + float(np.dot(x, pb.P @ x)) / 2
+    return v
+
+
+def objective_gradient(pb: Problem, x: np.ndarray) -> np.ndarray:
+    """QuadraticObjectiveFunction.scala:32 — a + P*x; LinearObjectiveFunction.scala:20 — a."""
+    if pb.P is None:
+        return pb.a0.copy()
+    return pb.a0 + pb.P @ x
+
+
+def objective_hessian(pb: Problem) -> np.ndarray:
+    """QuadraticObjectiveFunction.scala:33 — P; LinearObjectiveFunction.scala:21 — zeros(n,n)."""
+    if pb.P is None:
+        return np.zeros((pb.n, pb.n))
+    return pb.P
+
+
+def constraint_value(pb: Problem, i: int, x: np.ndarray) -> float:
+    """LinearConstraint.scala:22-24 — r + (a dot x)."""
+    return pb.r[i] + float(np.dot(pb.A[i], x))
+
+
+def is_satisfied_strictly(pb: Problem, i: int, x: np.ndarray) -> bool:
+    """Constraint.scala:23 — valueAt(x)*(1+3e-16) < ub."""
+    return constraint_value(pb, i, x) * (1 + 3e-16) < pb.ub[i]
+
+
+def is_in_set(pb: Problem, x: np.ndarray) -> bool:
+    """ConstraintSet.scala:34-38 via ConvexSet.scala:69 — short-circuit forall in list order."""
+    for i in range(pb.m):
+        if not is_satisfied_strictly(pb, i, x):
+            return False
+    return True
+
+
+def active_set(pb: Problem, x: np.ndarray, tol: float = 1e-12) -> np.ndarray:
+    """Constraint.scala:26 isActive — |g_i(x) - ub_i| < tol (never called by the reference)."""
+    g = pb.r + pb.A @ x
+    return np.nonzero(np.abs(g - pb.ub) < tol)[0]
+
+
+# ----------------------------------------------------------------------------------------------
+# Barrier oracles (BarrierSolver.scala:280-315): left folds over the constraint list
+# ----------------------------------------------------------------------------------------------
+
+
+def barrier_value(pb: Problem, t: float, x: np.ndarray) -> float:
+    """BarrierSolver.scala:280-289."""
+    s = t * objective_value(pb, x)
+    for i in range(pb.m):
+        d = pb.ub[i] - constraint_value(pb, i, x)
+        if d <= 0:
+            raise NotStrictlyFeasible(f"barrierFunction: x not strictly feasible, d = {d}")
+        s = s - math.log(d)
+    return s
+
+
+def barrier_gradient(pb: Problem, t: float, x: np.ndarray) -> np.ndarray:
+    """BarrierSolver.scala:291-301 — fold starts at objF.gradientAt(x)*t, adds G/d."""
+    s = objective_gradient(pb, x) * t
+    for i in range(pb.m):
+        d = pb.ub[i] - constraint_value(pb, i, x)
+        if d <= 0:
+            raise NotStrictlyFeasible(f"gradientBarrierFunction: x not strictly feasible, d = {d}")
+        s = s + pb.A[i] / d
+    return s
+
+
+def barrier_hessian(pb: Problem, t: float, x: np.ndarray, literal: bool = True) -> np.ndarray:
+    """BarrierSolver.scala:303-315 — fold starts at objF.hessianAt(x)*t and adds
+    GGt/(d*d) + H/d per constraint, H = LinearConstraint.hessianAt = zeros(n,n) (LinearConstraint.scala:30-32).
+
+    ``literal=True`` keeps every temporary of the reference (G*G.t, /(d*d), zeros, /d, two sums) —
+    that is the CPU-baseline cost model.  ``literal=False`` drops only the +zeros/d term, which adds
+    exact zeros (bit-identical result for d > 0).
+    """
+    n = pb.n
+    s = objective_hessian(pb) * t
+    for i in range(pb.m):
+        d = pb.ub[i] - constraint_value(pb, i, x)
+        if d <= 0:
+            raise NotStrictlyFeasible(f"hessianBarrierFunction: x not strictly feasible, d = {d}")
+        G = pb.A[i]
+        GGt = np.outer(G, G)
+        if literal:
+            Hc = np.zeros((n, n))
+            s = s + GGt / (d * d) + Hc / d
+        else:
+            s = s + GGt / (d * d)
+    return s
+
+
+# ----------------------------------------------------------------------------------------------
+# Dense linear algebra (MatrixUtils.scala)
+# ----------------------------------------------------------------------------------------------
+
+
+def ruiz_equilibrate(H: np.ndarray) -> Tuple[np.ndarray, np.ndarray, int]:
+    """MatrixUtils.scala:240-268. Jacobi-style: every row of one sweep uses the Q computed at the top
+    of the sweep; rho measured before the update; <=20 sweeps or rho<=1e-6; zero row -> scale 1.
+    Returns (d, Q=(dd')oH, sweeps)."""
+    n = H.shape[0]
+    d = np.ones(n)
+    rho = 1.0
+    itermax = 20
+    it = 0
+    while it < itermax and rho > 1e-6:
+        Q = np.outer(d, d) * H
+        rho = 0.0
+        for i in range(n):
+            u = math.sqrt(float(np.linalg.norm(Q[i, :])))
+            v = 1.0 / u if u > 0 else 1.0
+            d[i] *= v
+            r = abs(1 - u)
+            if r > rho:
+                rho = r
+        it += 1
+    return d, np.outer(d, d) * H, it
+
+
+def _require_symmetric(X: np.ndarray, tol: float = 1e-7) -> None:
+    """Breeze 0.10 requireSymmetricMatrix (un-vendored): |X_ij - X_ji| <= |X_ij|*tol."""
+    diff = np.abs(X - X.T)
+    if np.any(diff > np.abs(X) * tol):
+        raise ValueError("MatrixNotSymmetricException")
+
+
+def cholesky(X: np.ndarray) -> np.ndarray:
+    """Breeze 0.10 `cholesky`: symmetry check, lowerTriangular copy, LAPACK dpotrf('L');
+    info>0 -> NotConvergedException."""
+    _require_symmetric(X)
+    L, info = lapack.dpotrf(np.tril(X), lower=1, clean=1)
+    if info > 0:
+        raise NotConvergedException("dpotrf: not positive definite")
+    return np.tril(L)
+
+
+def regularized_cholesky(Q: np.ndarray) -> Tuple[np.ndarray, int]:
+    """MatrixUtils.scala:452-461. Returns (L, regularized) where regularized = 1 when Q+1e-10*I was used."""
+    Qd = Q + np.eye(Q.shape[0]) * 1e-10
+    reg = 0
+    try:
+        C = cholesky(Q)
+    except (NotConvergedException, ValueError):
+        C = cholesky(Qd)
+        reg = 1
+    minD = float(np.min(np.diag(C)))
+    if minD > 1e-7:
+        return C, reg
+    return cholesky(Qd), 1
+
+
+def forward_solve(L: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """MatrixUtils.scala:383-403 — x_i = (b_i - sum_{j<i} L_ij x_j)/L_ii, j ascending."""
+    n = L.shape[0]
+    assert all(abs(L[i, i]) > 0 for i in range(n)), "Singular lower triangular matrix L"
+    x = np.zeros(n)
+    for i in range(n):
+        s = 0.0
+        row = L[i]
+        for j in range(i):
+            s += row[j] * x[j]
+        x[i] = (b[i] - s) / L[i, i]
+    return x
+
+
+def back_solve(U: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """MatrixUtils.scala:410-430 — x_i = (b_i - sum_{j>i} U_ij x_j)/U_ii, j descending."""
+    n = U.shape[0]
+    assert all(abs(U[i, i]) > 0 for i in range(n)), "Singular upper triangular matrix U"
+    x = np.zeros(n)
+    for i in range(n - 1, -1, -1):
+        s = 0.0
+        row = U[i]
+        for j in range(n - 1, i, -1):
+            s += row[j] * x[j]
+        x[i] = (b[i] - s) / U[i, i]
+    return x
+
+
+def triangular_solve(A: np.ndarray, ltype: str, B: np.ndarray) -> np.ndarray:
+    """MatrixUtils.scala:362-376 — LAPACK dtrtrs(Ltype,'N','N') on the triangular copy."""
+    assert ltype in ("L", "U")
+    Q = np.tril(A) if ltype == "L" else np.triu(A)
+    X, info = lapack.dtrtrs(Q, np.asarray(B, dtype=np.float64), lower=1 if ltype == "L" else 0,
+                            trans=0, unitdiag=0)
+    return X
+
+
+def relative_size(a: np.ndarray, b: np.ndarray, tol: float) -> float:
+    """MatrixUtils.scala:437-442."""
+    norm_b = float(np.linalg.norm(b))
+    f = tol if norm_b < tol else tol + norm_b
+    return float(np.linalg.norm(a)) / f
+
+
+@dataclass
+class CholSolveInfo:
+    d_ruiz: np.ndarray = None
+    ruiz_sweeps: int = 0
+    diagL: np.ndarray = None
+    regularized: int = 0
+    rel_err: float = float("nan")
+
+
+def cholesky_solve(H: np.ndarray, b: np.ndarray, tol: float,
+                   info: Optional[CholSolveInfo] = None, fast_subst: bool = False) -> np.ndarray:
+    """MatrixUtils.scala:468-516: Ruiz -> regularizedCholesky -> w = fwd(L, d*b) -> u = back(L', w)
+    -> x = d*u; LinSolveException when relativeSize(Hx-b, b, tol) > tol.
+    ``fast_subst`` replaces the scalar substitutions by dtrtrs (same math, LAPACK order) for the
+    large-size CPU baseline."""
+    d, Q, sweeps = ruiz_equilibrate(H)
+    L, reg = regularized_cholesky(Q)
+    if fast_subst:
+        w = triangular_solve(L, "L", (d * b)[:, None])[:, 0]
+        u = triangular_solve(L.T, "U", w[:, None])[:, 0]
+    else:
+        w = forward_solve(L, d * b)
+        u = back_solve(L.T, w)
+    x = d * u
+    rel = relative_size(H @ x - b, b, tol)
+    if info is not None:
+        info.d_ruiz, info.ruiz_sweeps, info.diagL, info.regularized, info.rel_err = (
+            d, sweeps, np.diag(L).copy(), reg, rel)
+    if rel > tol:
+        raise LinSolveException(f"choleskySolve: ||Hx-b||/||b|| = {rel}")
+    return x
+
+
+def diagonalization_solve(A, U, dvals, V, b, tol) -> np.ndarray:
+    """MatrixUtils.scala:603-707. Quirk: the regularisation loop shadows relError, so once the plain
+    solution misses tol the routine always ends in UnsolvableSystemException."""
+    n = U.shape[0]
+    nz = np.abs(dvals) > 0
+    a = np.where(nz, U.T @ b, 0.0)
+    b0 = U @ a
+    relDist = relative_size(b - b0, b, tol)
+    if relDist > tol:
+        raise UnsolvableSystemException(f"min_x||Ax-b||/||b|| = {relDist} > tol")
+    z = np.where(nz, (U.T @ b) / np.where(nz, dvals, 1.0), 0.0)
+    w = V @ z
+    relError = relative_size(A @ w - b, b, tol)
+    if relError > tol:
+        raise UnsolvableSystemException("system not solvable within tolerance")
+    return w
+
+
+def sym_solve(A: np.ndarray, b: np.ndarray, tol: float) -> np.ndarray:
+    """MatrixUtils.scala:734-751 — eigSym then diagonalizationSolve."""
+    lam, evs = np.linalg.eigh(A)
+    return diagonalization_solve(A, evs, lam, evs, b, tol)
+
+
+# ----------------------------------------------------------------------------------------------
+# KKT system (KKTSystem.scala)
+# ----------------------------------------------------------------------------------------------
+
+
+def kkt_solve_with_chol_factor(L, A, q, b, tol):
+    """KKTSystem.scala:99-167."""
+    n = L.shape[1]
+    p = A.shape[0]
+    B = np.zeros((n, p + 1))
+    B[:, :p] = A.T
+    B[:, p] = q
+    Y = triangular_solve(L, "L", B)
+    X = triangular_solve(L.T, "U", Y)
+    Hinv_At = X[:, :p]
+    Hinv_q = X[:, p]
+    R = A @ Hinv_At
+    S = (R + R.T) * 0.5
+    K = cholesky(S)
+    z = -(b + A @ Hinv_q)
+    u = forward_solve(K, z)
+    w = back_solve(K.T, u)
+    x = -(Hinv_q + Hinv_At @ w)
+    Ltx = L.T @ x
+    Hx = L @ Ltx
+    residual_1 = Hx + A.T @ w + q
+    err1 = relative_size(residual_1, -q, tol)
+    residual_2 = A @ x - b
+    err2 = relative_size(residual_2, b, tol)
+    if err1 > tol or err2 > tol:
+        raise LinSolveException("Error in solution exceeds tolerance.")
+    return x, w
+
+
+def kkt_block_solve(H, A, q, b, tol):
+    """KKTSystem.scala:178-190."""
+    L, _ = regularized_cholesky(H)
+    return kkt_solve_with_chol_factor(L, A, q, b, tol)
+
+
+def kkt_solve_pd(H, A, q, b, tol):
+    """KKTSystem.scala:200-246 — Ruiz, B = A diag(d), Dq = d*q, blockSolve, x = d*y."""
+    d, Q, _ = ruiz_equilibrate(H)
+    B = A * d[None, :]
+    Dq = d * q
+    y, w = kkt_block_solve(Q, B, Dq, b, tol)
+    return d * y, w
+
+
+def kkt_matrix(H, A):
+    """KKTSystem.scala:253-260."""
+    p = A.shape[0]
+    return np.block([[H, A.T], [A, np.zeros((p, p))]])
+
+
+def kkt_sym_solve(H, A, g, r, tol):
+    """KKTSystem.scala:283-310."""
+    n = H.shape[0]
+    rhs = np.concatenate([-g, r])
+    w = sym_solve(kkt_matrix(H, A), rhs, tol)
+    return w[:n], w[n:]
+
+
+def kkt_solve(H, A, q, b, tol, info: Optional[dict] = None):
+    """KKTSystem.scala:43-66 — solvePD(H) -> solvePD(H+A'A, q-A'b) -> kktSymSolve."""
+    try:
+        res = kkt_solve_pd(H, A, q, b, tol)
+        if info is not None:
+            info["fallback"] = 0
+        return res
+    except Exception:
+        try:
+            K = H + A.T @ A
+            z = q - A.T @ b
+            res = kkt_solve_pd(K, A, z, b, tol)
+            if info is not None:
+                info["fallback"] = 1
+            return res
+        except Exception:
+            res = kkt_sym_solve(H, A, q, b, tol)
+            if info is not None:
+                info["fallback"] = 2
+            return res
+
+
+# ----------------------------------------------------------------------------------------------
+# Inner Newton solvers
+# ----------------------------------------------------------------------------------------------
+
+
+@dataclass
+class NewtonStepRecord:
+    """One inner Newton iteration as the GPU engine reports it (cvxg_step_info)."""
+
+    x: np.ndarray
+    grad: np.ndarray
+    f: float
+    dx: np.ndarray
+    q: float
+    newton_decrement: float
+    step: float = float("nan")
+    backtracks_c: int = 0
+    backtracks_armijo: int = 0
+    fallback: int = 0
+    ruiz_sweeps: int = 0
+    regularized: int = 0
+    rel_err: float = float("nan")
+    d_ruiz: Optional[np.ndarray] = None
+    diagL: Optional[np.ndarray] = None
+
+
+@dataclass
+class Solution:
+    """Solution.scala:32-43 (subset used by the barrier path)."""
+
+    x: np.ndarray
+    newtonDecrement: Optional[float] = None
+    dualityGap: Optional[float] = None
+    equalityGap: Optional[float] = None
+    normGrad: Optional[float] = None
+    iter: int = 0
+    maxedOut: bool = False
+    newton_steps: int = 0  # instrumentation: total inner Newton steps (the reference only keeps the last count)
+    records: List[NewtonStepRecord] = field(default_factory=list)
+
+
+def newton_direction(pb: Problem, t: float, x: np.ndarray, y: np.ndarray, tolEqSolve: float,
+                     rec: Optional[NewtonStepRecord] = None, fast_subst: bool = False) -> np.ndarray:
+    """UnconstrainedSolver.scala:50-67 — H at x, choleskySolve(H,-y) -> choleskySolve(H+1e-9 I,-y) -> symSolve."""
+    H = barrier_hessian(pb, t, x, literal=False)
+    info = CholSolveInfo()
+    fb = 0
+    try:
+        d = cholesky_solve(H, -y, tolEqSolve, info, fast_subst)
+    except Exception:
+        try:
+            fb = 1
+            M = H + np.eye(H.shape[0]) * 1e-9
+            d = cholesky_solve(M, -y, tolEqSolve, info, fast_subst)
+        except Exception:
+            fb = 2
+            d = sym_solve(H, -y, tolEqSolve)
+    if rec is not None:
+        rec.fallback, rec.ruiz_sweeps, rec.regularized, rec.rel_err = fb, info.ruiz_sweeps, info.regularized, info.rel_err
+        rec.d_ruiz, rec.diagL = info.d_ruiz, info.diagL
+    return d
+
+
+def unconstrained_solve(pb: Problem, t: float, x0: np.ndarray, pars: SolverParams,
+                        record: bool = False, max_steps: Optional[int] = None) -> Solution:
+    """UnconstrainedSolver.scala:34-125 with objF = the barrier objective at parameter t.
+
+    Quirks reproduced: rho = 1+1/4 == 1 (integer), so the trust radius stays
+    at |d_0|_H; steps longer than it are scaled; Armijo uses the UNSCALED q; both backtracking loops
+    share `it` (bound 200) and only throw at it == 100; t *= beta repeatedly."""
+    maxIter, alpha, beta, tol, tolEq = pars.maxIter, pars.alpha, pars.beta, pars.tolSolver, pars.tolEqSolve
+    it_n = 0
+    newtonDecrement = tol + 1
+    x = x0.copy()
+    y = barrier_gradient(pb, t, x)
+    normGrad = float(np.linalg.norm(y))
+    trustRadius = float("nan")
+    records = []
+    while it_n < maxIter and newtonDecrement > tol and normGrad > tol:
+        if max_steps is not None and it_n >= max_steps:
+            break
+        f = barrier_value(pb, t, x)
+        rec = NewtonStepRecord(x=x.copy(), grad=y.copy(), f=f, dx=None, q=0.0, newton_decrement=0.0)
+        d = newton_direction(pb, t, x, y, tolEq, rec)
+        q = float(np.dot(d, y))
+        newtonDecrement = -q / 2
+        rec.dx, rec.q, rec.newton_decrement = d.copy(), q, newtonDecrement
+        if newtonDecrement > tol:
+            hNorm_d = math.sqrt(-q)
+            if it_n == 0:
+                trustRadius = hNorm_d
+            s = d if (it_n == 0 or hNorm_d <= trustRadius) else d * (trustRadius / hNorm_d)
+            it = 0
+            st = 1.0
+            while (not is_in_set(pb, x + s * st)) and it < 200:
+                st *= beta
+                it += 1
+            if it == 100:
+                raise NotConvergedException("Line search: backtracking into the set C failed.")
+            k1 = it
+            # trust-radius update: rho == 1 so both branches are no-ops (the f_new evaluation has no
+            # observable effect when x+s is in C, and is skipped).
+            while barrier_value(pb, t, x + s * st) > f + alpha * st * q and it < 200:
+                st *= beta
+                it += 1
+            if it == 100:
+                raise NotConvergedException("Line search: sufficient decrease not reached")
+            x = x + s * st
+            y = barrier_gradient(pb, t, x)
+            normGrad = float(np.linalg.norm(y))
+            rec.step, rec.backtracks_c, rec.backtracks_armijo = st, k1, it - k1
+        it_n += 1
+        if record:
+            records.append(rec)
+    return Solution(x=x, newtonDecrement=newtonDecrement, normGrad=normGrad, iter=it_n,
+                    maxedOut=it_n >= maxIter, newton_steps=it_n, records=records)
+
+
+def equality_constrained_solve(pb: Problem, t: float, x0: np.ndarray, pars: SolverParams,
+                               record: bool = False) -> Solution:
+    """EqualityConstrainedSolver.scala:37-107 — KKT Newton step, no trust region, shared `it`
+    bound 100 that throws at it == 100."""
+    A, b = pb.Aeq, pb.beq
+    maxIter, alpha, beta, tol, tolEq = pars.maxIter, pars.alpha, pars.beta, pars.tolSolver, pars.tolEqSolve
+    it_n = 0
+    newtonDecrement = tol + 1
+    x = x0.copy()
+    y = barrier_gradient(pb, t, x)
+    normGrad = float(np.linalg.norm(y))
+    eqDiff = b - A @ x
+    records = []
+    while it_n < maxIter and ((newtonDecrement > tol and normGrad > tol) or float(np.linalg.norm(eqDiff)) > tol):
+        f = barrier_value(pb, t, x)
+        H = barrier_hessian(pb, t, x, literal=False)
+        info = {}
+        d, _w = kkt_solve(H, A, y, eqDiff, tolEq, info)
+        q = float(np.dot(d, y))
+        newtonDecrement = -q / 2
+        rec = NewtonStepRecord(x=x.copy(), grad=y.copy(), f=f, dx=d.copy(), q=q,
+                               newton_decrement=newtonDecrement, fallback=info.get("fallback", 0))
+        if newtonDecrement > tol:
+            it = 0
+            st = 1.0
+            while (not is_in_set(pb, x + d * st)) and it < 100:
+                st *= beta
+                it += 1
+            if it == 100:
+                raise NotConvergedException("Line search: backtracking into the set C failed.")
+            k1 = it
+            while barrier_value(pb, t, x + d * st) > f + alpha * st * q and it < 100:
+                st *= beta
+                it += 1
+            if it == 100:
+                raise NotConvergedException("Line search: sufficient decrease not reached")
+            x = x + d * st
+            y = barrier_gradient(pb, t, x)
+            normGrad = float(np.linalg.norm(y))
+            eqDiff = b - A @ x
+            rec.step, rec.backtracks_c, rec.backtracks_armijo = st, k1, it - k1
+        it_n += 1
+        if record:
+            records.append(rec)
+    return Solution(x=x, newtonDecrement=newtonDecrement, equalityGap=float(np.linalg.norm(eqDiff)),
+                    normGrad=normGrad, iter=it_n, maxedOut=it_n >= maxIter, newton_steps=it_n,
+                    records=records)
+
+
+# ----------------------------------------------------------------------------------------------
+# Barrier t-loop (BarrierSolver.scala:70-177)
+# ----------------------------------------------------------------------------------------------
+
+
+def standard_termination(pars: SolverParams) -> Callable[[dict], bool]:
+    """CvxUtils.scala:61-70."""
+    def tc(state):
+        return state["dualityGap"] < pars.tolSolver and (
+            state.get("equalityGap") is None or state["equalityGap"] < pars.tolSolver)
+    return tc
+
+
+def phase_I_termination(state) -> bool:
+    """CvxUtils.scala:78-87."""
+    return state["objectiveFunctionValue"] < 0 and (
+        state.get("equalityGap") is None or state["equalityGap"] < 1e-6)
+
+
+def barrier_solve(pb: Problem, x0: np.ndarray, pars: SolverParams,
+                  tc: Optional[Callable[[dict], bool]] = None, record: bool = False) -> Solution:
+    """BarrierSolver.scala:70-117 (no equalities) and :124-177 (with equalities)."""
+    if tc is None:
+        tc = standard_termination(pars)
+    withEqs = pb.Aeq is not None
+    mu = 10.0
+    t = 1.0
+    x = x0.copy()
+    state = {"dualityGap": float("inf"), "equalityGap": float("inf") if withEqs else None,
+             "objectiveFunctionValue": float("inf")}
+    sol = None
+    maxIter = 1000 / mu
+    it = 0
+    total = 0
+    records: List[NewtonStepRecord] = []
+    gaps = []
+    while not tc(state) and it < maxIter:
+        if withEqs:
+            sol = equality_constrained_solve(pb, t, x, pars, record)
+        else:
+            sol = unconstrained_solve(pb, t, x, pars, record)
+        total += sol.newton_steps
+        for r_ in sol.records:
+            r_.t = t
+        records.extend(sol.records)
+        x = sol.x
+        f = objective_value(pb, x)
+        gap = pb.m / t
+        state = {"dualityGap": gap, "equalityGap": sol.equalityGap if withEqs else 0.0,
+                 "objectiveFunctionValue": f}
+        gaps.append(gap)
+        t = mu * t
+        it += 1
+    return Solution(x=sol.x, newtonDecrement=sol.newtonDecrement, dualityGap=state["dualityGap"],
+                    equalityGap=state["equalityGap"], normGrad=sol.normGrad, iter=sol.iter,
+                    maxedOut=sol.maxedOut, newton_steps=total, records=records)
+
+
+# ----------------------------------------------------------------------------------------------
+# Phase I (basic method, linear constraints) — ConstraintSet.scala:123-168, 326-395
+# ----------------------------------------------------------------------------------------------
+
+
+def phase_I_problem(pb: Problem, x_where_defined: np.ndarray) -> Tuple[Problem, np.ndarray]:
+    """phase_I_ObjectiveFunction (f(x,s)=s) + phase_I_Constraints_noEqs (g_j(x)-s <= ub_j) with the
+    feasible point (x0, 1 + max_j(g_j(x0)-ub_j)) (ConstraintSet.scala:129-168; Constraint.scala:64-89)."""
+    n, m = pb.n, pb.m
+    A1 = np.hstack([pb.A, -np.ones((m, 1))])
+    a0 = np.zeros(n + 1)
+    a0[n] = 1.0
+    y0 = max(constraint_value(pb, j, x_where_defined) - pb.ub[j] for j in range(m))
+    fp = np.concatenate([x_where_defined, [1 + y0]])
+    return Problem(a0=a0, r0=0.0, P=None, A=A1, r=pb.r.copy(), ub=pb.ub.copy()), fp
+
+
+def phase_I_analysis(pb: Problem, x_where_defined: np.ndarray, pars: SolverParams):
+    """phase_I_Analysis (ConstraintSet.scala:404-413): with equalities the equalities are turned into
+    +-1e-6 inequalities (:326-347, EqualityConstraint.scala:84-100), then :355-395.
+    Returns (x_feas, s_feas)."""
+    if pb.Aeq is not None:
+        tolEqs = 1e-6
+        rowsA, rowsr, rowsub = [pb.A], [pb.r], [pb.ub]
+        for i in range(pb.Aeq.shape[0]):
+            rowsA.append(pb.Aeq[i:i + 1]); rowsr.append(np.zeros(1)); rowsub.append(np.array([pb.beq[i] + tolEqs]))
+            rowsA.append(-pb.Aeq[i:i + 1]); rowsr.append(np.zeros(1)); rowsub.append(np.array([-pb.beq[i] + tolEqs]))
+        base = Problem(a0=pb.a0, A=np.vstack(rowsA), r=np.concatenate(rowsr), ub=np.concatenate(rowsub))
+    else:
+        base = Problem(a0=pb.a0, A=pb.A, r=pb.r, ub=pb.ub)
+    p1, fp = phase_I_problem(base, x_where_defined)
+    sol = barrier_solve(p1, fp, pars, tc=phase_I_termination)
+    n = pb.n
+    return sol.x[:n], float(sol.x[n])
+
+
+def with_feasible_point(pb: Problem, x_where_defined: np.ndarray, pars: SolverParams) -> np.ndarray:
+    """ConstraintSet.withFeasiblePoint (:556-575): phase I, then a strictly feasible x0."""
+    x_feas, s_feas = phase_I_analysis(pb, x_where_defined, pars)
+    tol = pars.tolSolver
+    # FeasibilityReport.isFeasible(tol): s < tol (FeasibilityReport.scala)
+    if not s_feas < tol:
+        raise ValueError(f"InfeasibleProblemException: s = {s_feas}")
+    if not is_in_set(pb, x_feas):
+        raise ValueError("phase I point not strictly feasible")
+    return x_feas
