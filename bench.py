@@ -1,0 +1,191 @@
+"""Benchmark: Newton KKT solves/s of the MI355X barrier engine on the C3 random dense QP (n=4096, m=8192).
+
+One "step" = one full inner Newton iteration of the barrier method on device-resident data: barrier
+gradient (2 GEMV passes over A), Hessian assembly H = tP + A'diag(1/d^2)A (FP64 MFMA SYRK), Ruiz
+equilibration, regularised blocked Cholesky with the fused forward solve, backward solve, residual check,
+the backtracking line search and the iterate update (UnconstrainedSolver.scala:47-134).  The t-loop
+(BarrierSolver.scala:70-117) advances t *= 10 when a centering terminates, as the reference does.
+
+N > 1: one process per GPU, an independent instance per rank (config C5, seed 20261015 + rank), no
+collective inside the timed region except the bracketing barrier; value = total steps / max-rank time;
+one gather of the per-rank results to rank 0 afterwards.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Newton KKT solves/sec at n=4096 m=8192; % MFMA roofline on trailing SYRK"
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix peak (spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def cpu_baseline(spec, seconds_budget: float = 20.0):
+    """Reference-faithful CPU port timed on this host (oracle/cvx_oracle.py = restatement of the Breeze path):
+    the per-constraint rank-1 Hessian fold of BarrierSolver.scala:303-315 with all of its n x n temporaries,
+    timed on a bounded sample of constraints and scaled to m, plus one Ruiz + regularizedCholesky +
+    substitution solve (MatrixUtils.scala:240-516) at full n, plus m dot products per line-search trial."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import cvx_oracle as O
+    n, m = spec["A"].shape[1], spec["A"].shape[0]
+    pb = O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"])
+    x = spec["x0"]
+    with threadpool_limits(1):
+        # (1) fold sample
+        k = 0
+        s = spec["P"] * 1.0
+        t0 = time.perf_counter()
+        budget_fold = 0.5 * seconds_budget
+        while k < m and (time.perf_counter() - t0) < budget_fold:
+            d = pb.ub[k] - O.constraint_value(pb, k, x)
+            G = pb.A[k]
+            s = s + np.outer(G, G) / (d * d) + np.zeros((n, n)) / d
+            k += 1
+        t_fold = (time.perf_counter() - t0) / k * m
+        # (2) equilibrate + factor + solve at full size
+        dd = spec["ub"] - spec["A"] @ x
+        H = spec["P"] + spec["A"].T @ (spec["A"] / (dd * dd)[:, None])
+        y = O.barrier_gradient(pb, 1.0, x)
+        t1 = time.perf_counter()
+        O.cholesky_solve(H, -y, 0.1, fast_subst=True)
+        t_solve = time.perf_counter() - t1
+        # (3) one barrier value + feasibility sweep per line-search trial (m dots of length n)
+        t2 = time.perf_counter()
+        for i in range(min(m, 2048)):
+            O.constraint_value(pb, i, x)
+        t_trial = (time.perf_counter() - t2) / min(m, 2048) * m * 2
+    t_step = t_fold + t_solve + t_trial
+    return {"value": 1.0 / t_step, "unit": "Newton KKT solves/s", "cores": 1, "kind": "port",
+            "sample": (f"reference-faithful numpy port (oracle/cvx_oracle.py), 1 thread: rank-1 Hessian fold "
+                       f"timed on {k} of {m} constraints and scaled to m ({t_fold:.1f} s/Hessian), Ruiz+"
+                       f"regularizedCholesky+dtrtrs solve at n={n} ({t_solve:.2f} s), 2 trial sweeps "
+                       f"({t_trial:.2f} s); projected {t_step:.1f} s per Newton step")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    import torch
+
+    from cvx_amd import dist as D
+    from cvx_amd import problems as Z
+    from cvx_amd.api import SolverParams
+    from cvx_amd.engine import Engine
+
+    rank, local_rank, world = D.env_rank()
+    if world > 1:
+        D.init("nccl")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    n, m = args.n, args.m
+    spec = Z.random_qp(n, m, instance=rank)
+    pars = SolverParams.standardParams()
+
+    eng = Engine(n, m, 0, device=local_rank)
+    eng.load_problem(spec)
+    eng.set_x(spec["x0"])
+    state = {"t": 1.0}
+    eng.centering_begin(1.0)
+
+    def one_step():
+        st = eng.newton_step(pars)
+        if st.done:
+            if m / state["t"] < pars.tolSolver:  # barrier finished: restart the path from x0
+                eng.set_x(spec["x0"])
+                state["t"] = 1.0
+            else:
+                state["t"] *= 10.0
+            eng.centering_begin(state["t"])
+        return st
+
+    for _ in range(args.warmup):
+        one_step()
+    eng.set_timing(True)
+    syrk_ms, chol_ms, solve_ms, ruiz_ms, ls_ms = [], [], [], [], []
+    D.barrier(device)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = one_step()
+        ph = eng.phase_times()
+        syrk_ms.append(ph[5])
+        ruiz_ms.append(ph[1])
+        chol_ms.append(ph[2])
+        solve_ms.append(ph[3])
+        ls_ms.append(ph[4])
+    torch.cuda.synchronize()
+    D.barrier(device)
+    elapsed = time.perf_counter() - t0
+    elapsed = D.max_over_ranks(elapsed, device)
+    eng.set_timing(False)
+
+    x_final = eng.get_x()
+    stats = np.array([rank, args.steps, elapsed, state["t"]], dtype=np.float64)
+    gathered = D.gather_results(x_final, stats, device)
+
+    if rank == 0:
+        total_steps = args.steps * world
+        value = total_steps / elapsed
+        syrk = float(np.mean(syrk_ms))
+        flops_syrk = float(m) * n * (n + 1)  # lower triangle incl. diagonal
+        ach = flops_syrk / (syrk * 1e-3) / 1e12
+        chol = float(np.mean(chol_ms))
+        kkt_ms = float(np.mean(ruiz_ms)) + chol + float(np.mean(solve_ms))
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "Newton KKT solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded random dense QP, SURVEY.md §8d generator)",
+            "config": {"workload": f"C3: random dense QP n={n} m={m}, full barrier Newton iterations "
+                                   "(assembly + Ruiz + Cholesky + solves + line search) on one MI355X per rank",
+                       "n": n, "m": m,
+                       "parallelism": f"replicas x{world}: one independent QP per GPU (config C5), "
+                                      "RCCL gather of results after the timed region"},
+            "roofline": {"bound": "mfma", "kernel": "k_syrk_assemble (H = tP + A'diag(w)A)",
+                         "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                         "flops_per_launch": flops_syrk, "avg_launch_ms": syrk},
+            "phases_ms": {"syrk": syrk, "ruiz": float(np.mean(ruiz_ms)), "cholesky_fused_fwd": chol,
+                          "bwd_solve_residual": float(np.mean(solve_ms)), "line_search": float(np.mean(ls_ms))},
+            "kkt_factor_solve_per_s": 1e3 / kkt_ms,
+            "cholesky_tflops": (n ** 3 / 3) / (chol * 1e-3) / 1e12,
+            "gathered_ranks": len(gathered),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(spec, args.cpu_budget)
+        elif not args.no_cpu_baseline:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

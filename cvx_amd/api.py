@@ -1,0 +1,335 @@
+"""Host-side mirror of the reference's problem-model API for the barrier path.
+
+Same names, argument meaning and error behaviour as spyqqqdia/cvx, so a caller (and the parity tests)
+read like the reference:
+
+* ObjectiveFunction family ........ ObjectiveFunction.scala:8-14, QuadraticObjectiveFunction.scala:7-33,
+                                    LinearObjectiveFunction.scala:7-21
+* LinearConstraint ................ LinearConstraint.scala:7-32 (+ Constraint.scala:22-28 predicates)
+* ConstraintSet / FeasiblePoint ... ConstraintSet.scala:8-120, 556-638; FeasiblePoint.scala:6-9
+* EqualityConstraint .............. EqualityConstraint.scala:16-27, 84-100
+* SolverParams / Solution ......... SolverParams.scala:24-46, Solution.scala:32-43
+* BarrierSolver.apply ............. BarrierSolver.scala:269-317 — returns a GpuBarrierSolver whose inner
+                                    loop runs on the MI355X engine (libcvxg.so) behind the C-ABI
+* OptimizationProblem ............. OptimizationProblem.scala:133-196 (solverType "BR" = this engine)
+
+Eligibility: quadratic or linear objective, linear inequality constraints, optional
+EqualityConstraint with at most CVXG_MAX_EQ rows.  Anything else raises TypeError — the reference's
+CPU BarrierSolver remains the path for general callbacks.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .engine import CvxgError, Engine, NotStrictlyFeasible
+
+# ------------------------------------------------------------------------------------------------
+
+
+@dataclass
+class SolverParams:
+    maxIter: int
+    alpha: float
+    beta: float
+    tolSolver: float
+    tolEqSolve: float
+    tolFeas: float
+    delta: float
+
+    @staticmethod
+    def standardParams() -> "SolverParams":
+        return SolverParams(1000, 0.04, 0.8, 1e-8, 1e-1, 1e-7, 1e-6)
+
+
+@dataclass
+class Solution:
+    x: np.ndarray
+    newtonDecrement: Optional[float]
+    dualityGap: Optional[float]
+    equalityGap: Optional[float]
+    normGrad: Optional[float]
+    iter: int
+    maxedOut: bool
+    newtonSteps: int = 0
+    outerIters: int = 0
+
+
+class ObjectiveFunction:
+    def __init__(self, dim: int):
+        self.dim = dim
+
+    def valueAt(self, x):
+        raise NotImplementedError
+
+    def gradientAt(self, x):
+        raise NotImplementedError
+
+    def hessianAt(self, x):
+        raise NotImplementedError
+
+
+class QuadraticObjectiveFunction(ObjectiveFunction):
+    """f(x) = r + x'a + (1/2) x'Px."""
+
+    def __init__(self, dim: int, r: float, a, P):
+        super().__init__(dim)
+        a = np.asarray(a, dtype=np.float64)
+        P = np.asarray(P, dtype=np.float64)
+        if a.shape != (dim,):
+            raise ValueError(f"Vector a must be of dimension {dim} but length(a) {a.shape[0]}")
+        if P.shape != (dim, dim):
+            raise ValueError(f"Matrix P must be square of dimension {dim} but is {P.shape[0]}x{P.shape[1]}")
+        self.r, self.a, self.P = float(r), a, P
+
+    def valueAt(self, x):
+        return self.r + float(self.a @ x) + float(x @ (self.P @ x)) / 2
+
+    def gradientAt(self, x):
+        return self.a + self.P @ x
+
+    def hessianAt(self, x):
+        return self.P
+
+
+class LinearObjectiveFunction(ObjectiveFunction):
+    """f(x) = r + a'x."""
+
+    def __init__(self, dim: int, r: float, a):
+        super().__init__(dim)
+        a = np.asarray(a, dtype=np.float64)
+        if a.shape != (dim,):
+            raise ValueError(f"Vector a must be of dimension {dim} but length(a) {a.shape[0]}")
+        self.r, self.a = float(r), a
+
+    def valueAt(self, x):
+        return self.r + float(self.a @ x)
+
+    def gradientAt(self, x):
+        return self.a
+
+    def hessianAt(self, x):
+        return np.zeros((self.dim, self.dim))
+
+
+class LinearConstraint:
+    """Affine inequality r + a'x <= ub (LinearConstraint.scala:7-32)."""
+
+    def __init__(self, id: str, dim: int, ub: float, r: float, a):
+        a = np.asarray(a, dtype=np.float64)
+        if a.shape != (dim,):
+            raise ValueError(f"Vector a must be of dimension {dim} but length(a) {a.shape[0]}")
+        self.id, self.dim, self.ub, self.r, self.a = id, dim, float(ub), float(r), a
+
+    def valueAt(self, x):
+        return self.r + float(self.a @ x)
+
+    def gradientAt(self, x):
+        return self.a
+
+    def hessianAt(self, x):
+        return np.zeros((self.dim, self.dim))
+
+    def isSatisfied(self, x):
+        return self.valueAt(x) <= self.ub
+
+    def isSatisfiedStrictly(self, x):
+        return self.valueAt(x) * (1 + 3e-16) < self.ub
+
+    def isActive(self, x, tol: float = 1e-12):
+        return abs(self.valueAt(x) - self.ub) < tol
+
+    def margin(self, x):
+        return self.ub - self.valueAt(x)
+
+
+class EqualityConstraint:
+    """Ax = b with A p x n, p < n (EqualityConstraint.scala:16-27)."""
+
+    def __init__(self, A, b):
+        A = np.atleast_2d(np.asarray(A, dtype=np.float64))
+        b = np.asarray(b, dtype=np.float64).reshape(-1)
+        assert A.shape[0] < A.shape[1], f"m=A.rows={A.shape[0]} is not less than n=A.cols={A.shape[1]}"
+        assert A.shape[0] == b.shape[0], f"m=A.rows={A.shape[0]} != b.length = {b.shape[0]}"
+        self.A, self.b, self.dim = A, b, A.shape[1]
+
+    def errorAt(self, x):
+        return float(np.linalg.norm(self.A @ x - self.b))
+
+    def asInequalities(self, tol: float) -> List[LinearConstraint]:
+        """EqualityConstraint.scala:84-100."""
+        out = []
+        for i in range(self.A.shape[0]):
+            out.append(LinearConstraint(f"row_{i}(A)'x <= {self.b[i]}", self.dim, self.b[i] + tol, 0.0, self.A[i]))
+            out.append(LinearConstraint(f"row_{i}(A)'x >= {self.b[i]}", self.dim, -self.b[i] + tol, 0.0, -self.A[i]))
+        return out
+
+
+class ConstraintSet:
+    """ConstraintSet(dim, constraints) (ConstraintSet.scala:8); only LinearConstraint members are eligible."""
+
+    def __init__(self, dim: int, constraints: Sequence[LinearConstraint], pointWhereDefined=None):
+        assert all(c.dim == dim for c in constraints)
+        self.dim = dim
+        self.constraints = list(constraints)
+        self.pointWhereDefined = (np.zeros(dim) if pointWhereDefined is None
+                                  else np.asarray(pointWhereDefined, dtype=np.float64))
+        self.feasiblePoint = None
+
+    @property
+    def numConstraints(self):
+        return len(self.constraints)
+
+    def packed(self):
+        """(A, r, ub) with A row i = a_i in LIST order (fold and forall order)."""
+        m = len(self.constraints)
+        A = np.zeros((m, self.dim))
+        r = np.zeros(m)
+        ub = np.zeros(m)
+        for i, c in enumerate(self.constraints):
+            if not isinstance(c, LinearConstraint):
+                raise TypeError("GPU barrier engine supports LinearConstraint only")
+            A[i], r[i], ub[i] = c.a, c.r, c.ub
+        return A, r, ub
+
+    def isSatisfiedStrictlyBy(self, x) -> bool:
+        return all(c.isSatisfiedStrictly(x) for c in self.constraints)
+
+    def constraintFunctionAt(self, x):
+        return np.array([c.valueAt(x) - c.ub for c in self.constraints])
+
+    def addFeasiblePoint(self, x0) -> "ConstraintSet":
+        """ConstraintSet.scala:43-54."""
+        x0 = np.asarray(x0, dtype=np.float64)
+        assert x0.shape[0] == self.dim, "Feasible point does not have the right dimension"
+        assert self.isSatisfiedStrictlyBy(x0)
+        cs = ConstraintSet(self.dim, self.constraints, x0)
+        cs.feasiblePoint = x0
+        return cs
+
+    # --- phase I on the same engine (ConstraintSet.scala:123-168, 326-395, 556-575) ------------------
+    def phase_I_Analysis(self, eqs: Optional[EqualityConstraint], pars: SolverParams):
+        cnts = list(self.constraints)
+        if eqs is not None:
+            cnts = cnts + eqs.asInequalities(1e-6)  # phase_I_Analysis_withEqs (:326-347)
+        A, r, ub = ConstraintSet(self.dim, cnts).packed()
+        m, n = A.shape
+        x0 = self.pointWhereDefined
+        A1 = np.hstack([A, -np.ones((m, 1))])                 # g_j(x) - s <= ub_j  (Constraint.scala:64-89)
+        a0 = np.zeros(n + 1)
+        a0[n] = 1.0                                            # f(x,s) = s        (:129-140)
+        y0 = max(float(r[j] + A[j] @ x0) - ub[j] for j in range(m))
+        fp = np.concatenate([x0, [1 + y0]])                    # feasible point    (:161-164)
+        eng = Engine(n + 1, m, 0)
+        try:
+            eng.set_objective(a0, 0.0, None)
+            eng.set_ineq(A1, r, ub)
+            eng.set_x(fp)
+            eng.barrier_solve(pars, termination=1)             # phase_I_TerminationCriterion
+            w = eng.get_x()
+        finally:
+            eng.close()
+        return w[:n], float(w[n])
+
+    def withFeasiblePoint(self, eqs: Optional[EqualityConstraint], pars: SolverParams) -> "ConstraintSet":
+        """ConstraintSet.scala:556-575."""
+        if self.feasiblePoint is not None:
+            return self
+        x_feas, s_feas = self.phase_I_Analysis(eqs, pars)
+        if not s_feas < pars.tolSolver:  # FeasibilityReport.isFeasible
+            raise ValueError(f"InfeasibleProblemException: phase I ended with s = {s_feas}")
+        return self.addFeasiblePoint(x_feas)
+
+
+# ------------------------------------------------------------------------------------------------
+
+
+class GpuBarrierSolver:
+    """BarrierSolver with the inner Newton loop on the MI355X engine (BarrierSolver.scala:22-49, 269-317)."""
+
+    def __init__(self, objF: ObjectiveFunction, cnts: ConstraintSet, eqs: Optional[EqualityConstraint],
+                 pars: SolverParams, device: int = 0):
+        if not isinstance(objF, (QuadraticObjectiveFunction, LinearObjectiveFunction)):
+            raise TypeError("GPU barrier engine: objective must be Quadratic- or LinearObjectiveFunction")
+        if cnts.feasiblePoint is None:
+            raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
+        p = 0 if eqs is None else eqs.A.shape[0]
+        if p > _lib.CVXG_MAX_EQ:
+            raise TypeError(f"GPU barrier engine: at most {_lib.CVXG_MAX_EQ} equality rows")
+        self.objF, self.cnts, self.eqs, self.pars = objF, cnts, eqs, pars
+        self.dim = cnts.dim
+        self.startingPoint = cnts.feasiblePoint
+        A, r, ub = cnts.packed()
+        self.engine = Engine(cnts.dim, A.shape[0], p, device)
+        self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
+        self.engine.set_ineq(A, r, ub)
+        if p:
+            self.engine.set_eq(eqs.A, eqs.b)
+
+    @property
+    def numConstraints(self):
+        return self.cnts.numConstraints
+
+    def barrierFunction(self, t, x):
+        return self.engine.barrier_eval(t, x, want_grad=False)[0]
+
+    def gradientBarrierFunction(self, t, x):
+        return self.engine.barrier_eval(t, x, want_grad=True)[1]
+
+    def hessianBarrierFunction(self, t, x):
+        return self.engine.barrier_eval(t, x, want_grad=False, want_hess=True)[2]
+
+    def solveSpecial(self, termination: int = 0) -> Solution:
+        self.engine.set_x(self.startingPoint)
+        s = self.engine.barrier_solve(self.pars, termination)
+        return Solution(self.engine.get_x(), s.newton_decrement, s.duality_gap,
+                        s.equality_gap if self.eqs is not None else 0.0, s.norm_grad, s.iter, bool(s.maxed_out),
+                        s.newton_steps, s.outer_iters)
+
+    def solve(self, debugLevel: int = 0) -> Solution:
+        return self.solveSpecial(0)
+
+
+class BarrierSolver:
+    @staticmethod
+    def apply(objF, cnts, eqs, pars, device: int = 0) -> GpuBarrierSolver:
+        return GpuBarrierSolver(objF, cnts, eqs, pars, device)
+
+
+class OptimizationProblem:
+    def __init__(self, id: str, objectiveFunction, solver):
+        self.id, self.objectiveFunction, self.solver = id, objectiveFunction, solver
+
+    def solve(self, debugLevel: int = 0) -> Solution:
+        return self.solver.solve(debugLevel)
+
+    @staticmethod
+    def apply(id, objF, ineqs: ConstraintSet, eqs, solverType: str, pars, device: int = 0):
+        """OptimizationProblem.scala:133-157 (solverType "BR")."""
+        if solverType not in ("BR", "GPU"):
+            raise ValueError(f"Unknown solverType = {solverType}")
+        return OptimizationProblem(id, objF, BarrierSolver.apply(objF, ineqs, eqs, pars, device))
+
+    @staticmethod
+    def withoutFeasiblePoint(id, objF, ineqs: ConstraintSet, eqs, solverType: str, pars, device: int = 0):
+        """OptimizationProblem.scala:174-196: phase I, then the barrier solver."""
+        return OptimizationProblem.apply(id, objF, ineqs.withFeasiblePoint(eqs, pars), eqs, solverType, pars, device)
+
+
+def problem_from_spec(spec: dict):
+    """(objF, ConstraintSet, EqualityConstraint|None) from a cvx_amd.problems spec dict."""
+    n = spec["a0"].shape[0]
+    objF = (QuadraticObjectiveFunction(n, spec["r0"], spec["a0"], spec["P"]) if spec.get("P") is not None
+            else LinearObjectiveFunction(n, spec["r0"], spec["a0"]))
+    cnts = [LinearConstraint(f"LinCnt{i}", n, spec["ub"][i], spec["r"][i], spec["A"][i]) for i in range(spec["A"].shape[0])]
+    cs = ConstraintSet(n, cnts, spec.get("x_where_defined", spec.get("x0")))
+    eqs = EqualityConstraint(spec["Aeq"], spec["beq"]) if spec.get("Aeq") is not None else None
+    return objF, cs, eqs
+
+
+__all__ = ["SolverParams", "Solution", "ObjectiveFunction", "QuadraticObjectiveFunction", "LinearObjectiveFunction",
+           "LinearConstraint", "EqualityConstraint", "ConstraintSet", "GpuBarrierSolver", "BarrierSolver",
+           "OptimizationProblem", "problem_from_spec", "CvxgError", "NotStrictlyFeasible"]

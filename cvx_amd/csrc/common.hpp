@@ -1,0 +1,84 @@
+// common.hpp — shared device helpers and the device-side control block of the barrier engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cvxg {
+
+constexpr int NB = 64;        // Cholesky / triangular-solve block (row-major lower L)
+constexpr int TILE = 128;     // MFMA SYRK output tile
+constexpr int KC = 16;        // SYRK contraction chunk staged per LDS buffer
+constexpr int MPAD = 64;      // inequality rows padded to a multiple of this
+constexpr int LS_TRIALS = 64; // backtracking trials evaluated per line-search batch
+constexpr int MAX_RHS = 9;    // 1 + CVXG_MAX_EQ right-hand sides in the fused forward solve
+constexpr int RUIZ_MAX = 20;  // MatrixUtils.scala:247
+
+// Device control block: every scalar the graph-captured kernels need lives here, so launches can be
+// replayed with fixed arguments.  A pinned host mirror is read back once per Newton step.
+struct DevCtrl {
+  double t;                       // barrier parameter of the current centering
+  double reg;                     // diagonal shift added when forming Q (0 or 1e-10), MatrixUtils.scala:454
+  int infeasible;                 // # rows with d_i <= 0 at the last constraint evaluation
+  int not_strict;                 // # rows failing g_i*(1+3e-16) < ub_i
+  int chol_info;                  // 1-based global pivot index of the first non-positive pivot, 0 = ok
+  int ruiz_sweeps;                // Ruiz sweeps executed
+  unsigned long long min_diag;    // bits of min diag(L) (positive doubles order like uint64)
+  unsigned long long ruiz_rho[RUIZ_MAX + 2];
+  double sc[32];                  // reduced scalars, see SC_* below
+};
+
+enum {
+  SC_A0X = 0,   // a0 . x
+  SC_XPX,       // x . P x
+  SC_SUMLOG,    // sum_i log d_i
+  SC_GG,        // |grad|^2
+  SC_Q,         // dx . grad
+  SC_RES2,      // |H dx + grad|^2
+  SC_A0S,       // a0 . s
+  SC_SPX,       // s . P x
+  SC_SPS,       // s . P s
+  SC_EQ2,       // |b - Aeq x|^2
+  SC_RES2B,     // second KKT residual |A x - b|^2
+  SC_B2,        // |b|^2 (KKT)
+  SC_COUNT
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Deterministic block sum (fixed tree) for blockDim.x a multiple of 64, <= 1024.
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < nw; ++i) s += red[i];
+    red[0] = s;
+  }
+  __syncthreads();
+  s = red[0];
+  __syncthreads();
+  return s;
+}
+
+__device__ __forceinline__ void atomic_max_pos(unsigned long long* p, double v) {
+  // v >= 0: IEEE ordering of non-negative doubles equals unsigned ordering of their bits.
+  atomicMax(p, (unsigned long long)__double_as_longlong(v));
+}
+__device__ __forceinline__ void atomic_min_pos(unsigned long long* p, double v) {
+  atomicMin(p, (unsigned long long)__double_as_longlong(v));
+}
+
+}  // namespace cvxg

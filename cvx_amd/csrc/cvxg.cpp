@@ -1,0 +1,937 @@
+// cvxg.cpp — C-ABI (include/cvxg.h) and host orchestration of the MI355X barrier Newton engine.
+//
+// Host side keeps only scalar control flow that the reference evaluates sequentially: the t-loop
+// (BarrierSolver.scala:70-177), the inner Newton loop and its fallback chains
+// (UnconstrainedSolver.scala:34-125, EqualityConstrainedSolver.scala:37-107, KKTSystem.scala:43-66,
+// MatrixUtils.scala:452-516) and the backtracking decisions (UnconstrainedSolver.scala:83-113), read
+// from one small device->host copy per decision point.  All vector/matrix work is HIP (k_*.hip).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/cvxg.h"
+#include "kernels.hpp"
+
+using namespace cvxg;
+
+namespace {
+
+constexpr int NT = 8;  // phase timers
+
+struct Timer {
+  hipEvent_t ev[NT][2];
+  bool on = false;
+  double ms[NT] = {0};
+};
+
+}  // namespace
+
+struct cvxg_ctx {
+  int dev = 0, n = 0, m = 0, p = 0, np = 0, mp = 0, nblk = 0;
+  hipStream_t s = nullptr;
+  // problem
+  double* P = nullptr;
+  int hasP = 0;
+  double* a0 = nullptr;
+  double r0 = 0.0;
+  double *A = nullptr, *r = nullptr, *ub = nullptr;
+  double *Aeq = nullptr, *beq = nullptr;
+  int have_obj = 0, have_ineq = 0, have_eq = 0;
+  // iterate and vectors
+  double *x = nullptr, *y = nullptr, *dx = nullptr, *sdir = nullptr, *xtmp = nullptr, *vtmp = nullptr;
+  double *Px = nullptr, *Ps = nullptr, *e = nullptr;
+  double *c = nullptr, *d = nullptr, *invd = nullptr, *w = nullptr, *logd = nullptr;
+  double *eqd = nullptr, *eqtmp = nullptr;  // b - Aeq x
+  // matrices
+  double *H = nullptr, *L = nullptr, *Linv = nullptr, *Hsave = nullptr;
+  double *ruiz0 = nullptr, *ruiz1 = nullptr, *dfin = nullptr, *hdiag = nullptr;
+  double *rhs = nullptr, *sol = nullptr;
+  double* part = nullptr;
+  size_t part_bytes = 0;
+  double *kB = nullptr, *kw = nullptr, *kx = nullptr, *kz = nullptr;
+  double *ls_plog = nullptr, *ls_log = nullptr;
+  int *ls_pcnt = nullptr, *ls_cnt = nullptr;
+  int* tiles = nullptr;
+  int ntiles = 0, nsplit = 1;
+  DevCtrl* ctrl = nullptr;
+  DevCtrl* hctrl = nullptr;
+  double* hls = nullptr;  // pinned: [LS_TRIALS] logs then [2*LS_TRIALS] counts as ints
+  // centering state
+  double t = 1.0;
+  int iter = 0;
+  double trust = NAN;
+  int began = 0;
+  double nd = 0.0;        // newton decrement
+  double normGrad = 0.0;
+  double eqGap = 0.0;
+  double f_at_x = 0.0;    // barrier value at x
+  int x_eval_valid = 0;   // c/d/w/y/scalars correspond to the current x and t
+  Timer tm;
+  std::string err;
+};
+
+// ------------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------------
+static int set_err(cvxg_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return code;
+}
+
+#define HIPC(ctx, call)                                                                              \
+  do {                                                                                               \
+    hipError_t _e = (call);                                                                          \
+    if (_e != hipSuccess) return set_err(ctx, CVXG_E_HIP, "%s failed: %s (%s:%d)", #call,           \
+                                         hipGetErrorString(_e), __FILE__, __LINE__);                  \
+  } while (0)
+
+#define CHK(call)              \
+  do {                         \
+    int _rc = (call);          \
+    if (_rc != CVXG_OK) return _rc; \
+  } while (0)
+
+static inline int round_up(int v, int a) { return (v + a - 1) / a * a; }
+
+template <class T>
+static int dalloc(cvxg_ctx* ctx, T** p, size_t count) {
+  HIPC(ctx, hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T)));
+  HIPC(ctx, hipMemsetAsync(*p, 0, std::max<size_t>(count, 1) * sizeof(T), ctx->s));
+  return CVXG_OK;
+}
+
+static void tstart(cvxg_ctx* ctx, int i) {
+  if (ctx->tm.on) (void)hipEventRecord(ctx->tm.ev[i][0], ctx->s);
+}
+static void tstop(cvxg_ctx* ctx, int i) {
+  if (ctx->tm.on) (void)hipEventRecord(ctx->tm.ev[i][1], ctx->s);
+}
+
+static int sync_ctrl(cvxg_ctx* ctx) {
+  HIPC(ctx, hipMemcpyAsync(ctx->hctrl, ctx->ctrl, sizeof(DevCtrl), hipMemcpyDeviceToHost, ctx->s));
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  return CVXG_OK;
+}
+
+// Upload an n-vector into a zero-padded device vector of length np.
+static int upload_vec(cvxg_ctx* ctx, double* dst, const double* src, int n, int np) {
+  std::vector<double> h(np, 0.0);
+  memcpy(h.data(), src, sizeof(double) * n);
+  HIPC(ctx, hipMemcpyAsync(dst, h.data(), sizeof(double) * np, hipMemcpyHostToDevice, ctx->s));
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  return CVXG_OK;
+}
+
+// Pack a (rows x cols) matrix with leading dimension ld (row- or column-major) into a device row-major
+// buffer of (rows_pad x ldd), zero padded.
+static int upload_mat(cvxg_ctx* ctx, double* dst, int ldd, int rows_pad, const double* src, int rows, int cols,
+                      int ld, int row_major) {
+  std::vector<double> h((size_t)rows_pad * ldd, 0.0);
+  for (int i = 0; i < rows; ++i)
+    for (int j = 0; j < cols; ++j)
+      h[(size_t)i * ldd + j] = row_major ? src[(size_t)i * ld + j] : src[(size_t)j * ld + i];
+  HIPC(ctx, hipMemcpyAsync(dst, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, ctx->s));
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  return CVXG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Device pipeline pieces
+// ------------------------------------------------------------------------------------------------
+
+// Barrier value / gradient pieces at the current x and ctrl->t (BarrierSolver.scala:280-301):
+// c, d, w, invd, logd, Px, y, eqDiff, and sc[A0X, XPX, SUMLOG, GG, EQ2].
+static int eval_at_x(cvxg_ctx* ctx) {
+  hipStream_t s = ctx->s;
+  const int np = ctx->np, mp = ctx->mp;
+  launch_ctrl_reset_eval(s, ctx->ctrl);
+  launch_constraint_eval(s, ctx->A, np, mp, np, ctx->x, ctx->r, ctx->ub, ctx->c, ctx->d, ctx->invd, ctx->w,
+                         ctx->logd, ctx->ctrl);
+  if (ctx->hasP) launch_rowdot(s, ctx->P, np, np, np, ctx->x, ctx->Px);
+  launch_coldot_partials(s, ctx->A, np, mp, np, ctx->invd, ctx->part);
+  launch_gradient_finalize(s, ctx->a0, ctx->hasP ? ctx->Px : nullptr, ctx->part, mp / 64, np, ctx->ctrl, ctx->y);
+  launch_dot(s, ctx->a0, ctx->x, np, ctx->ctrl, SC_A0X);
+  if (ctx->hasP) launch_dot(s, ctx->x, ctx->Px, np, ctx->ctrl, SC_XPX);
+  launch_sum(s, ctx->logd, mp, ctx->ctrl, SC_SUMLOG);
+  launch_dot(s, ctx->y, nullptr, np, ctx->ctrl, SC_GG);
+  if (ctx->p > 0) {
+    launch_rowdot(s, ctx->Aeq, np, ctx->p, np, ctx->x, ctx->eqtmp);
+    launch_axpy(s, ctx->beq, ctx->eqtmp, -1.0, ctx->p, ctx->eqd);  // b - A*x
+    launch_dot(s, ctx->eqd, nullptr, ctx->p, ctx->ctrl, SC_EQ2);
+  }
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  const DevCtrl& h = *ctx->hctrl;
+  const double f0 = ctx->r0 + h.sc[SC_A0X] + (ctx->hasP ? h.sc[SC_XPX] / 2 : 0.0);
+  ctx->f_at_x = ctx->t * f0 - h.sc[SC_SUMLOG];
+  ctx->normGrad = sqrt(h.sc[SC_GG]);
+  ctx->eqGap = ctx->p > 0 ? sqrt(h.sc[SC_EQ2]) : 0.0;
+  ctx->x_eval_valid = 1;
+  if (h.infeasible > 0)
+    return set_err(ctx, CVXG_E_INFEASIBLE_X, "barrier: x not strictly feasible (%d constraints with d <= 0)",
+                   h.infeasible);
+  return CVXG_OK;
+}
+
+static double objective_at_x(cvxg_ctx* ctx) {
+  const DevCtrl& h = *ctx->hctrl;
+  return ctx->r0 + h.sc[SC_A0X] + (ctx->hasP ? h.sc[SC_XPX] / 2 : 0.0);
+}
+
+static int assemble_hessian(cvxg_ctx* ctx) {
+  tstart(ctx, 5);
+  launch_syrk_assemble(ctx->s, ctx->A, ctx->np, ctx->w, ctx->mp, ctx->hasP ? ctx->P : nullptr, ctx->ctrl, ctx->H,
+                       ctx->np, TileList{ctx->tiles, ctx->ntiles}, ctx->nsplit, ctx->part);
+  tstop(ctx, 5);
+  HIPC(ctx, hipGetLastError());
+  return CVXG_OK;
+}
+
+// Ruiz equilibration of H into dfin (MatrixUtils.scala:240-268).
+static void ruiz(cvxg_ctx* ctx) {
+  hipStream_t s = ctx->s;
+  launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl);
+  for (int k = 0; k < RUIZ_MAX; ++k)
+    launch_ruiz_sweep(s, ctx->H, ctx->np, ctx->n, (k & 1) ? ctx->ruiz1 : ctx->ruiz0, (k & 1) ? ctx->ruiz0 : ctx->ruiz1,
+                      ctx->ctrl, k);
+  launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl);
+}
+
+// One factorisation attempt of Q = DHD (+reg I) with the fused forward solve of nrhs right-hand sides,
+// which `fill_rhs` writes into ctx->rhs first.  Returns chol_info / min_diag via hctrl.
+template <class F>
+static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs) {
+  hipStream_t s = ctx->s;
+  launch_ctrl_set(s, ctx->ctrl, 1, reg);
+  launch_ctrl_reset_chol(s, ctx->ctrl);
+  launch_form_q(s, ctx->H, ctx->L, ctx->np, ctx->n, ctx->np, ctx->dfin, ctx->ctrl);
+  fill_rhs();
+  for (int k = 0; k < ctx->nblk; ++k) {
+    launch_potrf_diag(s, ctx->L, ctx->np, k, ctx->rhs, nrhs, ctx->ctrl);
+    launch_trsm_panel(s, ctx->L, ctx->np, ctx->np, k, ctx->rhs, nrhs, ctx->ctrl);
+    launch_syrk_update(s, ctx->L, ctx->np, ctx->np, k * NB, ctx->ctrl);
+  }
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  return CVXG_OK;
+}
+
+static double min_diag_of(const DevCtrl& h) {
+  double v;
+  memcpy(&v, &h.min_diag, sizeof(v));
+  return v;
+}
+
+// regularizedCholesky (MatrixUtils.scala:452-461): chol(Q); on failure or min diag(L) <= 1e-7 use
+// chol(Q + 1e-10 I), whose failure propagates (CVXG_E_NOT_PD).
+template <class F>
+static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regularized, double* mind) {
+  CHK(factor_attempt(ctx, 0.0, nrhs, fill_rhs));
+  *regularized = 0;
+  if (ctx->hctrl->chol_info == 0 && min_diag_of(*ctx->hctrl) > 1e-7) {
+    *mind = min_diag_of(*ctx->hctrl);
+    return CVXG_OK;
+  }
+  CHK(factor_attempt(ctx, 1e-10, nrhs, fill_rhs));
+  *regularized = 1;
+  *mind = min_diag_of(*ctx->hctrl);
+  if (ctx->hctrl->chol_info != 0)
+    return set_err(ctx, CVXG_E_NOT_PD, "cholesky: matrix not positive definite (pivot %d)", ctx->hctrl->chol_info);
+  return CVXG_OK;
+}
+
+static void backward_solve(cvxg_ctx* ctx, int nrhs) {
+  launch_trtri_diag(ctx->s, ctx->L, ctx->np, ctx->nblk, ctx->Linv, ctx->ctrl);
+  for (int k = ctx->nblk - 1; k >= 0; --k)
+    launch_bwd_step(ctx->s, ctx->L, ctx->np, ctx->Linv, k, ctx->rhs, ctx->sol, nrhs, ctx->ctrl);
+}
+
+// MatrixUtils.choleskySolve(H, b = -grad, tol) (MatrixUtils.scala:468-516); result in ctx->dx.
+static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
+  hipStream_t s = ctx->s;
+  tstart(ctx, 1);
+  ruiz(ctx);
+  tstop(ctx, 1);
+  tstart(ctx, 2);
+  int reg = 0;
+  double mind = 0.0;
+  int rc = regularized_cholesky(
+      ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, ctx->y, -1.0, ctx->n, ctx->np, 1, 0, ctx->rhs); }, &reg, &mind);
+  tstop(ctx, 2);
+  info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
+  info->regularized = reg;
+  info->min_diag = mind;
+  if (rc != CVXG_OK) return rc;
+  tstart(ctx, 3);
+  backward_solve(ctx, 1);
+  launch_scale_vec(s, ctx->sol, ctx->dfin, ctx->np, ctx->dx);  // x = d :* u
+  // relativeSize(H*x - b, b, tol), b = -grad  (MatrixUtils.scala:437-442, 496)
+  launch_rowdot(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->dx, ctx->vtmp);
+  launch_axpy(s, ctx->vtmp, ctx->y, 1.0, ctx->n, ctx->vtmp);
+  launch_dot(s, ctx->vtmp, nullptr, ctx->n, ctx->ctrl, SC_RES2);
+  launch_dot(s, ctx->dx, ctx->y, ctx->np, ctx->ctrl, SC_Q);
+  tstop(ctx, 3);
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  const double nb = ctx->normGrad;
+  const double f = nb < tol ? tol : tol + nb;
+  const double rel = sqrt(ctx->hctrl->sc[SC_RES2]) / f;
+  info->rel_err = rel;
+  if (!(rel <= tol))
+    return set_err(ctx, CVXG_E_LINSOLVE_TOL, "choleskySolve: ||Hx-b||/||b|| = %.5g exceeds tolerance", rel);
+  return CVXG_OK;
+}
+
+// UnconstrainedSolver Newton direction with its fallback chain (UnconstrainedSolver.scala:54-67).
+static int newton_direction_p0(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
+  int rc = cholesky_solve(ctx, pars->tolEqSolve, info);
+  info->fallback = 0;
+  if (rc == CVXG_OK) return rc;
+  if (rc == CVXG_E_HIP) return rc;
+  // choleskySolve(H + 1e-9 I, -y)
+  launch_copy_diag(ctx->s, ctx->H, ctx->np, ctx->n, ctx->hdiag);
+  launch_add_diag(ctx->s, ctx->H, ctx->np, ctx->n, 1e-9);
+  rc = cholesky_solve(ctx, pars->tolEqSolve, info);
+  launch_set_diag(ctx->s, ctx->H, ctx->np, ctx->n, ctx->hdiag);
+  info->fallback = 1;
+  if (rc == CVXG_OK || rc == CVXG_E_HIP) return rc;
+  info->fallback = 2;
+  return set_err(ctx, CVXG_E_UNSOLVABLE,
+                 "symSolve fallback (eigen-decomposition, MatrixUtils.scala:734-751) reached: not in this build");
+}
+
+// KKTSystem.solvePD(Hm, Aeq, q, b) (KKTSystem.scala:200-246) with the block elimination of
+// solveWithCholFactor (:99-167); Hm = ctx->H, q = qv (device n-vector), b = bv (device p-vector).
+static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
+  hipStream_t s = ctx->s;
+  const int n = ctx->n, np = ctx->np, p = ctx->p, nr = p + 1;
+  tstart(ctx, 1);
+  ruiz(ctx);
+  tstop(ctx, 1);
+  tstart(ctx, 2);
+  int reg = 0;
+  double mind = 0.0;
+  int rc = regularized_cholesky(
+      ctx, nr,
+      [&]() {
+        launch_kkt_prep(s, ctx->Aeq, np, p, n, np, ctx->dfin, ctx->kB, ctx->rhs, nr);  // B = A diag(d), B'
+        launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, nr, p, ctx->rhs);            // D q
+      },
+      &reg, &mind);
+  tstop(ctx, 2);
+  info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
+  info->regularized = reg;
+  info->min_diag = mind;
+  if (rc != CVXG_OK) return rc;
+  tstart(ctx, 3);
+  backward_solve(ctx, nr);  // X = H^-1 [B' | Dq]
+  launch_ctrl_reset_chol(s, ctx->ctrl);
+  launch_kkt_schur(s, ctx->sol, nr, ctx->kB, np, p, np, bv, ctx->kw, ctx->kx, ctx->ctrl);
+  // residual_1 = Q y + B' w + Dq  with  Q y = d o (H (d o y)), relative to -Dq   (:148-150)
+  launch_scale_vec(s, ctx->kx, ctx->dfin, np, ctx->xtmp);
+  launch_rowdot(s, ctx->H, np, n, np, ctx->xtmp, ctx->vtmp);
+  launch_scale_vec(s, ctx->vtmp, ctx->dfin, n, ctx->vtmp);
+  launch_scale_strided(s, ctx->dfin, qv, 1, 0, n, ctx->kz);  // Dq
+  launch_btw_plus(s, ctx->kB, np, p, ctx->kw, ctx->kz, n, ctx->xtmp);
+  launch_axpy(s, ctx->vtmp, ctx->xtmp, 1.0, n, ctx->vtmp);
+  launch_dot(s, ctx->vtmp, nullptr, n, ctx->ctrl, SC_RES2);
+  launch_dot(s, ctx->kz, nullptr, n, ctx->ctrl, SC_Q);  // |Dq|^2 (temporarily)
+  // residual_2 = B y - b  (:152-153)
+  launch_rowdot(s, ctx->kB, np, p, np, ctx->kx, ctx->eqtmp);
+  launch_axpy(s, ctx->eqtmp, bv, -1.0, p, ctx->eqtmp);
+  launch_dot(s, ctx->eqtmp, nullptr, p, ctx->ctrl, SC_RES2B);
+  launch_dot(s, bv, nullptr, p, ctx->ctrl, SC_B2);
+  launch_scale_vec(s, ctx->kx, ctx->dfin, np, ctx->dx);  // x = D y  (:244)
+  tstop(ctx, 3);
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  if (ctx->hctrl->chol_info != 0) return set_err(ctx, CVXG_E_NOT_PD, "KKT Schur complement not positive definite");
+  auto relsize = [&](double na, double nb_) { return na / (nb_ < tol ? tol : tol + nb_); };
+  const double err1 = relsize(sqrt(ctx->hctrl->sc[SC_RES2]), sqrt(ctx->hctrl->sc[SC_Q]));
+  const double err2 = relsize(sqrt(ctx->hctrl->sc[SC_RES2B]), sqrt(ctx->hctrl->sc[SC_B2]));
+  info->rel_err = std::max(err1, err2);
+  if (err1 > tol || err2 > tol)
+    return set_err(ctx, CVXG_E_LINSOLVE_TOL, "KKT: Error in solution exceeds tolerance (%.3g, %.3g)", err1, err2);
+  return CVXG_OK;
+}
+
+// KKTSystem.solve (KKTSystem.scala:43-66): solvePD(H) -> solvePD(H + A'A, q - A'b) -> kktSymSolve.
+static int newton_direction_kkt(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
+  hipStream_t s = ctx->s;
+  int rc = kkt_solve_pd(ctx, ctx->y, ctx->eqd, pars->tolEqSolve, info);
+  info->fallback = 0;
+  if (rc == CVXG_OK || rc == CVXG_E_HIP) return rc;
+  const size_t bytes = (size_t)ctx->np * ctx->np * sizeof(double);
+  HIPC(ctx, hipMemcpyAsync(ctx->Hsave, ctx->H, bytes, hipMemcpyDeviceToDevice, s));
+  launch_add_ata(s, ctx->H, ctx->np, ctx->Aeq, ctx->p, ctx->n);
+  launch_q_minus_atb(s, ctx->y, ctx->Aeq, ctx->np, ctx->p, ctx->eqd, ctx->n, ctx->e);
+  rc = kkt_solve_pd(ctx, ctx->e, ctx->eqd, pars->tolEqSolve, info);
+  HIPC(ctx, hipMemcpyAsync(ctx->H, ctx->Hsave, bytes, hipMemcpyDeviceToDevice, s));
+  info->fallback = 1;
+  if (rc == CVXG_OK || rc == CVXG_E_HIP) {
+    if (rc == CVXG_OK) {  // q for the decrement uses the original gradient
+      launch_dot(s, ctx->dx, ctx->y, ctx->np, ctx->ctrl, SC_Q);
+      CHK(sync_ctrl(ctx));
+    }
+    return rc;
+  }
+  info->fallback = 2;
+  return set_err(ctx, CVXG_E_UNSOLVABLE, "kktSymSolve fallback (KKTSystem.scala:283-310) reached: not in this build");
+}
+
+static int newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
+  tstart(ctx, 0);
+  CHK(assemble_hessian(ctx));
+  tstop(ctx, 0);
+  int rc;
+  if (ctx->p == 0) {
+    rc = newton_direction_p0(ctx, pars, info);
+  } else {
+    rc = newton_direction_kkt(ctx, pars, info);
+    if (rc == CVXG_OK && info->fallback == 0) {
+      launch_dot(ctx->s, ctx->dx, ctx->y, ctx->np, ctx->ctrl, SC_Q);
+      CHK(sync_ctrl(ctx));
+    }
+  }
+  return rc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Line search (UnconstrainedSolver.scala:83-113 / EqualityConstrainedSolver.scala:78-97)
+// ------------------------------------------------------------------------------------------------
+struct TrialBatch {
+  int k0 = -1;
+  double logs[LS_TRIALS];
+  int viol[LS_TRIALS], npos[LS_TRIALS];
+};
+
+static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch* b) {
+  if (ctx->m == 0) {  // no inequality constraints: every trial is in C and contributes no log terms
+    b->k0 = k0;
+    for (int k = 0; k < LS_TRIALS; ++k) b->logs[k] = 0.0, b->viol[k] = 0, b->npos[k] = 0;
+    return CVXG_OK;
+  }
+  const int nb = ls_blocks(ctx->m);
+  launch_ls_trials(ctx->s, ctx->c, ctx->e, ctx->ub, ctx->m, tbase, beta, ctx->ls_plog, ctx->ls_pcnt);
+  launch_ls_finalize(ctx->s, ctx->ls_plog, ctx->ls_pcnt, nb, ctx->ls_log, ctx->ls_cnt);
+  HIPC(ctx, hipGetLastError());
+  HIPC(ctx, hipMemcpyAsync(ctx->hls, ctx->ls_log, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
+  HIPC(ctx, hipMemcpyAsync((int*)(ctx->hls + LS_TRIALS), ctx->ls_cnt, 2 * LS_TRIALS * sizeof(int),
+                           hipMemcpyDeviceToHost, ctx->s));
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  b->k0 = k0;
+  memcpy(b->logs, ctx->hls, sizeof(b->logs));
+  const int* cnt = (const int*)(ctx->hls + LS_TRIALS);
+  for (int k = 0; k < LS_TRIALS; ++k) {
+    b->viol[k] = cnt[2 * k];
+    b->npos[k] = cnt[2 * k + 1];
+  }
+  return CVXG_OK;
+}
+
+// Backtracking from x along s (device ctx->sdir).  limit = 200 / throw_at = 100 (Unconstrained) or
+// 100 / 100 (EqualityConstrained).  Returns the accepted t and the two counters.
+static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int limit, double* t_out, int* k_c,
+                       int* k_a) {
+  hipStream_t s = ctx->s;
+  const double beta = pars->beta, alpha = pars->alpha;
+  // e = A s, and the quadratic pieces of f0(x + s t)
+  launch_rowdot(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e);
+  launch_dot(s, ctx->a0, ctx->sdir, ctx->np, ctx->ctrl, SC_A0S);
+  if (ctx->hasP) {
+    launch_rowdot(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps);
+    launch_dot(s, ctx->sdir, ctx->Px, ctx->np, ctx->ctrl, SC_SPX);
+    launch_dot(s, ctx->sdir, ctx->Ps, ctx->np, ctx->ctrl, SC_SPS);
+  }
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  const DevCtrl h = *ctx->hctrl;
+  const double tb = ctx->t, f = ctx->f_at_x;
+  auto f0_at = [&](double tt) {  // r + a.(x+st) + (x+st)'P(x+st)/2
+    double v = ctx->r0 + (h.sc[SC_A0X] + tt * h.sc[SC_A0S]);
+    if (ctx->hasP) v += (h.sc[SC_XPX] + 2 * tt * h.sc[SC_SPX] + tt * tt * h.sc[SC_SPS]) / 2;
+    return v;
+  };
+  TrialBatch b;
+  double tcur = 1.0;
+  double tbatch = 1.0;  // t at the start of the next batch (products of beta, UnconstrainedSolver.scala:93)
+  int next_k0 = 0;
+  auto ensure = [&](int k) -> int {
+    while (!(b.k0 >= 0 && k >= b.k0 && k < b.k0 + LS_TRIALS)) {
+      CHK(ls_batch(ctx, next_k0, tbatch, beta, &b));
+      for (int i = 0; i < LS_TRIALS; ++i) tbatch *= beta;
+      next_k0 += LS_TRIALS;
+    }
+    return CVXG_OK;
+  };
+  int it = 0;
+  // while (!C.isInSet(x + s*t) && it < limit) { t *= beta; it += 1 }
+  while (true) {
+    if (it >= limit) break;
+    CHK(ensure(it));
+    if (b.viol[it - b.k0] == 0) break;
+    tcur *= beta;
+    ++it;
+  }
+  if (it == 100) return set_err(ctx, CVXG_E_LINESEARCH, "Line search: backtracking into the set C failed.");
+  *k_c = it;
+  // while (objF.valueAt(x + s*t) > f + alpha*t*q && it < limit) { t *= beta; it += 1 }
+  while (it < limit) {
+    CHK(ensure(it));
+    const int j = it - b.k0;
+    if (b.npos[j] > 0)
+      return set_err(ctx, CVXG_E_INFEASIBLE_X, "barrierFunction: x not strictly feasible in line search");
+    const double fv = tb * f0_at(tcur) - b.logs[j];
+    if (!(fv > f + alpha * tcur * q)) break;
+    tcur *= beta;
+    ++it;
+  }
+  if (it == 100) return set_err(ctx, CVXG_E_LINESEARCH, "Line search: sufficient decrease not reached");
+  *k_a = it - *k_c;
+  *t_out = tcur;
+  return CVXG_OK;
+}
+
+static bool loop_cond(cvxg_ctx* ctx, const cvxg_params* pars) {
+  const double tol = pars->tolSolver;
+  if (!(ctx->iter < pars->maxIter)) return false;
+  if (ctx->p == 0) return ctx->nd > tol && ctx->normGrad > tol;
+  return (ctx->nd > tol && ctx->normGrad > tol) || ctx->eqGap > tol;
+}
+
+static void timing_collect(cvxg_ctx* ctx) {
+  if (!ctx->tm.on) return;
+  (void)hipStreamSynchronize(ctx->s);
+  for (int i = 0; i < NT; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->tm.ev[i][0], ctx->tm.ev[i][1]) == hipSuccess) ctx->tm.ms[i] = ms;
+    else ctx->tm.ms[i] = 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// C-ABI
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+const char* cvxg_version(void) { return "cvxg 0.1 (gfx950, FP64 MFMA SYRK, blocked Cholesky NB=64)"; }
+
+const char* cvxg_last_error(const cvxg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
+  if (!out) return CVXG_E_ARG;
+  *out = nullptr;
+  if (n <= 0 || m < 0 || p < 0) return CVXG_E_DIM;
+  if (p > CVXG_MAX_EQ) return CVXG_E_UNSUPPORTED;
+  if (n > 32767 * TILE) return CVXG_E_UNSUPPORTED;
+  cvxg_ctx* ctx = new cvxg_ctx();
+  *out = ctx;
+  ctx->dev = device;
+  ctx->n = n;
+  ctx->m = m;
+  ctx->p = p;
+  ctx->np = round_up(n, TILE);
+  ctx->mp = round_up(std::max(m, 1), MPAD);
+  ctx->nblk = ctx->np / NB;
+  HIPC(ctx, hipSetDevice(device));
+  HIPC(ctx, hipStreamCreateWithFlags(&ctx->s, hipStreamNonBlocking));
+  const size_t np = ctx->np, mp = ctx->mp;
+  CHK(dalloc(ctx, &ctx->a0, np));
+  CHK(dalloc(ctx, &ctx->A, mp * np));
+  CHK(dalloc(ctx, &ctx->r, mp));
+  CHK(dalloc(ctx, &ctx->ub, mp));
+  {  // padded rows: ub = 1 so d = 1, log d = 0
+    std::vector<double> one(mp, 1.0);
+    HIPC(ctx, hipMemcpy(ctx->ub, one.data(), mp * sizeof(double), hipMemcpyHostToDevice));
+  }
+  if (p > 0) {
+    CHK(dalloc(ctx, &ctx->Aeq, (size_t)CVXG_MAX_EQ * np));
+    CHK(dalloc(ctx, &ctx->beq, CVXG_MAX_EQ));
+    CHK(dalloc(ctx, &ctx->kB, (size_t)CVXG_MAX_EQ * np));
+    CHK(dalloc(ctx, &ctx->Hsave, np * np));
+  }
+  CHK(dalloc(ctx, &ctx->kw, CVXG_MAX_EQ));
+  CHK(dalloc(ctx, &ctx->kx, np));
+  CHK(dalloc(ctx, &ctx->kz, np));
+  CHK(dalloc(ctx, &ctx->eqd, CVXG_MAX_EQ));
+  CHK(dalloc(ctx, &ctx->eqtmp, CVXG_MAX_EQ));
+  for (double** v : {&ctx->x, &ctx->y, &ctx->dx, &ctx->sdir, &ctx->xtmp, &ctx->vtmp, &ctx->Px, &ctx->Ps, &ctx->ruiz0,
+                     &ctx->ruiz1, &ctx->dfin, &ctx->hdiag})
+    CHK(dalloc(ctx, v, np));
+  for (double** v : {&ctx->c, &ctx->d, &ctx->invd, &ctx->w, &ctx->logd, &ctx->e}) CHK(dalloc(ctx, v, std::max(mp, np)));
+  CHK(dalloc(ctx, &ctx->H, np * np));
+  CHK(dalloc(ctx, &ctx->L, np * np));
+  CHK(dalloc(ctx, &ctx->Linv, (size_t)ctx->nblk * NB * NB));
+  CHK(dalloc(ctx, &ctx->rhs, np * MAX_RHS));
+  CHK(dalloc(ctx, &ctx->sol, np * MAX_RHS));
+  // SYRK tile list (lower tiles) and split-K factor
+  const int nt = ctx->np / TILE;
+  std::vector<int> tl;
+  for (int I = 0; I < nt; ++I)
+    for (int J = 0; J <= I; ++J) tl.push_back((I << 16) | J);
+  ctx->ntiles = (int)tl.size();
+  const int kchunks = (int)(mp / KC);
+  ctx->nsplit = 1;
+  if (ctx->ntiles < 256) ctx->nsplit = std::max(1, std::min(kchunks, (512 + ctx->ntiles - 1) / ctx->ntiles));
+  CHK(dalloc(ctx, &ctx->tiles, tl.size()));
+  HIPC(ctx, hipMemcpy(ctx->tiles, tl.data(), tl.size() * sizeof(int), hipMemcpyHostToDevice));
+  size_t part = (mp / 64) * np;
+  if (ctx->nsplit > 1) part = std::max(part, (size_t)ctx->nsplit * ctx->ntiles * TILE * TILE);
+  CHK(dalloc(ctx, &ctx->part, part));
+  const int lsb = ls_blocks(std::max(m, 1));
+  CHK(dalloc(ctx, &ctx->ls_plog, (size_t)lsb * LS_TRIALS));
+  CHK(dalloc(ctx, &ctx->ls_pcnt, (size_t)lsb * LS_TRIALS * 2));
+  CHK(dalloc(ctx, &ctx->ls_log, LS_TRIALS));
+  CHK(dalloc(ctx, &ctx->ls_cnt, 2 * LS_TRIALS));
+  CHK(dalloc(ctx, &ctx->ctrl, 1));
+  HIPC(ctx, hipHostMalloc((void**)&ctx->hctrl, sizeof(DevCtrl), hipHostMallocDefault));
+  HIPC(ctx, hipHostMalloc((void**)&ctx->hls, 3 * LS_TRIALS * sizeof(double), hipHostMallocDefault));
+  memset(ctx->hctrl, 0, sizeof(DevCtrl));
+  for (int i = 0; i < NT; ++i) {
+    HIPC(ctx, hipEventCreate(&ctx->tm.ev[i][0]));
+    HIPC(ctx, hipEventCreate(&ctx->tm.ev[i][1]));
+  }
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  return CVXG_OK;
+}
+
+void cvxg_destroy(cvxg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->dev);
+  if (ctx->s) (void)hipStreamSynchronize(ctx->s);
+  void* ptrs[] = {ctx->P, ctx->a0, ctx->A, ctx->r, ctx->ub, ctx->Aeq, ctx->beq, ctx->x, ctx->y, ctx->dx, ctx->sdir,
+                  ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
+                  ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
+                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
+                  ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
+  if (ctx->hls) (void)hipHostFree(ctx->hls);
+  for (int i = 0; i < NT; ++i) {
+    if (ctx->tm.ev[i][0]) (void)hipEventDestroy(ctx->tm.ev[i][0]);
+    if (ctx->tm.ev[i][1]) (void)hipEventDestroy(ctx->tm.ev[i][1]);
+  }
+  if (ctx->s) (void)hipStreamDestroy(ctx->s);
+  delete ctx;
+}
+
+int cvxg_set_objective(cvxg_ctx* ctx, const double* P, int ldP, const double* a, double r) {
+  if (!ctx || !a) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  const int n = ctx->n, np = ctx->np;
+  if (P) {
+    if (ldP < n) return set_err(ctx, CVXG_E_DIM, "ldP < n");
+    if (!ctx->P) CHK(dalloc(ctx, &ctx->P, (size_t)np * np));
+    CHK(upload_mat(ctx, ctx->P, np, np, P, n, n, ldP, 1));  // symmetric: either layout
+    ctx->hasP = 1;
+  } else {
+    ctx->hasP = 0;
+  }
+  CHK(upload_vec(ctx, ctx->a0, a, n, np));
+  ctx->r0 = r;
+  ctx->have_obj = 1;
+  ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+int cvxg_set_ineq(cvxg_ctx* ctx, const double* A, int ldA, int row_major, const double* r, const double* ub) {
+  if (!ctx || (ctx->m > 0 && (!A || !r || !ub))) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  const int n = ctx->n, m = ctx->m;
+  if (m > 0) {
+    if (ldA < (row_major ? n : m)) return set_err(ctx, CVXG_E_DIM, "ldA too small");
+    CHK(upload_mat(ctx, ctx->A, ctx->np, ctx->mp, A, m, n, ldA, row_major));
+    std::vector<double> rr(ctx->mp, 0.0), uu(ctx->mp, 1.0);
+    memcpy(rr.data(), r, m * sizeof(double));
+    memcpy(uu.data(), ub, m * sizeof(double));
+    HIPC(ctx, hipMemcpy(ctx->r, rr.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
+    HIPC(ctx, hipMemcpy(ctx->ub, uu.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
+  }
+  ctx->have_ineq = 1;
+  ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+int cvxg_set_eq(cvxg_ctx* ctx, const double* Aeq, int ldAeq, int row_major, const double* beq) {
+  if (!ctx) return CVXG_E_ARG;
+  if (ctx->p == 0) return CVXG_OK;
+  if (!Aeq || !beq) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(upload_mat(ctx, ctx->Aeq, ctx->np, CVXG_MAX_EQ, Aeq, ctx->p, ctx->n, ldAeq, row_major));
+  std::vector<double> b(CVXG_MAX_EQ, 0.0);
+  memcpy(b.data(), beq, ctx->p * sizeof(double));
+  HIPC(ctx, hipMemcpy(ctx->beq, b.data(), CVXG_MAX_EQ * sizeof(double), hipMemcpyHostToDevice));
+  ctx->have_eq = 1;
+  ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+int cvxg_set_x(cvxg_ctx* ctx, const double* x) {
+  if (!ctx || !x) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(upload_vec(ctx, ctx->x, x, ctx->n, ctx->np));
+  ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+int cvxg_get_x(cvxg_ctx* ctx, double* x) {
+  if (!ctx || !x) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  HIPC(ctx, hipMemcpyAsync(x, ctx->x, ctx->n * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  return CVXG_OK;
+}
+
+static int check_ready(cvxg_ctx* ctx) {
+  if (!ctx->have_obj || !ctx->have_ineq || (ctx->p > 0 && !ctx->have_eq))
+    return set_err(ctx, CVXG_E_ARG, "objective / inequalities / equalities not set");
+  return CVXG_OK;
+}
+
+static int set_t(cvxg_ctx* ctx, double t) {
+  if (ctx->t != t) ctx->x_eval_valid = 0;
+  ctx->t = t;
+  launch_ctrl_set(ctx->s, ctx->ctrl, 0, t);
+  HIPC(ctx, hipGetLastError());
+  return CVXG_OK;
+}
+
+int cvxg_barrier_eval(cvxg_ctx* ctx, double t, const double* x, double* f, double* g, double* H) {
+  if (!ctx || !x) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(check_ready(ctx));
+  CHK(cvxg_set_x(ctx, x));
+  CHK(set_t(ctx, t));
+  CHK(eval_at_x(ctx));
+  if (f) *f = ctx->f_at_x;
+  if (g) HIPC(ctx, hipMemcpy(g, ctx->y, ctx->n * sizeof(double), hipMemcpyDeviceToHost));
+  if (H) {
+    CHK(assemble_hessian(ctx));
+    HIPC(ctx, hipStreamSynchronize(ctx->s));
+    HIPC(ctx, hipMemcpy2D(H, ctx->n * sizeof(double), ctx->H, ctx->np * sizeof(double), ctx->n * sizeof(double),
+                          ctx->n, hipMemcpyDeviceToHost));
+  }
+  return CVXG_OK;
+}
+
+int cvxg_constraint_values(cvxg_ctx* ctx, const double* x, double* gx) {
+  if (!ctx || !x || !gx) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(cvxg_set_x(ctx, x));
+  launch_ctrl_reset_eval(ctx->s, ctx->ctrl);
+  launch_constraint_eval(ctx->s, ctx->A, ctx->np, ctx->mp, ctx->np, ctx->x, ctx->r, ctx->ub, ctx->c, ctx->d,
+                         ctx->invd, ctx->w, ctx->logd, ctx->ctrl);
+  HIPC(ctx, hipGetLastError());
+  HIPC(ctx, hipMemcpyAsync(gx, ctx->c, ctx->m * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+int cvxg_active_set(cvxg_ctx* ctx, const double* x, double tol, int* idx, int* count) {
+  if (!ctx || !x || !count) return CVXG_E_ARG;
+  std::vector<double> g(ctx->m), ub(ctx->m);
+  CHK(cvxg_constraint_values(ctx, x, g.data()));
+  HIPC(ctx, hipMemcpy(ub.data(), ctx->ub, ctx->m * sizeof(double), hipMemcpyDeviceToHost));
+  int k = 0;
+  for (int i = 0; i < ctx->m; ++i)
+    if (fabs(g[i] - ub[i]) < tol) {  // Constraint.isActive, Constraint.scala:26
+      if (idx) idx[k] = i;
+      ++k;
+    }
+  *count = k;
+  return CVXG_OK;
+}
+
+int cvxg_newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, double* dx, double* w,
+                          cvxg_step_info* info) {
+  if (!ctx || !pars || !x) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(check_ready(ctx));
+  cvxg_step_info tmp;
+  if (!info) info = &tmp;
+  memset(info, 0, sizeof(*info));
+  CHK(cvxg_set_x(ctx, x));
+  CHK(set_t(ctx, t));
+  CHK(eval_at_x(ctx));
+  info->t = t;
+  info->f = ctx->f_at_x;
+  info->norm_grad = ctx->normGrad;
+  int rc = newton_direction(ctx, pars, info);
+  if (rc != CVXG_OK) return rc;
+  info->q = ctx->hctrl->sc[SC_Q];
+  info->newton_decrement = -info->q / 2;
+  if (dx) HIPC(ctx, hipMemcpy(dx, ctx->dx, ctx->n * sizeof(double), hipMemcpyDeviceToHost));
+  if (w && ctx->p > 0) HIPC(ctx, hipMemcpy(w, ctx->kw, ctx->p * sizeof(double), hipMemcpyDeviceToHost));
+  return CVXG_OK;
+}
+
+int cvxg_centering_begin(cvxg_ctx* ctx, double t) {
+  if (!ctx) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(check_ready(ctx));
+  CHK(set_t(ctx, t));
+  ctx->iter = 0;
+  ctx->trust = NAN;
+  ctx->began = 1;
+  CHK(eval_at_x(ctx));  // y = objF.gradientAt(x); normGrad; eqDiff   (UnconstrainedSolver.scala:44-46)
+  ctx->nd = std::numeric_limits<double>::infinity();  // set to tol + 1 by the first cvxg_newton_step
+  return CVXG_OK;
+}
+
+int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
+  if (!ctx || !pars) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  if (!ctx->began) return set_err(ctx, CVXG_E_ARG, "cvxg_newton_step before cvxg_centering_begin");
+  cvxg_step_info tmp;
+  if (!info) info = &tmp;
+  memset(info, 0, sizeof(*info));
+  info->t = ctx->t;
+  info->iter = ctx->iter;
+  if (ctx->nd == std::numeric_limits<double>::infinity()) ctx->nd = pars->tolSolver + 1;
+  if (!loop_cond(ctx, pars)) {
+    info->done = 1;
+    info->newton_decrement = ctx->nd;
+    info->norm_grad = ctx->normGrad;
+    return CVXG_OK;
+  }
+  if (!ctx->x_eval_valid) CHK(eval_at_x(ctx));
+  const double tol = pars->tolSolver;
+  info->f = ctx->f_at_x;
+  info->norm_grad = ctx->normGrad;
+  int rc = newton_direction(ctx, pars, info);
+  if (rc != CVXG_OK) return rc;
+  const double q = ctx->hctrl->sc[SC_Q];
+  ctx->nd = -q / 2;
+  info->q = q;
+  info->newton_decrement = ctx->nd;
+  if (ctx->nd > tol) {
+    tstart(ctx, 4);
+    double scale = 1.0;
+    int limit = 100;
+    if (ctx->p == 0) {
+      // trust region: rho = 1+1/4 == 1 (integer), radius frozen at |d_0|_H  (UnconstrainedSolver.scala:86-101)
+      const double hNorm = sqrt(-q);
+      if (ctx->iter == 0) ctx->trust = hNorm;
+      info->hnorm = hNorm;
+      info->trust_radius = ctx->trust;
+      if (!(ctx->iter == 0 || hNorm <= ctx->trust)) scale = ctx->trust / hNorm;
+      limit = 200;
+    }
+    if (scale == 1.0) {
+      HIPC(ctx, hipMemcpyAsync(ctx->sdir, ctx->dx, ctx->np * sizeof(double), hipMemcpyDeviceToDevice, ctx->s));
+    } else {
+      launch_axpy_strided(ctx->s, nullptr, ctx->dx, 1, 0, scale, ctx->np, ctx->sdir);  // d * (radius/hNorm)
+    }
+    double tacc = 1.0;
+    int kc = 0, ka = 0;
+    rc = line_search(ctx, pars, q, limit, &tacc, &kc, &ka);
+    tstop(ctx, 4);
+    if (rc != CVXG_OK) return rc;
+    launch_axpy(ctx->s, ctx->x, ctx->sdir, tacc, ctx->np, ctx->x);  // x = x + s*t
+    HIPC(ctx, hipGetLastError());
+    info->step = tacc;
+    info->backtracks_c = kc;
+    info->backtracks_armijo = ka;
+    info->took_step = 1;
+    rc = eval_at_x(ctx);  // y = objF.gradientAt(x); normGrad (and eqDiff)
+    if (rc != CVXG_OK) return rc;
+  }
+  ctx->iter += 1;
+  info->norm_grad_new = ctx->normGrad;
+  info->equality_gap = ctx->eqGap;
+  info->done = loop_cond(ctx, pars) ? 0 : 1;
+  timing_collect(ctx);
+  return CVXG_OK;
+}
+
+int cvxg_centering(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg_centering_info* info) {
+  if (!ctx || !pars) return CVXG_E_ARG;
+  CHK(cvxg_centering_begin(ctx, t));
+  cvxg_step_info si;
+  while (true) {
+    CHK(cvxg_newton_step(ctx, pars, &si));
+    if (si.done) break;
+  }
+  if (info) {
+    info->iter = ctx->iter;
+    info->maxed_out = ctx->iter >= pars->maxIter;
+    info->newton_decrement = ctx->nd;
+    info->norm_grad = ctx->normGrad;
+    info->equality_gap = ctx->eqGap;
+  }
+  return CVXG_OK;
+}
+
+int cvxg_barrier_solve(cvxg_ctx* ctx, const cvxg_params* pars, int termination, cvxg_solution* sol) {
+  if (!ctx || !pars) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(check_ready(ctx));
+  // assert(C.isInSet(startingPoint))  (BarrierSolver.scala:35)
+  CHK(set_t(ctx, 1.0));
+  int rc = eval_at_x(ctx);
+  if (rc != CVXG_OK || ctx->hctrl->not_strict > 0)
+    return set_err(ctx, CVXG_E_INFEASIBLE_X, "Starting point x not in set C");
+  const double mu = 10.0;  // BarrierSolver.scala:73
+  double t = 1.0;
+  double gap = INFINITY, eqgap = INFINITY, fval = 1.7976931348623157e308;
+  bool eq_defined = false;  // OptimizationState.equalityGap: None before the first pass without EQs
+  const double maxIter = 1000 / mu;
+  int outer = 0, total = 0;
+  cvxg_centering_info ci{};
+  auto tc = [&]() -> bool {
+    if (termination == 1)  // CvxUtils.phase_I_TerminationCriterion
+      return fval < 0 && (!eq_defined || eqgap < 1e-6);
+    return gap < pars->tolSolver && (!eq_defined || eqgap < pars->tolSolver);  // standardTerminationCriterion
+  };
+  if (ctx->p > 0) eq_defined = true;  // solveWithEQs starts with Some(equalityGap = MaxValue)
+  while (!tc() && outer < maxIter) {
+    CHK(cvxg_centering(ctx, pars, t, &ci));
+    total += ci.iter;
+    fval = objective_at_x(ctx);  // objF.valueAt(x) at the centred point
+    gap = ctx->m / t;            // dualityGap = numConstraints/t
+    eqgap = ctx->p > 0 ? ci.equality_gap : 0.0;
+    eq_defined = true;
+    t = mu * t;
+    ++outer;
+  }
+  if (sol) {
+    sol->duality_gap = gap;
+    sol->equality_gap = eqgap;
+    sol->newton_decrement = ci.newton_decrement;
+    sol->norm_grad = ci.norm_grad;
+    sol->objective = fval;
+    sol->iter = ci.iter;
+    sol->maxed_out = ci.maxed_out;
+    sol->outer_iters = outer;
+    sol->newton_steps = total;
+  }
+  return CVXG_OK;
+}
+
+int cvxg_set_timing(cvxg_ctx* ctx, int enabled) {
+  if (!ctx) return CVXG_E_ARG;
+  ctx->tm.on = enabled != 0;
+  return CVXG_OK;
+}
+
+int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count) {
+  if (!ctx || !ms) return CVXG_E_ARG;
+  for (int i = 0; i < count && i < NT; ++i) ms[i] = ctx->tm.ms[i];
+  return CVXG_OK;
+}
+
+}  // extern "C"

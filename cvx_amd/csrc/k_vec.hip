@@ -1,0 +1,544 @@
+// k_vec.hip — HBM-streaming kernels of the barrier Newton step (gfx950).
+//
+// Row-major constraint matrix A (row i = a_i, LinearConstraint.scala:7-32), one 64-lane wave per row so
+// each row is read as 1 KiB coalesced double2 sweeps; column reductions write per-64-row-chunk partials
+// that a second pass sums in a fixed order (results are bitwise reproducible run to run).
+#include <math.h>
+
+#include "kernels.hpp"
+
+namespace cvxg {
+
+// ------------------------------------------------------------------------------------------------
+// Row dot products: one wave per row, double2 loads, fixed-order wave reduction.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double row_dot_wave(const double* __restrict__ row, const double* __restrict__ v,
+                                               int cols, int lane) {
+  double acc0 = 0.0, acc1 = 0.0;
+  int j = 2 * lane;
+  for (; j + 1 < cols; j += 128) {
+    const double2 a = *reinterpret_cast<const double2*>(row + j);
+    const double2 b = *reinterpret_cast<const double2*>(v + j);
+    acc0 = fma(a.x, b.x, acc0);
+    acc1 = fma(a.y, b.y, acc1);
+  }
+  if (j < cols) acc0 = fma(row[j], v[j], acc0);
+  return wave_sum(acc0 + acc1);
+}
+
+__global__ __launch_bounds__(256) void k_constraint_eval(const double* __restrict__ A, int ld, int mp, int cols,
+                                                         const double* __restrict__ x,
+                                                         const double* __restrict__ r,
+                                                         const double* __restrict__ ub, double* __restrict__ c,
+                                                         double* __restrict__ d, double* __restrict__ invd,
+                                                         double* __restrict__ w, double* __restrict__ logd,
+                                                         DevCtrl* ctrl) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= mp) return;
+  const double dot = row_dot_wave(A + (size_t)row * ld, x, cols, lane);
+  if (lane == 0) {
+    const double ci = r[row] + dot;          // r + (a dot x)          LinearConstraint.scala:23
+    const double di = ub[row] - ci;          // d = ub - valueAt(x)    BarrierSolver.scala:283
+    c[row] = ci;
+    d[row] = di;
+    invd[row] = 1.0 / di;
+    w[row] = 1.0 / (di * di);                // GGt/(d*d)              BarrierSolver.scala:314
+    logd[row] = (di > 0.0) ? log(di) : 0.0;
+    if (!(di > 0.0)) atomicAdd(&ctrl->infeasible, 1);
+    if (!(ci * (1 + 3e-16) < ub[row])) atomicAdd(&ctrl->not_strict, 1);  // Constraint.scala:23
+  }
+}
+
+void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int n_cols, const double* x,
+                            const double* r, const double* ub, double* c, double* d, double* invd,
+                            double* w, double* logd, DevCtrl* ctrl) {
+  k_constraint_eval<<<(mp + 3) / 4, 256, 0, s>>>(A, ld, mp, n_cols, x, r, ub, c, d, invd, w, logd, ctrl);
+}
+
+__global__ __launch_bounds__(256) void k_rowdot(const double* __restrict__ M, int ld, int rows, int cols,
+                                                const double* __restrict__ v, double* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const double dot = row_dot_wave(M + (size_t)row * ld, v, cols, lane);
+  if (lane == 0) y[row] = dot;
+}
+
+void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y) {
+  k_rowdot<<<(rows + 3) / 4, 256, 0, s>>>(M, ld, rows, cols, v, y);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Column reductions A' v: grid (cols/512, rows/64); thread owns 2 adjacent columns, loops 64 rows.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_coldot_partials(const double* __restrict__ M, int ld, int rows, int cols,
+                                                         const double* __restrict__ v, double* __restrict__ part) {
+  const int j = (blockIdx.x * 256 + threadIdx.x) * 2;
+  const int r0 = blockIdx.y * 64;
+  if (j >= cols) return;
+  double a0 = 0.0, a1 = 0.0;
+  const int rend = min(r0 + 64, rows);
+  for (int i = r0; i < rend; ++i) {
+    const double vi = v[i];
+    const double2 m = *reinterpret_cast<const double2*>(M + (size_t)i * ld + j);
+    a0 = fma(m.x, vi, a0);
+    a1 = fma(m.y, vi, a1);
+  }
+  double2 o;
+  o.x = a0;
+  o.y = a1;
+  *reinterpret_cast<double2*>(part + (size_t)blockIdx.y * cols + j) = o;
+}
+
+void launch_coldot_partials(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
+                            double* part) {
+  dim3 grid((cols / 2 + 255) / 256, (rows + 63) / 64);
+  k_coldot_partials<<<grid, 256, 0, s>>>(M, ld, rows, cols, v, part);
+}
+
+__global__ void k_gradient_finalize(const double* __restrict__ a0, const double* __restrict__ Px,
+                                    const double* __restrict__ part, int nchunks, int cols, const DevCtrl* ctrl,
+                                    double* __restrict__ y) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cols) return;
+  const double t = ctrl->t;
+  // objF.gradientAt(x) * t  (QuadraticObjectiveFunction.scala:32: a + P*x), then + sum_i a_i/d_i
+  double g = (Px ? (a0[j] + Px[j]) : a0[j]) * t;
+  double s = 0.0;
+  for (int c = 0; c < nchunks; ++c) s += part[(size_t)c * cols + j];
+  y[j] = g + s;
+}
+
+void launch_gradient_finalize(hipStream_t s, const double* a0, const double* Px, const double* part,
+                              int nchunks, int n_cols, const DevCtrl* ctrl, double* y) {
+  k_gradient_finalize<<<(n_cols + 255) / 256, 256, 0, s>>>(a0, Px, part, nchunks, n_cols, ctrl, y);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Deterministic single-block reductions into ctrl->sc[slot].
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_dot(const double* __restrict__ u, const double* __restrict__ v, int n,
+                                              DevCtrl* ctrl, int slot) {
+  __shared__ double red[16];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc = fma(u[i], v ? v[i] : u[i], acc);
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) ctrl->sc[slot] = acc;
+}
+
+__global__ __launch_bounds__(1024) void k_sum(const double* __restrict__ u, int n, DevCtrl* ctrl, int slot) {
+  __shared__ double red[16];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += u[i];
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) ctrl->sc[slot] = acc;
+}
+
+void launch_dot(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot) {
+  k_dot<<<1, 1024, 0, s>>>(u, v, n, ctrl, slot);
+}
+void launch_sum(hipStream_t s, const double* u, int n, DevCtrl* ctrl, int slot) {
+  k_sum<<<1, 1024, 0, s>>>(u, n, ctrl, slot);
+}
+
+__global__ void k_axpy(const double* __restrict__ u, const double* __restrict__ v, double alpha, int n,
+                       double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = u[i] + v[i] * alpha;  // x + s*t  (UnconstrainedSolver.scala:130)
+}
+void launch_axpy(hipStream_t s, const double* u, const double* v, double alpha, int n, double* out) {
+  k_axpy<<<(n + 255) / 256, 256, 0, s>>>(u, v, alpha, n, out);
+}
+
+__global__ void k_scale_vec(const double* __restrict__ u, const double* __restrict__ d, int n,
+                            double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = d[i] * u[i];
+}
+void launch_scale_vec(hipStream_t s, const double* u, const double* d, int n, double* out) {
+  k_scale_vec<<<(n + 255) / 256, 256, 0, s>>>(u, d, n, out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Ruiz equilibration, MatrixUtils.scala:240-268 (Jacobi form: a sweep reads d of the previous sweep).
+// Sweep k runs iff rho[k] > 1e-6 (rho[0] = 1); it writes d into the other buffer and max|1-u| into rho[k+1].
+// ------------------------------------------------------------------------------------------------
+__global__ void k_ruiz_init(double* d0, int np, DevCtrl* ctrl) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < np) d0[i] = 1.0;
+  if (i < RUIZ_MAX + 2) ctrl->ruiz_rho[i] = (i == 0) ? (unsigned long long)__double_as_longlong(1.0) : 0ull;
+}
+void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl) {
+  k_ruiz_init<<<(np + 255) / 256, 256, 0, s>>>(d0, np, ctrl);
+}
+
+__global__ __launch_bounds__(256) void k_ruiz_sweep(const double* __restrict__ H, int ld, int n,
+                                                    const double* __restrict__ dcur, double* __restrict__ dnext,
+                                                    DevCtrl* ctrl, int k) {
+  const double rho = __longlong_as_double((long long)ctrl->ruiz_rho[k]);
+  if (!(rho > 1e-6)) return;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const double* hr = H + (size_t)row * ld;
+  double a0 = 0.0, a1 = 0.0;
+  int j = 2 * lane;
+  for (; j + 1 < n; j += 128) {
+    const double2 h = *reinterpret_cast<const double2*>(hr + j);
+    const double2 dd = *reinterpret_cast<const double2*>(dcur + j);
+    const double q0 = dd.x * h.x, q1 = dd.y * h.y;
+    a0 = fma(q0, q0, a0);
+    a1 = fma(q1, q1, a1);
+  }
+  if (j < n) {
+    const double q0 = dcur[j] * hr[j];
+    a0 = fma(q0, q0, a0);
+  }
+  const double ssum = wave_sum(a0 + a1);
+  if (lane == 0) {
+    const double di = dcur[row];
+    const double u = sqrt(di * sqrt(ssum));        // sqrt(norm(Q(i,::)))   MatrixUtils.scala:258
+    const double v = (u > 0) ? 1.0 / u : 1.0;      // :259
+    dnext[row] = di * v;                           // :260
+    atomic_max_pos(&ctrl->ruiz_rho[k + 1], fabs(1.0 - u));  // :261-262
+  }
+}
+void launch_ruiz_sweep(hipStream_t s, const double* H, int ld, int n, const double* dcur, double* dnext,
+                       DevCtrl* ctrl, int k) {
+  k_ruiz_sweep<<<(n + 3) / 4, 256, 0, s>>>(H, ld, n, dcur, dnext, ctrl, k);
+}
+
+__global__ void k_ruiz_final(const double* __restrict__ d0, const double* __restrict__ d1, int np,
+                             double* __restrict__ dfin, DevCtrl* ctrl) {
+  int K = RUIZ_MAX;
+  for (int k = 0; k < RUIZ_MAX; ++k) {
+    if (!(__longlong_as_double((long long)ctrl->ruiz_rho[k]) > 1e-6)) {
+      K = k;
+      break;
+    }
+  }
+  const double* src = (K & 1) ? d1 : d0;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < np) dfin[i] = src[i];
+  if (i == 0) ctrl->ruiz_sweeps = K;
+}
+void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl) {
+  k_ruiz_final<<<(np + 255) / 256, 256, 0, s>>>(d0, d1, np, dfin, ctrl);
+}
+
+// Q = (dd') o H (+ reg I), lower triangle into L; padded part: identity.   MatrixUtils.scala:267, :454
+__global__ __launch_bounds__(256) void k_form_q(const double* __restrict__ H, double* __restrict__ L, int ld,
+                                                int n, int np, const double* __restrict__ d,
+                                                const DevCtrl* ctrl) {
+  const int i = blockIdx.y;
+  const int j = (blockIdx.x * 256 + threadIdx.x) * 2;
+  if (j > i) return;
+  const double reg = ctrl->reg;
+  double2 o;
+  if (i < n) {
+    const double di = d[i];
+    const double2 h = *reinterpret_cast<const double2*>(H + (size_t)i * ld + j);
+    const double2 dj = *reinterpret_cast<const double2*>(d + j);
+    o.x = (j < n) ? (di * dj.x) * h.x : 0.0;
+    o.y = (j + 1 < n) ? (di * dj.y) * h.y : 0.0;
+    if (j == i) o.x += reg;
+    if (j + 1 == i) o.y += reg;
+  } else {
+    o.x = (j == i) ? 1.0 : 0.0;
+    o.y = (j + 1 == i) ? 1.0 : 0.0;
+  }
+  *reinterpret_cast<double2*>(L + (size_t)i * ld + j) = o;
+}
+void launch_form_q(hipStream_t s, const double* H, double* L, int ld, int n, int np, const double* d,
+                   const DevCtrl* ctrl) {
+  dim3 grid((np / 2 + 255) / 256, np);
+  k_form_q<<<grid, 256, 0, s>>>(H, L, ld, n, np, d, ctrl);
+}
+
+__global__ void k_add_diag(double* H, int ld, int n, double v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) H[(size_t)i * ld + i] += v;
+}
+__global__ void k_copy_diag(const double* H, int ld, int n, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = H[(size_t)i * ld + i];
+}
+__global__ void k_set_diag(double* H, int ld, int n, const double* diag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) H[(size_t)i * ld + i] = diag[i];
+}
+void launch_add_diag(hipStream_t s, double* H, int ld, int n, double v) {
+  k_add_diag<<<(n + 255) / 256, 256, 0, s>>>(H, ld, n, v);
+}
+void launch_copy_diag(hipStream_t s, const double* H, int ld, int n, double* out) {
+  k_copy_diag<<<(n + 255) / 256, 256, 0, s>>>(H, ld, n, out);
+}
+void launch_set_diag(hipStream_t s, double* H, int ld, int n, const double* diag) {
+  k_set_diag<<<(n + 255) / 256, 256, 0, s>>>(H, ld, n, diag);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Line search trials (UnconstrainedSolver.scala:107-128): the reference evaluates g_i(x + s t) for the
+// geometric sequence t = beta^k.  g is affine, so g_i(x + s t) = g_i(x) + t (a_i . s): one GEMV e = A s
+// per Newton step, then O(m) per trial.  Each thread owns one constraint and sweeps LS_TRIALS trials.
+// ------------------------------------------------------------------------------------------------
+int ls_blocks(int m) { return (m + 255) / 256; }
+
+__global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c, const double* __restrict__ e,
+                                                   const double* __restrict__ ub, int m, double tbase, double beta,
+                                                   double* __restrict__ part_log, int* __restrict__ part_cnt) {
+  __shared__ double slog[4][LS_TRIALS];
+  __shared__ int sviol[4][LS_TRIALS];
+  __shared__ int snpos[4][LS_TRIALS];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool valid = i < m;
+  const double ci = valid ? c[i] : 0.0, ei = valid ? e[i] : 0.0, ubi = valid ? ub[i] : 1.0;
+  double t = tbase;
+  for (int k = 0; k < LS_TRIALS; ++k) {
+    const double g = ci + t * ei;
+    const double dd = ubi - g;
+    const bool viol = valid && !(g * (1 + 3e-16) < ubi);   // Constraint.scala:23
+    const bool npos = valid && !(dd > 0.0);                 // BarrierSolver.scala:284
+    const double lg = (valid && dd > 0.0) ? log(dd) : 0.0;
+    const double sl = wave_sum(lg);
+    const unsigned long long bv = __ballot(viol), bn = __ballot(npos);
+    if (lane == 0) {
+      slog[wid][k] = sl;
+      sviol[wid][k] = __popcll(bv);
+      snpos[wid][k] = __popcll(bn);
+    }
+    t *= beta;  // t *= beta (repeated products, not pow)   UnconstrainedSolver.scala:93
+  }
+  __syncthreads();
+  if (threadIdx.x < LS_TRIALS) {
+    const int k = threadIdx.x;
+    double s = 0.0;
+    int v = 0, np_ = 0;
+    for (int w = 0; w < 4; ++w) {
+      s += slog[w][k];
+      v += sviol[w][k];
+      np_ += snpos[w][k];
+    }
+    part_log[(size_t)blockIdx.x * LS_TRIALS + k] = s;
+    part_cnt[((size_t)blockIdx.x * LS_TRIALS + k) * 2 + 0] = v;
+    part_cnt[((size_t)blockIdx.x * LS_TRIALS + k) * 2 + 1] = np_;
+  }
+}
+
+void launch_ls_trials(hipStream_t s, const double* c, const double* e, const double* ub, int m, double tbase,
+                      double beta, double* part_log, int* part_cnt) {
+  k_ls_trials<<<ls_blocks(m), 256, 0, s>>>(c, e, ub, m, tbase, beta, part_log, part_cnt);
+}
+
+__global__ void k_ls_finalize(const double* __restrict__ part_log, const int* __restrict__ part_cnt, int nblocks,
+                              double* __restrict__ out_log, int* __restrict__ out_cnt) {
+  const int k = threadIdx.x;
+  if (k >= LS_TRIALS) return;
+  double s = 0.0;
+  int v = 0, np_ = 0;
+  for (int b = 0; b < nblocks; ++b) {
+    s += part_log[(size_t)b * LS_TRIALS + k];
+    v += part_cnt[((size_t)b * LS_TRIALS + k) * 2 + 0];
+    np_ += part_cnt[((size_t)b * LS_TRIALS + k) * 2 + 1];
+  }
+  out_log[k] = s;
+  out_cnt[2 * k] = v;
+  out_cnt[2 * k + 1] = np_;
+}
+void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_cnt, int nblocks, double* out_log,
+                        int* out_cnt) {
+  k_ls_finalize<<<1, 64, 0, s>>>(part_log, part_cnt, nblocks, out_log, out_cnt);
+}
+
+// ------------------------------------------------------------------------------------------------
+// KKT Schur complement for p <= CVXG_MAX_EQ equalities (KKTSystem.scala:99-167), one workgroup.
+// X = [H^-1 B' | H^-1 Dq] (n x nrhs row-major, nrhs = p+1), B = A diag(d) (p x ld row-major).
+// R = B X[:, :p]; S = (R+R')/2; K = chol(S); z = -(b + B X[:,p]); w = K'^-1 K^-1 z;
+// x = -(X[:,p] + X[:,:p] w).  chol failure -> ctrl->chol_info = -1.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_kkt_schur(const double* __restrict__ X, int nrhs,
+                                                   const double* __restrict__ B, int ldb, int p, int n,
+                                                   const double* __restrict__ bvec, double* __restrict__ w_out,
+                                                   double* __restrict__ xsol, DevCtrl* ctrl) {
+  __shared__ double red[16];
+  __shared__ double R[8][9];  // R[a][0..p-1], column p holds B X[:,p]
+  __shared__ double wsh[8];
+  __shared__ int fail;
+  if (threadIdx.x == 0) fail = 0;
+  for (int a = 0; a < p; ++a) {
+    for (int c = 0; c <= p; ++c) {
+      double acc = 0.0;
+      for (int i = threadIdx.x; i < n; i += blockDim.x) acc = fma(B[(size_t)a * ldb + i], X[(size_t)i * nrhs + c], acc);
+      acc = block_sum(acc, red);
+      if (threadIdx.x == 0) R[a][c] = acc;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double S[8][8], K[8][8], z[8], u[8];
+    for (int a = 0; a < p; ++a)
+      for (int c = 0; c < p; ++c) S[a][c] = (R[a][c] + R[c][a]) * 0.5;  // KKTSystem.scala:139
+    // cholesky(S), lower (dpotrf semantics: fail on non-positive pivot)
+    for (int a = 0; a < p; ++a)
+      for (int c = 0; c < p; ++c) K[a][c] = 0.0;
+    for (int j = 0; j < p && !fail; ++j) {
+      double s = S[j][j];
+      for (int k = 0; k < j; ++k) s -= K[j][k] * K[j][k];
+      if (!(s > 0.0)) {
+        fail = 1;
+        break;
+      }
+      K[j][j] = sqrt(s);
+      for (int i = j + 1; i < p; ++i) {
+        double t = S[i][j];
+        for (int k = 0; k < j; ++k) t -= K[i][k] * K[j][k];
+        K[i][j] = t / K[j][j];
+      }
+    }
+    if (!fail) {
+      for (int a = 0; a < p; ++a) z[a] = -(bvec[a] + R[a][p]);  // z = -(b + A*Hinv_q)   :141
+      for (int i = 0; i < p; ++i) {                             // forwardSolve(K, z)  :143
+        double s = 0.0;
+        for (int j = 0; j < i; ++j) s += K[i][j] * u[j];
+        u[i] = (z[i] - s) / K[i][i];
+      }
+      for (int i = p - 1; i >= 0; --i) {                        // backSolve(K', u)    :144
+        double s = 0.0;
+        for (int j = p - 1; j > i; --j) s += K[j][i] * wsh[j];
+        wsh[i] = (u[i] - s) / K[i][i];
+      }
+      for (int a = 0; a < p; ++a) w_out[a] = wsh[a];
+    } else {
+      ctrl->chol_info = -1;
+    }
+  }
+  __syncthreads();
+  if (fail) return;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {          // x = -(Hinv_q + Hinv_At*w)  :145
+    double s = 0.0;
+    for (int a = 0; a < p; ++a) s += X[(size_t)i * nrhs + a] * wsh[a];
+    xsol[i] = -(X[(size_t)i * nrhs + p] + s);
+  }
+}
+
+void launch_kkt_schur(hipStream_t s, const double* X, int nrhs, const double* B, int ldb, int p, int n,
+                      const double* bvec, double* w_out, double* xsol, DevCtrl* ctrl) {
+  k_kkt_schur<<<1, 256, 0, s>>>(X, nrhs, B, ldb, p, n, bvec, w_out, xsol, ctrl);
+}
+
+}  // namespace cvxg
+
+// ------------------------------------------------------------------------------------------------
+// Small control / vector helpers (stream-ordered, kernel arguments captured at launch).
+// ------------------------------------------------------------------------------------------------
+namespace cvxg {
+
+__global__ void k_ctrl_set(DevCtrl* ctrl, int which, double v) {
+  if (which == 0) ctrl->t = v;
+  else if (which == 1) ctrl->reg = v;
+}
+__global__ void k_ctrl_reset_eval(DevCtrl* ctrl) {
+  ctrl->infeasible = 0;
+  ctrl->not_strict = 0;
+}
+__global__ void k_ctrl_reset_chol(DevCtrl* ctrl) {
+  ctrl->chol_info = 0;
+  ctrl->min_diag = (unsigned long long)__double_as_longlong(__builtin_inf());
+}
+void launch_ctrl_set(hipStream_t s, DevCtrl* ctrl, int which, double v) { k_ctrl_set<<<1, 1, 0, s>>>(ctrl, which, v); }
+void launch_ctrl_reset_eval(hipStream_t s, DevCtrl* ctrl) { k_ctrl_reset_eval<<<1, 1, 0, s>>>(ctrl); }
+void launch_ctrl_reset_chol(hipStream_t s, DevCtrl* ctrl) { k_ctrl_reset_chol<<<1, 1, 0, s>>>(ctrl); }
+
+// rhs[i*nrhs + col] = d_i * sgn * v_i   (d*b with b = -grad for the Newton system)
+__global__ void k_scaled_col(const double* __restrict__ d, const double* __restrict__ v, double sgn, int n, int np,
+                             int nrhs, int col, double* __restrict__ rhs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < np) rhs[(size_t)i * nrhs + col] = (i < n) ? d[i] * (sgn * v[i]) : 0.0;
+}
+void launch_scaled_col(hipStream_t s, const double* d, const double* v, double sgn, int n, int np, int nrhs, int col,
+                       double* rhs) {
+  k_scaled_col<<<(np + 255) / 256, 256, 0, s>>>(d, v, sgn, n, np, nrhs, col, rhs);
+}
+
+// B = Aeq diag(d) (p x ld), and rhs[i][a] = B[a][i]   (KKTSystem.scala:238, :116-118)
+__global__ void k_kkt_prep(const double* __restrict__ Aeq, int ld, int p, int n, int np, const double* __restrict__ d,
+                           double* __restrict__ B, double* __restrict__ rhs, int nrhs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np) return;
+  for (int a = 0; a < p; ++a) {
+    const double b = (i < n) ? d[i] * Aeq[(size_t)a * ld + i] : 0.0;
+    B[(size_t)a * ld + i] = b;
+    rhs[(size_t)i * nrhs + a] = b;
+  }
+}
+void launch_kkt_prep(hipStream_t s, const double* Aeq, int ld, int p, int n, int np, const double* d, double* B,
+                     double* rhs, int nrhs) {
+  k_kkt_prep<<<(np + 255) / 256, 256, 0, s>>>(Aeq, ld, p, n, np, d, B, rhs, nrhs);
+}
+
+// out = u + alpha*v elementwise with a strided source column: out_i = u_i + alpha * v[i*vs + vc]
+__global__ void k_axpy_strided(const double* __restrict__ u, const double* __restrict__ v, int vs, int vc,
+                               double alpha, int n, double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (u ? u[i] : 0.0) + alpha * v[(size_t)i * vs + vc];
+}
+void launch_axpy_strided(hipStream_t s, const double* u, const double* v, int vs, int vc, double alpha, int n,
+                         double* out) {
+  k_axpy_strided<<<(n + 255) / 256, 256, 0, s>>>(u, v, vs, vc, alpha, n, out);
+}
+
+// out_i = d_i * v[i*vs + vc]
+__global__ void k_scale_strided(const double* __restrict__ d, const double* __restrict__ v, int vs, int vc, int n,
+                                double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = d[i] * v[(size_t)i * vs + vc];
+}
+void launch_scale_strided(hipStream_t s, const double* d, const double* v, int vs, int vc, int n, double* out) {
+  k_scale_strided<<<(n + 255) / 256, 256, 0, s>>>(d, v, vs, vc, n, out);
+}
+
+// H += Aeq' Aeq (KKT fallback K = H + A'A, KKTSystem.scala:57), full symmetric update, p small.
+__global__ void k_add_ata(double* __restrict__ H, int ld, const double* __restrict__ Aeq, int p, int n) {
+  const int i = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || j >= n) return;
+  double s = 0.0;
+  for (int a = 0; a < p; ++a) s += Aeq[(size_t)a * ld + i] * Aeq[(size_t)a * ld + j];
+  H[(size_t)i * ld + j] += s;
+}
+void launch_add_ata(hipStream_t s, double* H, int ld, const double* Aeq, int p, int n) {
+  dim3 grid((n + 255) / 256, n);
+  k_add_ata<<<grid, 256, 0, s>>>(H, ld, Aeq, p, n);
+}
+
+// z = q - A' b  (KKTSystem.scala:58)
+__global__ void k_q_minus_atb(const double* __restrict__ q, const double* __restrict__ Aeq, int ld, int p,
+                              const double* __restrict__ b, int n, double* __restrict__ z) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int a = 0; a < p; ++a) s += Aeq[(size_t)a * ld + i] * b[a];
+  z[i] = q[i] - s;
+}
+void launch_q_minus_atb(hipStream_t s, const double* q, const double* Aeq, int ld, int p, const double* b, int n,
+                        double* z) {
+  k_q_minus_atb<<<(n + 255) / 256, 256, 0, s>>>(q, Aeq, ld, p, b, n, z);
+}
+
+// y = B' w + u (n), B p x ld
+__global__ void k_btw_plus(const double* __restrict__ B, int ld, int p, const double* __restrict__ w,
+                           const double* __restrict__ u, int n, double* __restrict__ y) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = u ? u[i] : 0.0;
+  for (int a = 0; a < p; ++a) s += B[(size_t)a * ld + i] * w[a];
+  y[i] = s;
+}
+void launch_btw_plus(hipStream_t s, const double* B, int ld, int p, const double* w, const double* u, int n,
+                     double* y) {
+  k_btw_plus<<<(n + 255) / 256, 256, 0, s>>>(B, ld, p, w, u, n, y);
+}
+
+}  // namespace cvxg

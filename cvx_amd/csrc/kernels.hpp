@@ -1,0 +1,94 @@
+// kernels.hpp — host-side launch wrappers for the HIP kernels of the barrier engine.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+
+namespace cvxg {
+
+struct TileList {
+  const int* ij;  // device array of packed (I<<16 | J), J <= I
+  int count;
+};
+
+// ---- GEMV-like streaming kernels (k_vec.hip) -----------------------------------------------------
+// Constraint evaluation at x: c = r + A x, d = ub - c, invd = 1/d, w = 1/(d*d), logd = log d and
+// the infeasible / not-strict counters in ctrl (LinearConstraint.scala:22-24, BarrierSolver.scala:283-312,
+// Constraint.scala:23).
+void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int n_cols, const double* x,
+                            const double* r, const double* ub, double* c, double* d, double* invd,
+                            double* w, double* logd, DevCtrl* ctrl);
+// y = M v (row-major, one wave per row); rows, cols multiples of 128 / any.
+void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y);
+// part[chunk][j] = sum_{i in chunk} M[i][j] v[i]  (chunks of 64 rows)
+void launch_coldot_partials(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
+                            double* part);
+// y_j = t*(a0_j + Px_j) + sum_chunks part[chunk][j]   (gradientBarrierFunction, BarrierSolver.scala:291-301)
+void launch_gradient_finalize(hipStream_t s, const double* a0, const double* Px, const double* part,
+                              int nchunks, int n_cols, const DevCtrl* ctrl, double* y);
+// single-block deterministic sums into ctrl->sc[slot]
+void launch_dot(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot);
+void launch_sum(hipStream_t s, const double* u, int n, DevCtrl* ctrl, int slot);
+// out = u + v*alpha (alpha read from device scalar pointer or host value)
+void launch_axpy(hipStream_t s, const double* u, const double* v, double alpha, int n, double* out);
+void launch_scale_vec(hipStream_t s, const double* u, const double* d, int n, double* out);  // out = d*u
+
+// ---- Ruiz equilibration + Q formation ------------------------------------------------------------
+void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl);
+void launch_ruiz_sweep(hipStream_t s, const double* H, int ld, int n, const double* dcur, double* dnext,
+                       DevCtrl* ctrl, int k);
+void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl);
+// L[i][j] = d_i d_j H_ij (+reg on the diagonal), lower triangle; padded diagonal = 1.
+void launch_form_q(hipStream_t s, const double* H, double* L, int ld, int n, int np, const double* d,
+                   const DevCtrl* ctrl);
+void launch_add_diag(hipStream_t s, double* H, int ld, int n, double v);
+void launch_copy_diag(hipStream_t s, const double* H, int ld, int n, double* out);
+void launch_set_diag(hipStream_t s, double* H, int ld, int n, const double* diag);
+
+// ---- MFMA SYRK (k_syrk.hip) -----------------------------------------------------------------------
+// H = t*P + A' diag(w) A over the lower tile list; split-K when nsplit > 1 (partials + ordered reduce).
+void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double* w, int mp, const double* P,
+                          const DevCtrl* ctrl, double* H, int ldh, TileList tiles, int nsplit, double* partials);
+// Cholesky trailing update: C[r0:, r0:] (lower tiles) -= Pn Pn', Pn = C[r0:, k0:k0+64]
+void launch_syrk_update(hipStream_t s, double* C, int ld, int np, int k0, const DevCtrl* ctrl);
+
+// ---- Cholesky (k_chol.hip) ------------------------------------------------------------------------
+void launch_potrf_diag(hipStream_t s, double* L, int ld, int k, double* rhs, int nrhs, DevCtrl* ctrl);
+void launch_trsm_panel(hipStream_t s, double* L, int ld, int np, int k, double* rhs, int nrhs,
+                       const DevCtrl* ctrl);
+void launch_trtri_diag(hipStream_t s, const double* L, int ld, int nblk, double* Linv, const DevCtrl* ctrl);
+void launch_bwd_step(hipStream_t s, const double* L, int ld, const double* Linv, int k, double* rhs,
+                     double* out, int nrhs, const DevCtrl* ctrl);
+
+// ---- line search ----------------------------------------------------------------------------------
+// For trials k in [0, LS_TRIALS): t_k = tbase*beta^k; g_i = c_i + t_k e_i; per-block partials of
+// (#violations of g*(1+3e-16)<ub, #(ub-g<=0), sum log(ub-g)).
+void launch_ls_trials(hipStream_t s, const double* c, const double* e, const double* ub, int m, double tbase,
+                      double beta, double* part_log, int* part_cnt);
+void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_cnt, int nblocks,
+                        double* out_log, int* out_cnt);
+int ls_blocks(int m);
+
+// ---- KKT Schur complement (p > 0) ------------------------------------------------------------------
+void launch_kkt_schur(hipStream_t s, const double* X, int nrhs, const double* B, int ldb, int p, int n,
+                      const double* bvec, double* w_out, double* xsol, DevCtrl* ctrl);
+
+}  // namespace cvxg
+
+namespace cvxg {
+void launch_ctrl_set(hipStream_t s, DevCtrl* ctrl, int which, double v);
+void launch_ctrl_reset_eval(hipStream_t s, DevCtrl* ctrl);
+void launch_ctrl_reset_chol(hipStream_t s, DevCtrl* ctrl);
+void launch_scaled_col(hipStream_t s, const double* d, const double* v, double sgn, int n, int np, int nrhs, int col,
+                       double* rhs);
+void launch_kkt_prep(hipStream_t s, const double* Aeq, int ld, int p, int n, int np, const double* d, double* B,
+                     double* rhs, int nrhs);
+void launch_axpy_strided(hipStream_t s, const double* u, const double* v, int vs, int vc, double alpha, int n,
+                         double* out);
+void launch_scale_strided(hipStream_t s, const double* d, const double* v, int vs, int vc, int n, double* out);
+void launch_add_ata(hipStream_t s, double* H, int ld, const double* Aeq, int p, int n);
+void launch_q_minus_atb(hipStream_t s, const double* q, const double* Aeq, int ld, int p, const double* b, int n,
+                        double* z);
+void launch_btw_plus(hipStream_t s, const double* B, int ld, int p, const double* w, const double* u, int n,
+                     double* y);
+}  // namespace cvxg

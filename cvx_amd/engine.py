@@ -1,0 +1,180 @@
+"""Thin Python handle over one ``cvxg_ctx`` (one context per GPU; see include/cvxg.h)."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _lib as L
+
+
+class CvxgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{L.STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class LinSolveException(CvxgError):
+    """LinSolveException.scala"""
+
+
+class NotConvergedException(CvxgError):
+    """breeze NotConvergedException (cholesky / line search)"""
+
+
+class NotStrictlyFeasible(CvxgError, ValueError):
+    """IllegalArgumentException 'x not strictly feasible' (BarrierSolver.scala:285)"""
+
+
+class UnsolvableSystemException(CvxgError):
+    """UnsolvableSystemException.scala"""
+
+
+_EXC = {L.CVXG_E_LINSOLVE_TOL: LinSolveException, L.CVXG_E_NOT_PD: NotConvergedException,
+        L.CVXG_E_LINESEARCH: NotConvergedException, L.CVXG_E_INFEASIBLE_X: NotStrictlyFeasible,
+        L.CVXG_E_UNSOLVABLE: UnsolvableSystemException}
+
+
+def _dp(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def params_struct(pars) -> L.cvxg_params:
+    return L.cvxg_params(int(pars.maxIter), float(pars.alpha), float(pars.beta), float(pars.tolSolver),
+                         float(pars.tolEqSolve), float(pars.tolFeas), float(pars.delta))
+
+
+class Engine:
+    """One device context holding the packed problem (P, a, r; A, r_i, ub_i; A_eq, b_eq) and the iterate."""
+
+    def __init__(self, n: int, m: int, p: int = 0, device: int = 0):
+        self.lib = L.lib()
+        self.n, self.m, self.p = n, m, p
+        h = C.c_void_p()
+        rc = self.lib.cvxg_create(device, n, m, p, C.byref(h))
+        self.h = h
+        if rc != 0:
+            msg = self.lib.cvxg_last_error(h).decode() if h.value else ""
+            if h.value:
+                self.lib.cvxg_destroy(h)
+                self.h = C.c_void_p()
+            raise CvxgError(rc, f"cvxg_create(n={n}, m={m}, p={p}) failed: {msg}")
+
+    def close(self):
+        if self.h is not None and self.h.value:
+            self.lib.cvxg_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != 0:
+            msg = self.lib.cvxg_last_error(self.h).decode()
+            raise _EXC.get(rc, CvxgError)(rc, msg)
+
+    # --- packing ---------------------------------------------------------------------------------
+    def set_objective(self, a0, r0: float = 0.0, P=None):
+        a0 = _f64(a0)
+        if P is not None:
+            P = _f64(P)
+            self._check(self.lib.cvxg_set_objective(self.h, _dp(P), P.shape[1], _dp(a0), float(r0)))
+        else:
+            self._check(self.lib.cvxg_set_objective(self.h, None, 0, _dp(a0), float(r0)))
+        self._keep_obj = (a0, P)
+
+    def set_ineq(self, A, r, ub):
+        A, r, ub = _f64(A), _f64(r), _f64(ub)
+        self._check(self.lib.cvxg_set_ineq(self.h, _dp(A), A.shape[1] if A.ndim == 2 else self.n, 1, _dp(r), _dp(ub)))
+
+    def set_eq(self, Aeq, beq):
+        Aeq, beq = _f64(Aeq), _f64(beq)
+        self._check(self.lib.cvxg_set_eq(self.h, _dp(Aeq), Aeq.shape[1], 1, _dp(beq)))
+
+    def load_problem(self, spec: dict):
+        self.set_objective(spec["a0"], spec.get("r0", 0.0), spec.get("P"))
+        self.set_ineq(spec["A"], spec["r"], spec["ub"])
+        if self.p > 0:
+            self.set_eq(spec["Aeq"], spec["beq"])
+
+    def set_x(self, x):
+        x = _f64(x)
+        self._check(self.lib.cvxg_set_x(self.h, _dp(x)))
+
+    def get_x(self) -> np.ndarray:
+        x = np.zeros(self.n)
+        self._check(self.lib.cvxg_get_x(self.h, _dp(x)))
+        return x
+
+    # --- oracles ---------------------------------------------------------------------------------
+    def barrier_eval(self, t: float, x, want_grad=True, want_hess=False):
+        x = _f64(x)
+        f = C.c_double()
+        g = np.zeros(self.n) if want_grad else None
+        H = np.zeros((self.n, self.n)) if want_hess else None
+        self._check(self.lib.cvxg_barrier_eval(self.h, float(t), _dp(x), C.byref(f), _dp(g), _dp(H)))
+        return f.value, g, H
+
+    def constraint_values(self, x) -> np.ndarray:
+        x = _f64(x)
+        g = np.zeros(self.m)
+        self._check(self.lib.cvxg_constraint_values(self.h, _dp(x), _dp(g)))
+        return g
+
+    def active_set(self, x, tol: float = 1e-12) -> np.ndarray:
+        x = _f64(x)
+        idx = np.zeros(max(self.m, 1), dtype=np.int32)
+        cnt = C.c_int()
+        self._check(self.lib.cvxg_active_set(self.h, _dp(x), float(tol),
+                                             idx.ctypes.data_as(C.POINTER(C.c_int)), C.byref(cnt)))
+        return idx[:cnt.value].copy()
+
+    # --- hot path --------------------------------------------------------------------------------
+    def newton_direction(self, pars, t: float, x):
+        x = _f64(x)
+        dx = np.zeros(self.n)
+        w = np.zeros(max(self.p, 1))
+        info = L.cvxg_step_info()
+        ps = params_struct(pars)
+        self._check(self.lib.cvxg_newton_direction(self.h, C.byref(ps), float(t), _dp(x), _dp(dx), _dp(w),
+                                                   C.byref(info)))
+        return dx, w[:self.p], info
+
+    def centering_begin(self, t: float):
+        self._check(self.lib.cvxg_centering_begin(self.h, float(t)))
+
+    def newton_step(self, pars) -> L.cvxg_step_info:
+        info = L.cvxg_step_info()
+        ps = params_struct(pars)
+        self._check(self.lib.cvxg_newton_step(self.h, C.byref(ps), C.byref(info)))
+        return info
+
+    def centering(self, pars, t: float) -> L.cvxg_centering_info:
+        info = L.cvxg_centering_info()
+        ps = params_struct(pars)
+        self._check(self.lib.cvxg_centering(self.h, C.byref(ps), float(t), C.byref(info)))
+        return info
+
+    def barrier_solve(self, pars, termination: int = 0) -> L.cvxg_solution:
+        sol = L.cvxg_solution()
+        ps = params_struct(pars)
+        self._check(self.lib.cvxg_barrier_solve(self.h, C.byref(ps), int(termination), C.byref(sol)))
+        return sol
+
+    def set_timing(self, on: bool):
+        self._check(self.lib.cvxg_set_timing(self.h, 1 if on else 0))
+
+    def phase_times(self) -> np.ndarray:
+        ms = np.zeros(8)
+        self._check(self.lib.cvxg_get_phase_times(self.h, _dp(ms), 8))
+        return ms

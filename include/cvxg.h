@@ -1,0 +1,171 @@
+/*
+ * cvxg.h — C-ABI of the MI355X dense barrier Newton-step engine (drop-in boundary).
+ *
+ * Plain pointers, sizes and status codes; no torch or HIP types.  Every entry point below names the
+ * reference interface (spyqqqdia/cvx, Scala 2.11 + Breeze 0.10) it replaces; INTEGRATION.md shows the
+ * JNI binding a maintainer adds on the Scala side (GpuBarrierSolver).
+ *
+ * Ownership: the caller owns every host array and the engine only reads / writes it during the call
+ * (never retained).  The context owns all device buffers.  One context per GPU, not thread-safe; calls
+ * are synchronous on return.  Matrices are dense FP64 with an explicit leading dimension; `row_major`
+ * selects the layout (Breeze DenseMatrix is column-major, so a JVM caller passes row_major = 0, or 1
+ * for a transposed view).
+ */
+#ifndef CVXG_H
+#define CVXG_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes: the JNI shim maps them back to the reference's exceptions so its fallback chains
+ *  keep working. */
+#define CVXG_OK 0
+#define CVXG_E_NOT_PD 1          /* breeze NotConvergedException from cholesky (dpotrf info>0), MatrixUtils.scala:456 */
+#define CVXG_E_LINSOLVE_TOL 2    /* LinSolveException, MatrixUtils.scala:507 / KKTSystem.scala:164 */
+#define CVXG_E_INFEASIBLE_X 3    /* IllegalArgumentException "x not strictly feasible", BarrierSolver.scala:285 */
+#define CVXG_E_LINESEARCH 4      /* NotConvergedException from line search, UnconstrainedSolver.scala:94,109 */
+#define CVXG_E_UNSOLVABLE 5      /* UnsolvableSystemException, MatrixUtils.scala:631,698 */
+#define CVXG_E_DIM 6             /* assert dimension mismatch */
+#define CVXG_E_HIP 7             /* HIP runtime / device error */
+#define CVXG_E_ARG 8             /* invalid argument or call order */
+#define CVXG_E_UNSUPPORTED 9     /* configuration outside this build (e.g. p > CVXG_MAX_EQ) */
+
+#define CVXG_MAX_EQ 8            /* equality rows handled by the on-device KKT Schur path */
+
+typedef struct cvxg_ctx cvxg_ctx;
+
+/* Mirrors SolverParams (SolverParams.scala:24-46). */
+typedef struct cvxg_params {
+  int maxIter;        /* 1000 */
+  double alpha;       /* 0.04  line-search descent factor */
+  double beta;        /* 0.8   line-search backtrack factor */
+  double tolSolver;   /* 1e-8  gap / decrement / gradient tolerance */
+  double tolEqSolve;  /* 1e-1  relative residual tolerance of the KKT solve */
+  double tolFeas;     /* 1e-7 */
+  double delta;       /* 1e-6 */
+} cvxg_params;
+
+/* One inner Newton iteration (UnconstrainedSolver.scala:47-134 / EqualityConstrainedSolver.scala:61-110). */
+typedef struct cvxg_step_info {
+  double t;                 /* barrier parameter */
+  double f;                 /* barrier value at x (BarrierSolver.scala:280-289) */
+  double norm_grad;         /* |grad| at x */
+  double q;                 /* dx . grad */
+  double newton_decrement;  /* -q/2 */
+  double hnorm;             /* sqrt(-q) = |dx|_H */
+  double trust_radius;      /* frozen at iteration 0 (rho = 1+1/4 == 1) */
+  double step;              /* accepted backtracking factor t = beta^k (0 if no step was taken) */
+  double rel_err;           /* relativeSize(H dx + grad, -grad, tolEqSolve) of the accepted solve */
+  double min_diag;          /* min diag(L) of the accepted Cholesky factor */
+  double norm_grad_new;     /* |grad| at the new x */
+  double equality_gap;      /* |b - A x| at the new x (p > 0) */
+  int backtracks_c;         /* halvings until x + t s in C */
+  int backtracks_armijo;    /* further halvings for sufficient decrease */
+  int fallback;             /* 0 choleskySolve(H), 1 choleskySolve(H+1e-9 I) / solvePD(H+A'A), 2 symSolve / kktSymSolve */
+  int ruiz_sweeps;          /* Ruiz iterations executed */
+  int regularized;          /* regularizedCholesky used Q + 1e-10 I */
+  int took_step;            /* 1 if x moved */
+  int done;                 /* 1 if the centering loop terminates after this iteration */
+  int iter;                 /* inner iteration index */
+} cvxg_step_info;
+
+/* UnconstrainedSolver / EqualityConstrainedSolver result (Solution.scala:32-43). */
+typedef struct cvxg_centering_info {
+  int iter;
+  int maxed_out;
+  double newton_decrement;
+  double norm_grad;
+  double equality_gap;
+} cvxg_centering_info;
+
+/* BarrierSolver.solve result (BarrierSolver.scala:113-116, 173-176). */
+typedef struct cvxg_solution {
+  double duality_gap;
+  double equality_gap;
+  double newton_decrement;
+  double norm_grad;
+  double objective;         /* objF.valueAt(x) at the returned x */
+  int iter;                 /* inner iterations of the LAST centering (reference semantics) */
+  int maxed_out;
+  int outer_iters;          /* t-loop passes */
+  int newton_steps;         /* total inner Newton iterations (instrumentation the reference lacks) */
+} cvxg_solution;
+
+/* ---- context ------------------------------------------------------------------------------------ */
+
+/* Allocate a context on HIP device `device` for n variables, m linear inequalities, p equalities. */
+int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out);
+void cvxg_destroy(cvxg_ctx* ctx);
+const char* cvxg_last_error(const cvxg_ctx* ctx);
+/* Library version / build string (for logs). */
+const char* cvxg_version(void);
+
+/* ---- packing of the reference's callback objects ------------------------------- */
+
+/* QuadraticObjectiveFunction(dim, r, a, P) (QuadraticObjectiveFunction.scala:7-33); P == NULL gives
+ * LinearObjectiveFunction(dim, r, a) (LinearObjectiveFunction.scala:7-21).  P must be symmetric. */
+int cvxg_set_objective(cvxg_ctx* ctx, const double* P, int ldP, const double* a, double r);
+
+/* The LinearConstraint list r_i + a_i.x <= ub_i (LinearConstraint.scala:7-32), A row i = a_i in LIST
+ * order (fold and forall order matter: BarrierSolver.scala:280-315, ConstraintSet.scala:34-38). */
+int cvxg_set_ineq(cvxg_ctx* ctx, const double* A, int ldA, int row_major, const double* r,
+                  const double* ub);
+
+/* EqualityConstraint(A, b) (EqualityConstraint.scala:16). */
+int cvxg_set_eq(cvxg_ctx* ctx, const double* Aeq, int ldAeq, int row_major, const double* beq);
+
+/* Current iterate (device resident between calls): ConstraintSet.feasiblePoint / Solution.x. */
+int cvxg_set_x(cvxg_ctx* ctx, const double* x);
+int cvxg_get_x(cvxg_ctx* ctx, double* x);
+
+/* ---- barrier oracles ---------------------------------------------------------------------------- */
+
+/* BarrierSolver.barrierFunction / gradientBarrierFunction / hessianBarrierFunction
+ * (BarrierSolver.scala:280-315) at (t, x).  g and H may be NULL; H is written n x n column-major
+ * (symmetric).  Returns CVXG_E_INFEASIBLE_X when some d_i = ub_i - g_i(x) <= 0. */
+int cvxg_barrier_eval(cvxg_ctx* ctx, double t, const double* x, double* f, double* g, double* H);
+
+/* ConstraintSet.constraintFunctionAt without the -ub: g_i(x) = r_i + a_i.x (LinearConstraint.scala:22-24). */
+int cvxg_constraint_values(cvxg_ctx* ctx, const double* x, double* gx);
+
+/* Constraint.isActive (Constraint.scala:26): indices i with |g_i(x) - ub_i| < tol, ascending. */
+int cvxg_active_set(cvxg_ctx* ctx, const double* x, double tol, int* idx, int* count);
+
+/* ---- the hot path -------------------------------------------------------------------------------- */
+
+/* Newton direction at (t, x) without the line search: MatrixUtils.choleskySolve(H, -grad) with its
+ * UnconstrainedSolver fallbacks (UnconstrainedSolver.scala:54-67) when p == 0, KKTSystem.solve
+ * (KKTSystem.scala:43-66) when p > 0.  dx[n]; w[p] may be NULL. */
+int cvxg_newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x,
+                          double* dx, double* w, cvxg_step_info* info);
+
+/* Start the inner solver at barrier parameter t from the current iterate (new UnconstrainedSolver /
+ * EqualityConstrainedSolver, BarrierSolver.scala:97,154). */
+int cvxg_centering_begin(cvxg_ctx* ctx, double t);
+
+/* One inner Newton iteration on the device-resident iterate: assemble, equilibrate, factor, solve,
+ * line search, update (UnconstrainedSolver.scala:47-134 or EqualityConstrainedSolver.scala:60-111).
+ * info->done reports the loop condition for the next iteration. */
+int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info);
+
+/* The whole inner loop (UnconstrainedSolver.solve / EqualityConstrainedSolver.solve). */
+int cvxg_centering(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg_centering_info* info);
+
+/* BarrierSolver.solve / solveSpecial (BarrierSolver.scala:70-188): the t-loop (mu = 10, t0 = 1) from
+ * the current iterate.  termination: 0 = CvxUtils.standardTerminationCriterion, 1 =
+ * CvxUtils.phase_I_TerminationCriterion (CvxUtils.scala:61-87). */
+int cvxg_barrier_solve(cvxg_ctx* ctx, const cvxg_params* pars, int termination, cvxg_solution* sol);
+
+/* ---- instrumentation ----------------------------------------------------------------------------- */
+
+/* Per-phase device time of the last cvxg_newton_step (ms), measured with HIP events on the ctx
+ * stream when timing is enabled: [0] assembly (GEMVs+SYRK) [1] Ruiz+scale [2] Cholesky (+fused forward
+ * solve) [3] backward solve + residual [4] line search [5] SYRK kernel alone. */
+int cvxg_set_timing(cvxg_ctx* ctx, int enabled);
+int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CVXG_H */

@@ -1,0 +1,67 @@
+"""CPU-only checks of the drop-in boundary: libcvxg.so loads and exports exactly the C-ABI of include/cvxg.h."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "cvxg.h")
+
+
+def _header_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(cvxg_[a-z_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from cvx_amd import build as B
+    B.build(force=False, verbose=False)
+    from cvx_amd import _lib
+    return _lib.load()
+
+
+def test_header_declares_entry_points():
+    syms = _header_symbols()
+    for s in ["cvxg_create", "cvxg_destroy", "cvxg_set_objective", "cvxg_set_ineq", "cvxg_set_eq",
+              "cvxg_newton_step", "cvxg_centering", "cvxg_barrier_solve", "cvxg_barrier_eval",
+              "cvxg_newton_direction", "cvxg_last_error"]:
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol(lib):
+    from cvx_amd import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (cvxg_\w+)", out))
+    missing = [s for s in _header_symbols() if s not in exported]
+    assert not missing, missing
+    assert set(_header_symbols()) == set(_lib.SIGNATURES), "ctypes table must mirror the header"
+
+
+def test_version_and_no_gpu_behaviour(lib):
+    import ctypes as C
+    assert b"gfx950" in lib.cvxg_version()
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("GPU present: covered by the gpu tests")
+    h = C.c_void_p()
+    rc = lib.cvxg_create(0, 8, 8, 0, C.byref(h))
+    assert rc != 0  # CVXG_E_HIP without a device, no crash, no CPU fallback
+    msg = lib.cvxg_last_error(h)
+    assert msg is not None
+    if h.value:
+        lib.cvxg_destroy(h)
+
+
+def test_bad_arguments_rejected(lib):
+    import ctypes as C
+    from cvx_amd import _lib
+    h = C.c_void_p()
+    assert lib.cvxg_create(0, 0, 4, 0, C.byref(h)) == _lib.CVXG_E_DIM
+    assert lib.cvxg_create(0, 4, 4, _lib.CVXG_MAX_EQ + 1, C.byref(h)) == _lib.CVXG_E_UNSUPPORTED
+    assert lib.cvxg_newton_step(None, None, None) == _lib.CVXG_E_ARG
