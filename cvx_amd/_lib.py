@@ -74,7 +74,7 @@ SIGNATURES = {
     "cvxg_barrier_eval": (C.c_int, [_P, C.c_double, _D, _D, _D, _D]),
     "cvxg_constraint_values": (C.c_int, [_P, _D, _D]),
     "cvxg_active_set": (C.c_int, [_P, _D, C.c_double, _I, _I]),
-    "cvxg_newton_direction": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, _D, _D, _D,
+    "cvxg_newton_direction": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, _D, _D, _D, _D,
                                         C.POINTER(cvxg_step_info)]),
     "cvxg_centering_begin": (C.c_int, [_P, C.c_double]),
     "cvxg_newton_step": (C.c_int, [_P, C.POINTER(cvxg_params), C.POINTER(cvxg_step_info)]),
@@ -86,6 +86,12 @@ SIGNATURES = {
 
 
 def load(path: str = LIB_PATH) -> C.CDLL:
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7).  Loading torch
+    # first lets libcvxg.so bind to that same runtime, so torch tensors, RCCL and the engine share devices.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(path):
         raise ImportError(f"cvx_amd: HIP library {path} is not built (run __graft_entry__.build()); "
                           "there is no CPU fallback")

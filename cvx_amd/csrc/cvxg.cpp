@@ -756,8 +756,8 @@ int cvxg_active_set(cvxg_ctx* ctx, const double* x, double tol, int* idx, int* c
   return CVXG_OK;
 }
 
-int cvxg_newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, double* dx, double* w,
-                          cvxg_step_info* info) {
+int cvxg_newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, const double* grad,
+                          double* dx, double* w, cvxg_step_info* info) {
   if (!ctx || !pars || !x) return CVXG_E_ARG;
   HIPC(ctx, hipSetDevice(ctx->dev));
   CHK(check_ready(ctx));
@@ -767,6 +767,14 @@ int cvxg_newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, cons
   CHK(cvxg_set_x(ctx, x));
   CHK(set_t(ctx, t));
   CHK(eval_at_x(ctx));
+  if (grad) {  // caller-supplied gradient (e.g. the host's y of UnconstrainedSolver.scala:44,131)
+    std::vector<double> g(grad, grad + ctx->n);
+    double gg = 0.0;
+    for (double v : g) gg += v * v;
+    CHK(upload_vec(ctx, ctx->y, g.data(), ctx->n, ctx->np));
+    ctx->normGrad = sqrt(gg);
+    ctx->x_eval_valid = 0;
+  }
   info->t = t;
   info->f = ctx->f_at_x;
   info->norm_grad = ctx->normGrad;

@@ -140,13 +140,14 @@ class Engine:
         return idx[:cnt.value].copy()
 
     # --- hot path --------------------------------------------------------------------------------
-    def newton_direction(self, pars, t: float, x):
+    def newton_direction(self, pars, t: float, x, grad=None):
         x = _f64(x)
+        g = None if grad is None else _f64(grad)
         dx = np.zeros(self.n)
         w = np.zeros(max(self.p, 1))
         info = L.cvxg_step_info()
         ps = params_struct(pars)
-        self._check(self.lib.cvxg_newton_direction(self.h, C.byref(ps), float(t), _dp(x), _dp(dx), _dp(w),
+        self._check(self.lib.cvxg_newton_direction(self.h, C.byref(ps), float(t), _dp(x), _dp(g), _dp(dx), _dp(w),
                                                    C.byref(info)))
         return dx, w[:self.p], info
 

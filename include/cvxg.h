@@ -136,9 +136,11 @@ int cvxg_active_set(cvxg_ctx* ctx, const double* x, double tol, int* idx, int* c
 
 /* Newton direction at (t, x) without the line search: MatrixUtils.choleskySolve(H, -grad) with its
  * UnconstrainedSolver fallbacks (UnconstrainedSolver.scala:54-67) when p == 0, KKTSystem.solve
- * (KKTSystem.scala:43-66) when p > 0.  dx[n]; w[p] may be NULL. */
+ * (KKTSystem.scala:43-66) when p > 0.  grad may be NULL (then the engine's own barrier gradient at
+ * (t, x) is used) or the caller's gradient (the reference passes `y` computed by the host).
+ * dx[n]; w[p] may be NULL. */
 int cvxg_newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x,
-                          double* dx, double* w, cvxg_step_info* info);
+                          const double* grad, double* dx, double* w, cvxg_step_info* info);
 
 /* Start the inner solver at barrier parameter t from the current iterate (new UnconstrainedSolver /
  * EqualityConstrainedSolver, BarrierSolver.scala:97,154). */

@@ -45,7 +45,7 @@ def test_barrier_oracles_match(mods, n, m):
     pb = _opb(O, spec)
     eng = _engine(Engine, spec)
     rng = np.random.default_rng(3)
-    x = 0.01 * rng.standard_normal(n)
+    x = 1e-3 * rng.standard_normal(n) / np.sqrt(n)
     for t in (1.0, 37.5, 1e4):
         f, g, H = eng.barrier_eval(t, x, want_grad=True, want_hess=True)
         fr = O.barrier_value(pb, t, x)
@@ -83,8 +83,10 @@ def test_newton_direction_vs_oracle(mods, n, m):
     pars = SP.standardParams()
     x = spec["x0"]
     for t in (1.0, 1e2, 1e4):
-        dx, _, info = eng.newton_direction(pars, t, x)
         y = O.barrier_gradient(pb, t, x)
+        dx, _, info = eng.newton_direction(pars, t, x, grad=y)
+        dx_own, _, _ = eng.newton_direction(pars, t, x)  # engine's own gradient (no cancellation at x0)
+        assert np.linalg.norm(dx_own - dx) <= 1e-10 * np.linalg.norm(dx)
         rec = O.NewtonStepRecord(x=x, grad=y, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
         dref = O.newton_direction(pb, t, x, y, pars.tolEqSolve, rec)
         rel = np.linalg.norm(dx - dref) / np.linalg.norm(dref)
@@ -112,7 +114,9 @@ def test_golden_newton_steps(mods, path):
     worst = 0.0
     for k in range(nsteps):
         t, x = float(fx["t"][k]), fx["x"][k]
-        dx, _, info = eng.newton_direction(pars, t, x)
+        # identical inputs: the oracle's (t, x, grad) -- the gradient near a centred point is a sum of
+        # large terms that cancels to ~tol, so two FP64 summation orders differ there (checked below).
+        dx, _, info = eng.newton_direction(pars, t, x, grad=fx["grad"][k])
         dref = fx["dx"][k]
         rel = np.linalg.norm(dx - dref) / np.linalg.norm(dref)
         if t <= 1e4:
@@ -120,6 +124,28 @@ def test_golden_newton_steps(mods, path):
         worst = max(worst, rel if t <= 1e4 else 0.0)
         # the decrement decides loop termination: same side of tol
         assert (-info.q / 2 > pars.tolSolver) == (-fx["q"][k] / 2 > pars.tolSolver) or abs(info.q - fx["q"][k]) < 1e-12
+    eng.close()
+
+
+@pytest.mark.parametrize("path", _fixtures(), ids=lambda p: os.path.basename(p))
+def test_golden_gradients(mods, path):
+    """Engine gradient at every golden (t, x) vs the oracle's fold, bounded by the cancellation scale
+    eps * (t|a+Px| + sum_i |a_i|/d_i) of the terms that are summed (componentwise, 64 eps)."""
+    Z, SP, Engine, O = mods
+    fx = dict(np.load(path))
+    spec = dict(a0=fx["a0"], r0=float(fx["r0"]), P=fx.get("P"), A=fx["A"], r=fx["r"], ub=fx["ub"],
+                Aeq=fx.get("Aeq"), beq=fx.get("beq"))
+    eng = _engine(Engine, spec)
+    for k in range(fx["t"].shape[0]):
+        t, x = float(fx["t"][k]), fx["x"][k]
+        f, g, _ = eng.barrier_eval(t, x)
+        d = spec["ub"] - (spec["r"] + spec["A"] @ x)
+        obj = np.abs(spec["a0"] + (spec["P"] @ x if spec["P"] is not None else 0.0)) * t
+        scale = obj + np.abs(spec["A"]).T @ (1.0 / d)
+        assert np.all(np.abs(g - fx["grad"][k]) <= 64 * np.finfo(float).eps * scale + 1e-300)
+        assert abs(f - fx["f"][k]) <= 64 * np.finfo(float).eps * (abs(t * O.objective_value(
+            O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"]), x))
+            + np.sum(np.abs(np.log(d))))
     eng.close()
 
 
