@@ -12,6 +12,7 @@ constexpr int MPAD = 64;      // inequality rows padded to a multiple of this
 constexpr int LS_TRIALS = 64; // backtracking trials evaluated per line-search batch
 constexpr int MAX_RHS = 9;    // 1 + CVXG_MAX_EQ right-hand sides in the fused forward solve
 constexpr int RUIZ_MAX = 20;  // MatrixUtils.scala:247
+constexpr int COLDOT_ROWS = 128;  // row chunk of the A'v column reduction (partials summed in fixed order)
 
 // Device control block: every scalar the graph-captured kernels need lives here, so launches can be
 // replayed with fixed arguments.  A pinned host mirror is read back once per Newton step.

