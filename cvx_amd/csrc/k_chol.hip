@@ -13,100 +13,103 @@
 
 namespace cvxg {
 
+typedef double vd2c __attribute__((ext_vector_type(2)));
+
+// 1/sqrt(p) to full FP64 accuracy: hardware estimate + two Newton steps (no long div/sqrt sequences on
+// the per-column critical path).
+__device__ __forceinline__ double rsqrt_fp64(double p) {
+  double y = __builtin_amdgcn_rsq(p);
+  const double h = 0.5 * p;
+  y = y * (1.5 - h * y * y);
+  y = y * (1.5 - h * y * y);
+  return y;
+}
+
 // ------------------------------------------------------------------------------------------------
-// Diagonal block factorisation: 256 threads as 16x16, thread (tr,tc) owns rows tr+16a, cols tc+16b of
-// the block (e) and of the identity border (ee) in registers.  Step j: owners of column j publish it,
-// everybody updates its trailing entries a_rc -= a_rj a_cj / a_jj (one barrier per step).  Results are
-// collected in LDS and written once at the end.  Non-positive or NaN pivot -> ctrl->chol_info =
-// global index + 1 (dpotrf info > 0).
+// Diagonal block factorisation, row-owned: 3 waves run the same sweep, lane r of wave w owns ONE row of
+// a 64-wide bordered system in 64 registers:
+//   wave 0: row r of the block A_kk (lower part),
+//   wave 1: row r of the identity border  -> row r of (L_kk^-1)^T,
+//   wave 2: rhs column r (lanes < nrhs)    -> w = L_kk^-1 b (fused forward substitution).
+// Step j (unrolled, static register index): wave 0 publishes column j to LDS, one barrier, then every
+// row applies  v_c -= (v_j / l_jj) (a_cj / l_jj)  for c > j and finalises v_j /= l_jj.  One barrier per
+// column, no divisions (rsqrt + Newton), outputs staged through LDS and written once, coalesced.
+// Non-positive / NaN pivot -> ctrl->chol_info = global index + 1 (dpotrf info > 0).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_potrf_diag(double* __restrict__ L, int ld, int k, double* __restrict__ rhs,
+__global__ __launch_bounds__(192) void k_potrf_diag(double* __restrict__ L, int ld, int k, double* __restrict__ rhs,
                                                     int nrhs, double* __restrict__ Linv, DevCtrl* ctrl) {
   if (ctrl->chol_info != 0) return;
-  __shared__ double col[2][NB];
-  __shared__ double colE[2][NB];
-  __shared__ double lfin[NB][NB + 1];
-  __shared__ double linv[NB][NB + 1];
-  __shared__ double rh[MAX_RHS][NB];
-  __shared__ double wfin[MAX_RHS][NB];
-  const int tid = threadIdx.x;
-  const int tr = tid >> 4, tc = tid & 15;
+  __shared__ __attribute__((aligned(16))) double col[NB];
+  __shared__ double stage[NB][NB + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int base = k * NB;
-  double e[4][4], ee[4][4];
+  double v[NB];
+  if (wid == 0) {
+    const double* src = L + (size_t)(base + lane) * ld + base;
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int r = tr + 16 * a, c = tc + 16 * b;
-      e[a][b] = (c <= r) ? L[(size_t)(base + r) * ld + base + c] : 0.0;
-      ee[a][b] = (c == r) ? 1.0 : 0.0;
+    for (int c = 0; c < NB; c += 2) {
+      const vd2c t = *reinterpret_cast<const vd2c*>(src + c);
+      v[c] = (c <= lane) ? t[0] : 0.0;
+      v[c + 1] = (c + 1 <= lane) ? t[1] : 0.0;
     }
-  for (int t = tid; t < nrhs * NB; t += 256) rh[t / NB][t % NB] = rhs[(size_t)(base + t % NB) * nrhs + t / NB];
-  for (int t = tid; t < NB * (NB + 1); t += 256) {
-    (&lfin[0][0])[t] = 0.0;
-    (&linv[0][0])[t] = 0.0;
+  } else if (wid == 1) {
+#pragma unroll
+    for (int c = 0; c < NB; ++c) v[c] = (c == lane) ? 1.0 : 0.0;
+  } else {
+    const int rr = lane < nrhs ? lane : 0;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) v[c] = rhs[(size_t)(base + c) * nrhs + rr];
   }
   double mind = __builtin_inf();
-  __syncthreads();
-
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int buf = j & 1;
-    if (tc == (j & 15)) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int r = tr + 16 * a;
-        col[buf][r] = (r >= j) ? e[a][j >> 4] : 0.0;
-        colE[buf][r] = ee[a][j >> 4];
-      }
-    }
+    if (wid == 0) col[lane] = v[j];  // a_rj (unscaled) of every row
     __syncthreads();
-    const double piv = col[buf][j];
-    if (!(piv > 0.0)) {  // dpotrf info > 0 -> NotConvergedException (uniform across the block)
+    const double piv = col[j];
+    if (!(piv > 0.0)) {  // uniform across the block
       if (tid == 0) atomicCAS(&ctrl->chol_info, 0, base + j + 1);
       return;
     }
-    const double ljj = sqrt(piv);
-    const double rl = 1.0 / ljj;
-    const double ipiv = 1.0 / piv;
-    if (tc == (j & 15)) {
+    const double rl = rsqrt_fp64(piv);
+    mind = fmin(mind, piv * rl);
+    const double lr = v[j] * rl;  // final entry of column j (L_rj, W_rj or w_j)
+    const double lrr = lr * rl;
+    v[j] = lr;
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int r = tr + 16 * a;
-        if (r >= j) lfin[r][j] = (r == j) ? ljj : col[buf][r] * rl;
-        linv[j][r] = colE[buf][r] * rl;  // Linv[j][r] = (L^-1 e_r)_j
+    for (int c = j + 1; c < NB; c += 2) {
+      if (c + 1 < NB) {
+        const vd2c cc = *reinterpret_cast<const vd2c*>(&col[c]);  // broadcast read
+        v[c] = fma(-lrr, cc[0], v[c]);
+        v[c + 1] = fma(-lrr, cc[1], v[c + 1]);
+      } else {
+        v[c] = fma(-lrr, col[c], v[c]);
       }
     }
-    mind = fmin(mind, ljj);
+    __syncthreads();  // col is rewritten by the next step
+  }
+  // stage rows through LDS, write coalesced
+  if (wid == 0) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int r = tr + 16 * a, c = tc + 16 * b;
-        if (c > j) {
-          const double f = col[buf][c] * ipiv;
-          if (c <= r) e[a][b] -= col[buf][r] * f;
-          ee[a][b] -= colE[buf][r] * f;
-        }
-      }
-    for (int t = tid; t < nrhs * NB; t += 256) {
-      const int rho = t / NB, c = t % NB;
-      if (c > j) rh[rho][c] -= rh[rho][j] * (col[buf][c] * ipiv);
-      else if (c == j) wfin[rho][j] = rh[rho][j] * rl;  // w_j
-    }
+    for (int c = 0; c < NB; ++c) stage[lane][c] = v[c];
   }
   __syncthreads();
-  for (int t = tid; t < NB * NB; t += 256) {
+  for (int t = tid; t < NB * NB; t += 192) {
     const int r = t / NB, c = t % NB;
-    if (c <= r) L[(size_t)(base + r) * ld + base + c] = lfin[r][c];
-    Linv[(size_t)k * NB * NB + t] = linv[r][c];
+    if (c <= r) L[(size_t)(base + r) * ld + base + c] = stage[r][c];
   }
-  for (int t = tid; t < nrhs * NB; t += 256) rhs[(size_t)(base + t % NB) * nrhs + t / NB] = wfin[t / NB][t % NB];
+  __syncthreads();
+  if (wid == 1) {  // lane r holds row r of W = (L^-1)^T, i.e. Linv[j][r] = v[j]
+#pragma unroll
+    for (int j = 0; j < NB; ++j) Linv[(size_t)k * NB * NB + j * NB + lane] = v[j];
+  } else if (wid == 2 && lane < nrhs) {
+#pragma unroll
+    for (int c = 0; c < NB; ++c) rhs[(size_t)(base + c) * nrhs + lane] = v[c];
+  }
   if (tid == 0) atomic_min_pos(&ctrl->min_diag, mind);
 }
 
 void launch_potrf_diag(hipStream_t s, double* L, int ld, int k, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl) {
-  k_potrf_diag<<<1, 256, 0, s>>>(L, ld, k, rhs, nrhs, Linv, ctrl);
+  k_potrf_diag<<<1, 192, 0, s>>>(L, ld, k, rhs, nrhs, Linv, ctrl);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -133,8 +136,7 @@ __global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ L, int 
   double* row = L + (size_t)ir * ld + base;
 #pragma unroll
   for (int c = 0; c < NB; c += 2) {
-    typedef double d2 __attribute__((ext_vector_type(2)));
-    const d2 v = *reinterpret_cast<const d2*>(row + c);
+    const vd2c v = *reinterpret_cast<const vd2c*>(row + c);
     a[c] = v[0];
     a[c + 1] = v[1];
   }

@@ -131,7 +131,7 @@ def test_golden_newton_steps(mods, path):
 @pytest.mark.parametrize("path", _fixtures(), ids=lambda p: os.path.basename(p))
 def test_golden_gradients(mods, path):
     """Engine gradient at every golden (t, x) vs the oracle's fold, bounded by the cancellation scale
-    eps * (t|a+Px| + sum_i |a_i|/d_i) of the terms that are summed (componentwise, 64 eps)."""
+    eps * (t(|a|+|P||x|) + sum_i |a_i|/d_i) of the terms that are summed (componentwise)."""
     Z, SP, Engine, O = mods
     fx = dict(np.load(path))
     spec = dict(a0=fx["a0"], r0=float(fx["r0"]), P=fx.get("P"), A=fx["A"], r=fx["r"], ub=fx["ub"],
@@ -140,13 +140,19 @@ def test_golden_gradients(mods, path):
     for k in range(fx["t"].shape[0]):
         t, x = float(fx["t"][k]), fx["x"][k]
         f, g, _ = eng.barrier_eval(t, x)
+        eps = np.finfo(float).eps
         d = spec["ub"] - (spec["r"] + spec["A"] @ x)
         obj = (np.abs(spec["a0"]) + (np.abs(spec["P"]) @ np.abs(x) if spec["P"] is not None else 0.0)) * t
-        scale = obj + np.abs(spec["A"]).T @ (1.0 / d)
-        assert np.all(np.abs(g - fx["grad"][k]) <= 64 * np.finfo(float).eps * scale + 1e-300)
-        assert abs(f - fx["f"][k]) <= 64 * np.finfo(float).eps * (abs(t * O.objective_value(
-            O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"]), x))
-            + np.sum(np.abs(np.log(d))))
+        # first-order error scale: the summed terms, plus the slack d_i = ub_i - g_i(x) (which cancels
+        # near the boundary) propagated through a_i / d_i
+        d_abs_err = np.abs(spec["ub"]) + np.abs(spec["r"]) + np.abs(spec["A"]) @ np.abs(x)
+        scale = obj + np.abs(spec["A"]).T @ (1.0 / d) + np.abs(spec["A"]).T @ (d_abs_err / (d * d))
+        nterms = spec["A"].shape[1] + 16
+        assert np.all(np.abs(g - fx["grad"][k]) <= nterms * eps * scale + 1e-300)
+        f_scale = (abs(t) * (abs(spec["r0"]) + np.abs(spec["a0"]) @ np.abs(x)
+                             + (np.abs(x) @ (np.abs(spec["P"]) @ np.abs(x)) if spec["P"] is not None else 0.0))
+                   + np.sum(np.abs(np.log(d))) + np.sum(d_abs_err / d))
+        assert abs(f - fx["f"][k]) <= nterms * eps * f_scale
     eng.close()
 
 
