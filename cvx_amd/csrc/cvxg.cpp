@@ -9,6 +9,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -61,6 +62,7 @@ struct cvxg_ctx {
   int *ls_pcnt = nullptr, *ls_cnt = nullptr;
   int* tiles = nullptr;
   int ntiles = 0, nsplit = 1;
+  int chol_outer = 4;  // 64-blocks per outer Cholesky panel (trailing update width 256)
   DevCtrl* ctrl = nullptr;
   DevCtrl* hctrl = nullptr;
   double* hls = nullptr;  // pinned: [LS_TRIALS] logs then [2*LS_TRIALS] counts as ints
@@ -223,10 +225,20 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs) {
   launch_ctrl_reset_chol(s, ctx->ctrl);
   launch_form_q(s, ctx->H, ctx->L, ctx->np, ctx->n, ctx->np, ctx->dfin, ctx->ctrl);
   fill_rhs();
-  for (int k = 0; k < ctx->nblk; ++k) {
-    launch_potrf_diag(s, ctx->L, ctx->np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
-    launch_trsm_panel(s, ctx->L, ctx->np, ctx->np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
-    launch_syrk_update(s, ctx->L, ctx->np, ctx->np, k * NB, ctx->ctrl);
+  // Two-level right-looking blocked Cholesky: outer panels of `chol_outer` 64-blocks.  Inside a panel each
+  // block is factored (potrf + fused forward solve), its column below is solved by MFMA TRSM and only the
+  // remaining panel columns are updated (K = 64); the trailing matrix is then updated once with K = the
+  // whole panel width, so it is read-modify-written nblk/chol_outer times instead of nblk times.
+  const int np = ctx->np, ow = ctx->chol_outer;
+  for (int K0 = 0; K0 < ctx->nblk; K0 += ow) {
+    const int K1 = std::min(K0 + ow, ctx->nblk);
+    for (int k = K0; k < K1; ++k) {
+      launch_potrf_diag(s, ctx->L, np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
+      launch_trsm_mfma(s, ctx->L, np, np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
+      if (k + 1 < K1) launch_chol_update(s, ctx->L, np, np, k * NB, NB, (k + 1) * NB, (k + 1) * NB, K1 * NB, ctx->ctrl);
+    }
+    if (K1 < ctx->nblk)
+      launch_chol_update(s, ctx->L, np, np, K0 * NB, (K1 - K0) * NB, K1 * NB, K1 * NB, np, ctx->ctrl);
   }
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
@@ -552,6 +564,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   ctx->np = round_up(n, TILE);
   ctx->mp = round_up(std::max(m, 1), MPAD);
   ctx->nblk = ctx->np / NB;
+  if (const char* e = getenv("CVXG_CHOL_OUTER")) ctx->chol_outer = std::max(1, atoi(e));
   HIPC(ctx, hipSetDevice(device));
   HIPC(ctx, hipStreamCreateWithFlags(&ctx->s, hipStreamNonBlocking));
   const size_t np = ctx->np, mp = ctx->mp;

@@ -14,6 +14,7 @@
 namespace cvxg {
 
 typedef double vd2c __attribute__((ext_vector_type(2)));
+constexpr int TRSM_THREADS = 64;  // 16 rows per workgroup: the panel spreads over ~4x more CUs
 
 // 1/sqrt(p) to full FP64 accuracy: hardware estimate + two Newton steps (no long div/sqrt sequences on
 // the per-column critical path).
@@ -108,7 +109,8 @@ __global__ __launch_bounds__(192) void k_potrf_diag(double* __restrict__ L, int 
   if (tid == 0) atomic_min_pos(&ctrl->min_diag, mind);
 }
 
-void launch_potrf_diag(hipStream_t s, double* L, int ld, int k, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl) {
+void launch_potrf_diag_rowowned(hipStream_t s, double* L, int ld, int k, double* rhs, int nrhs, double* Linv,
+                                DevCtrl* ctrl) {
   k_potrf_diag<<<1, 192, 0, s>>>(L, ld, k, rhs, nrhs, Linv, ctrl);
 }
 
@@ -117,7 +119,7 @@ void launch_potrf_diag(hipStream_t s, double* L, int ld, int k, double* rhs, int
 // Four threads per row (each owns the outputs c = q + 4u), the row in registers, Linv broadcast from
 // LDS.  Fused forward substitution: rhs[i] -= L[i, kb] . w_kb (shuffle-reduced over the 4 threads).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ L, int ld, int np, int k,
+__global__ __launch_bounds__(TRSM_THREADS) void k_trsm_panel(double* __restrict__ L, int ld, int np, int k,
                                                     double* __restrict__ rhs, int nrhs,
                                                     const double* __restrict__ Linv, const DevCtrl* ctrl) {
   if (ctrl->chol_info != 0) return;
@@ -125,11 +127,11 @@ __global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ L, int 
   __shared__ double wk[MAX_RHS][NB];
   const int base = k * NB;
   const double* lsrc = Linv + (size_t)k * NB * NB;
-  for (int t = threadIdx.x; t < NB * NB; t += 256) li[t / NB][t % NB] = lsrc[t];
-  for (int t = threadIdx.x; t < nrhs * NB; t += 256) wk[t / NB][t % NB] = rhs[(size_t)(base + t % NB) * nrhs + t / NB];
+  for (int t = threadIdx.x; t < NB * NB; t += TRSM_THREADS) li[t / NB][t % NB] = lsrc[t];
+  for (int t = threadIdx.x; t < nrhs * NB; t += TRSM_THREADS) wk[t / NB][t % NB] = rhs[(size_t)(base + t % NB) * nrhs + t / NB];
   __syncthreads();
   const int q = threadIdx.x & 3;
-  const int i = base + NB + blockIdx.x * 64 + (threadIdx.x >> 2);
+  const int i = base + NB + blockIdx.x * (TRSM_THREADS / 4) + (threadIdx.x >> 2);
   const bool valid = i < np;
   const int ir = valid ? i : np - 1;
   double a[NB];
@@ -170,7 +172,7 @@ void launch_trsm_panel(hipStream_t s, double* L, int ld, int np, int k, double* 
                        const DevCtrl* ctrl) {
   const int rows = np - (k + 1) * NB;
   if (rows <= 0) return;
-  k_trsm_panel<<<(rows + 63) / 64, 256, 0, s>>>(L, ld, np, k, rhs, nrhs, Linv, ctrl);
+  k_trsm_panel<<<(rows + TRSM_THREADS / 4 - 1) / (TRSM_THREADS / 4), TRSM_THREADS, 0, s>>>(L, ld, np, k, rhs, nrhs, Linv, ctrl);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -58,6 +58,11 @@ void launch_syrk_update(hipStream_t s, double* C, int ld, int np, int k0, const 
 void launch_potrf_diag(hipStream_t s, double* L, int ld, int k, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl);
 void launch_trsm_panel(hipStream_t s, double* L, int ld, int np, int k, double* rhs, int nrhs, const double* Linv,
                        const DevCtrl* ctrl);
+// k_update.hip: MFMA panel TRSM (rows below block k) and the region update of the two-level Cholesky
+void launch_trsm_mfma(hipStream_t s, double* L, int ld, int np, int k, double* rhs, int nrhs, const double* Linv,
+                      const DevCtrl* ctrl);
+void launch_chol_update(hipStream_t s, double* C, int ld, int np, int k0, int kw, int r0, int c0, int c1,
+                        const DevCtrl* ctrl);
 void launch_bwd_step(hipStream_t s, const double* L, int ld, const double* Linv, int k, double* rhs,
                      double* out, int nrhs, const DevCtrl* ctrl);
 
