@@ -62,6 +62,7 @@ struct cvxg_ctx {
   int *ls_pcnt = nullptr, *ls_cnt = nullptr;
   int* tiles = nullptr;
   int ntiles = 0, nsplit = 1;
+  int ntiles_main = 0;  // tiles assembled without K split (whole waves of slots); the rest use nsplit
   int chol_outer = 4;  // 64-blocks per outer Cholesky panel (trailing update width 256)
   DevCtrl* ctrl = nullptr;
   DevCtrl* hctrl = nullptr;
@@ -123,6 +124,14 @@ static void tstop(cvxg_ctx* ctx, int i) {
     (void)hipEventRecord(ctx->tm.ev[i][1], ctx->s);
     ctx->tm.rec[i] = true;
   }
+}
+
+// Copies are ordered on the ctx stream: it is created non-blocking, so a plain hipMemcpy (null stream) would
+// not wait for work queued on it (e.g. dalloc's zero fill) and could be overwritten by it.
+static int copy_sync(cvxg_ctx* ctx, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  HIPC(ctx, hipMemcpyAsync(dst, src, bytes, kind, ctx->s));
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  return CVXG_OK;
 }
 
 static int sync_ctrl(cvxg_ctx* ctx) {
@@ -199,8 +208,16 @@ static double objective_at_x(cvxg_ctx* ctx) {
 
 static int assemble_hessian(cvxg_ctx* ctx) {
   tstart(ctx, 5);
-  launch_syrk_assemble(ctx->s, ctx->A, ctx->np, ctx->w, ctx->mp, ctx->hasP ? ctx->P : nullptr, ctx->ctrl, ctx->H,
-                       ctx->np, TileList{ctx->tiles, ctx->ntiles}, ctx->nsplit, ctx->part);
+  // full tiles in whole waves of workgroup slots, then the leftover tiles split along K across all slots
+  // (partials + ordered reduce) so the last wave is not a handful of tiles on an otherwise idle chip.
+  const double* P = ctx->hasP ? ctx->P : nullptr;
+  if (ctx->ntiles_main > 0)
+    launch_syrk_assemble(ctx->s, ctx->A, ctx->np, ctx->w, ctx->mp, P, ctx->ctrl, ctx->H, ctx->np,
+                         TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->part);
+  if (ctx->ntiles > ctx->ntiles_main)
+    launch_syrk_assemble(ctx->s, ctx->A, ctx->np, ctx->w, ctx->mp, P, ctx->ctrl, ctx->H, ctx->np,
+                         TileList{ctx->tiles + ctx->ntiles_main, ctx->ntiles - ctx->ntiles_main}, ctx->nsplit,
+                         ctx->part);
   tstop(ctx, 5);
   HIPC(ctx, hipGetLastError());
   return CVXG_OK;
@@ -574,7 +591,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   CHK(dalloc(ctx, &ctx->ub, mp));
   {  // padded rows: ub = 1 so d = 1, log d = 0
     std::vector<double> one(mp, 1.0);
-    HIPC(ctx, hipMemcpy(ctx->ub, one.data(), mp * sizeof(double), hipMemcpyHostToDevice));
+    CHK(copy_sync(ctx, ctx->ub, one.data(), mp * sizeof(double), hipMemcpyHostToDevice));
   }
   if (p > 0) {
     CHK(dalloc(ctx, &ctx->Aeq, (size_t)CVXG_MAX_EQ * np));
@@ -596,19 +613,28 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   CHK(dalloc(ctx, &ctx->Linv, (size_t)ctx->nblk * NB * NB));
   CHK(dalloc(ctx, &ctx->rhs, np * MAX_RHS));
   CHK(dalloc(ctx, &ctx->sol, np * MAX_RHS));
-  // SYRK tile list (lower tiles) and split-K factor
+  // SYRK tile list (lower tiles; diagonal tiles first, they carry 3/4 of the work) and the wave plan:
+  // `slots` workgroups run at once (2 per CU); floor(T/slots) whole waves of full-K tiles, then the
+  // remaining tiles are split along K so that they fill one more wave of slots.
   const int nt = ctx->np / TILE;
   std::vector<int> tl;
+  for (int I = 0; I < nt; ++I) tl.push_back((I << 16) | I);
   for (int I = 0; I < nt; ++I)
-    for (int J = 0; J <= I; ++J) tl.push_back((I << 16) | J);
+    for (int J = 0; J < I; ++J) tl.push_back((I << 16) | J);
   ctx->ntiles = (int)tl.size();
+  int ncu = 256;
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+  const int slots = 2 * std::max(ncu, 1);
   const int kchunks = (int)(mp / KC);
-  ctx->nsplit = 1;
-  if (ctx->ntiles < 256) ctx->nsplit = std::max(1, std::min(kchunks, (512 + ctx->ntiles - 1) / ctx->ntiles));
+  ctx->ntiles_main = (ctx->ntiles / slots) * slots;
+  if (const char* e = getenv("CVXG_SYRK_NOTAIL")) ctx->ntiles_main = atoi(e) ? ctx->ntiles : ctx->ntiles_main;
+  const int rest = ctx->ntiles - ctx->ntiles_main;
+  ctx->nsplit = rest > 0 ? std::max(1, std::min(kchunks, slots / rest)) : 1;
   CHK(dalloc(ctx, &ctx->tiles, tl.size()));
-  HIPC(ctx, hipMemcpy(ctx->tiles, tl.data(), tl.size() * sizeof(int), hipMemcpyHostToDevice));
+  CHK(copy_sync(ctx, ctx->tiles, tl.data(), tl.size() * sizeof(int), hipMemcpyHostToDevice));
   size_t part = (mp / 64) * np;
-  if (ctx->nsplit > 1) part = std::max(part, (size_t)ctx->nsplit * ctx->ntiles * TILE * TILE);
+  if (ctx->nsplit > 1)
+    part = std::max(part, (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE);
   CHK(dalloc(ctx, &ctx->part, part));
   const int lsb = ls_blocks(std::max(m, 1));
   CHK(dalloc(ctx, &ctx->ls_plog, (size_t)lsb * LS_TRIALS));
@@ -677,8 +703,8 @@ int cvxg_set_ineq(cvxg_ctx* ctx, const double* A, int ldA, int row_major, const 
     std::vector<double> rr(ctx->mp, 0.0), uu(ctx->mp, 1.0);
     memcpy(rr.data(), r, m * sizeof(double));
     memcpy(uu.data(), ub, m * sizeof(double));
-    HIPC(ctx, hipMemcpy(ctx->r, rr.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
-    HIPC(ctx, hipMemcpy(ctx->ub, uu.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
+    CHK(copy_sync(ctx, ctx->r, rr.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
+    CHK(copy_sync(ctx, ctx->ub, uu.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
   }
   ctx->have_ineq = 1;
   ctx->x_eval_valid = 0;
@@ -693,7 +719,7 @@ int cvxg_set_eq(cvxg_ctx* ctx, const double* Aeq, int ldAeq, int row_major, cons
   CHK(upload_mat(ctx, ctx->Aeq, ctx->np, CVXG_MAX_EQ, Aeq, ctx->p, ctx->n, ldAeq, row_major));
   std::vector<double> b(CVXG_MAX_EQ, 0.0);
   memcpy(b.data(), beq, ctx->p * sizeof(double));
-  HIPC(ctx, hipMemcpy(ctx->beq, b.data(), CVXG_MAX_EQ * sizeof(double), hipMemcpyHostToDevice));
+  CHK(copy_sync(ctx, ctx->beq, b.data(), CVXG_MAX_EQ * sizeof(double), hipMemcpyHostToDevice));
   ctx->have_eq = 1;
   ctx->x_eval_valid = 0;
   return CVXG_OK;
@@ -737,12 +763,12 @@ int cvxg_barrier_eval(cvxg_ctx* ctx, double t, const double* x, double* f, doubl
   CHK(set_t(ctx, t));
   CHK(eval_at_x(ctx));
   if (f) *f = ctx->f_at_x;
-  if (g) HIPC(ctx, hipMemcpy(g, ctx->y, ctx->n * sizeof(double), hipMemcpyDeviceToHost));
+  if (g) CHK(copy_sync(ctx, g, ctx->y, ctx->n * sizeof(double), hipMemcpyDeviceToHost));
   if (H) {
     CHK(assemble_hessian(ctx));
+    HIPC(ctx, hipMemcpy2DAsync(H, ctx->n * sizeof(double), ctx->H, ctx->np * sizeof(double), ctx->n * sizeof(double),
+                               ctx->n, hipMemcpyDeviceToHost, ctx->s));
     HIPC(ctx, hipStreamSynchronize(ctx->s));
-    HIPC(ctx, hipMemcpy2D(H, ctx->n * sizeof(double), ctx->H, ctx->np * sizeof(double), ctx->n * sizeof(double),
-                          ctx->n, hipMemcpyDeviceToHost));
   }
   return CVXG_OK;
 }
@@ -765,7 +791,7 @@ int cvxg_active_set(cvxg_ctx* ctx, const double* x, double tol, int* idx, int* c
   if (!ctx || !x || !count) return CVXG_E_ARG;
   std::vector<double> g(ctx->m), ub(ctx->m);
   CHK(cvxg_constraint_values(ctx, x, g.data()));
-  HIPC(ctx, hipMemcpy(ub.data(), ctx->ub, ctx->m * sizeof(double), hipMemcpyDeviceToHost));
+  CHK(copy_sync(ctx, ub.data(), ctx->ub, ctx->m * sizeof(double), hipMemcpyDeviceToHost));
   int k = 0;
   for (int i = 0; i < ctx->m; ++i)
     if (fabs(g[i] - ub[i]) < tol) {  // Constraint.isActive, Constraint.scala:26
@@ -802,8 +828,8 @@ int cvxg_newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, cons
   if (rc != CVXG_OK) return rc;
   info->q = ctx->hctrl->sc[SC_Q];
   info->newton_decrement = -info->q / 2;
-  if (dx) HIPC(ctx, hipMemcpy(dx, ctx->dx, ctx->n * sizeof(double), hipMemcpyDeviceToHost));
-  if (w && ctx->p > 0) HIPC(ctx, hipMemcpy(w, ctx->kw, ctx->p * sizeof(double), hipMemcpyDeviceToHost));
+  if (dx) CHK(copy_sync(ctx, dx, ctx->dx, ctx->n * sizeof(double), hipMemcpyDeviceToHost));
+  if (w && ctx->p > 0) CHK(copy_sync(ctx, w, ctx->kw, ctx->p * sizeof(double), hipMemcpyDeviceToHost));
   return CVXG_OK;
 }
 
