@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcvxg.so")
+LIB_PATH = os.environ.get("CVXG_LIB", os.path.join(_HERE, "libcvxg.so"))  # override: experiment builds
 
 CVXG_OK = 0
 CVXG_E_NOT_PD = 1

@@ -162,6 +162,54 @@ static int upload_mat(cvxg_ctx* ctx, double* dst, int ldd, int rows_pad, const d
   return CVXG_OK;
 }
 
+// Lower-tile order for the assembly SYRK.  Workgroup b runs on XCD b % 8 (round-robin dispatch; used for
+// locality only, never for correctness).  When nt % 4 == 0 the 32x32-tile triangle is cut into 4x4 block
+// pairs of g = nt/4 tile rows: the 6 off-diagonal pairs (g*g tiles, 2g column panels each) and two groups
+// of two diagonal pairs (g(g+1) tiles, 2g panels) give every XCD a tile set that touches only half of A's
+// column panels, so each XCD's L2 streams half of A instead of all of it.  Each XCD gets the same number
+// of full-K tiles (whole waves of its slots); the surplus of the diagonal groups (their diagonal tiles) is
+// the split-K tail.  Other shapes: diagonal tiles first, whole waves, the rest is the tail.
+static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
+  std::vector<int> tl;
+  const int per_xcd = slots / 8;
+  if (nt % 4 == 0 && nt >= 8 && slots % 8 == 0) {
+    const int g = nt / 4;
+    std::vector<std::vector<int>> grp;
+    for (int a = 1; a < 4; ++a)
+      for (int b = 0; b < a; ++b) {
+        std::vector<int> v;
+        for (int i = 0; i < g; ++i)
+          for (int j = 0; j < g; ++j) v.push_back(((a * g + i) << 16) | (b * g + j));
+        grp.push_back(v);
+      }
+    for (int pair = 0; pair < 2; ++pair) {
+      std::vector<int> v, dg;
+      for (int a = 2 * pair; a < 2 * pair + 2; ++a)
+        for (int i = 0; i < g; ++i) {
+          for (int j = 0; j < i; ++j) v.push_back(((a * g + i) << 16) | (a * g + j));
+          dg.push_back(((a * g + i) << 16) | (a * g + i));
+        }
+      v.insert(v.end(), dg.begin(), dg.end());  // diagonal tiles last: they become the tail
+      grp.push_back(v);
+    }
+    size_t shortest = grp[0].size();
+    for (auto& v : grp) shortest = std::min(shortest, v.size());
+    const int S = per_xcd > 0 ? (int)(shortest / per_xcd) * per_xcd : 0;
+    if (S > 0) {
+      for (int s = 0; s < S; ++s)
+        for (int x = 0; x < 8; ++x) tl.push_back(grp[x][s]);
+      for (int x = 0; x < 8; ++x) tl.insert(tl.end(), grp[x].begin() + S, grp[x].end());
+      *nmain = 8 * S;
+      return tl;
+    }
+  }
+  for (int I = 0; I < nt; ++I) tl.push_back((I << 16) | I);
+  for (int I = 0; I < nt; ++I)
+    for (int J = 0; J < I; ++J) tl.push_back((I << 16) | J);
+  *nmain = ((int)tl.size() / slots) * slots;
+  return tl;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Device pipeline pieces
 // ------------------------------------------------------------------------------------------------
@@ -613,20 +661,15 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   CHK(dalloc(ctx, &ctx->Linv, (size_t)ctx->nblk * NB * NB));
   CHK(dalloc(ctx, &ctx->rhs, np * MAX_RHS));
   CHK(dalloc(ctx, &ctx->sol, np * MAX_RHS));
-  // SYRK tile list (lower tiles; diagonal tiles first, they carry 3/4 of the work) and the wave plan:
-  // `slots` workgroups run at once (2 per CU); floor(T/slots) whole waves of full-K tiles, then the
-  // remaining tiles are split along K so that they fill one more wave of slots.
+  // SYRK tile list and wave plan (syrk_tile_plan): full-K tiles in whole waves of workgroup slots, the
+  // remaining tiles split along K so that they fill one more wave.
   const int nt = ctx->np / TILE;
-  std::vector<int> tl;
-  for (int I = 0; I < nt; ++I) tl.push_back((I << 16) | I);
-  for (int I = 0; I < nt; ++I)
-    for (int J = 0; J < I; ++J) tl.push_back((I << 16) | J);
-  ctx->ntiles = (int)tl.size();
   int ncu = 256;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
   const int slots = 2 * std::max(ncu, 1);
   const int kchunks = (int)(mp / KC);
-  ctx->ntiles_main = (ctx->ntiles / slots) * slots;
+  std::vector<int> tl = syrk_tile_plan(nt, slots, &ctx->ntiles_main);
+  ctx->ntiles = (int)tl.size();
   if (const char* e = getenv("CVXG_SYRK_NOTAIL")) ctx->ntiles_main = atoi(e) ? ctx->ntiles : ctx->ntiles_main;
   const int rest = ctx->ntiles - ctx->ntiles_main;
   ctx->nsplit = rest > 0 ? std::max(1, std::min(kchunks, slots / rest)) : 1;

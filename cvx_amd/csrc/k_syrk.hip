@@ -43,7 +43,6 @@ __global__ __launch_bounds__(256, 2) void k_syrk_assemble(const double* __restri
                                                           const int* __restrict__ tiles, int ntiles, int nsplit,
                                                           double* __restrict__ partials) {
   __shared__ __attribute__((aligned(16))) double lds[2][2][KC][SA];
-  __shared__ double wl[2][KC];
   const int tile = blockIdx.x, split = blockIdx.y;
   const int ij = tiles[tile];
   const int I = ij >> 16, J = ij & 0xffff;
@@ -61,57 +60,65 @@ __global__ __launch_bounds__(256, 2) void k_syrk_assemble(const double* __restri
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
 
-  d2 stg[8];
-  double wst = 0.0;
   const int colI = I * TILE + lane * 2, colJ = J * TILE + lane * 2;
 
-  // Unconditional, statically indexed staging (a predicated assignment sends stg[] to scratch); a
-  // diagonal tile simply stages panel I twice.
+  // Unconditional, statically indexed staging (a predicated assignment sends the staging registers to
+  // scratch); a diagonal tile simply stages panel I twice.  Two register sets (sa, sb) keep loads two
+  // chunks ahead of their LDS write, so about 2 x 4096 MFMA cycles of latency are covered.
   const double* srcI = A + colI;
   const double* srcJ = A + colJ;
-  auto gload = [&](int chunk) {
-    const size_t k0 = (size_t)chunk * KC;
+  // The weights w_k = 1/d_k^2 scale the J panel as it is written to LDS (row k of the slab is wave-uniform:
+  // wave `wid` stages rows wid + 4q), so the MFMA loop has no FP64 VALU work.
+  auto gload = [&](d2 (&st)[8], double (&wv)[4], int chunk) {
+    const size_t k0 = (size_t)min(chunk, kchunks - 1) * KC;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      stg[q] = *reinterpret_cast<const d2*>(srcI + (k0 + wid + 4 * q) * lda);
-      stg[q + 4] = *reinterpret_cast<const d2*>(srcJ + (k0 + wid + 4 * q) * lda);
+      st[q] = *reinterpret_cast<const d2*>(srcI + (k0 + wid + 4 * q) * lda);
+      st[q + 4] = *reinterpret_cast<const d2*>(srcJ + (k0 + wid + 4 * q) * lda);
+      wv[q] = w[k0 + wid + 4 * q];
     }
-    wst = w[k0 + (tid & (KC - 1))];
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](const d2 (&st)[8], const double (&wv)[4], int buf) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      *reinterpret_cast<d2*>(&lds[buf][0][wid + 4 * q][lane * 2]) = stg[q];
-      *reinterpret_cast<d2*>(&lds[buf][1][wid + 4 * q][lane * 2]) = stg[q + 4];
+      *reinterpret_cast<d2*>(&lds[buf][0][wid + 4 * q][lane * 2]) = st[q];
+      *reinterpret_cast<d2*>(&lds[buf][1][wid + 4 * q][lane * 2]) = st[q + 4] * wv[q];
     }
-    if (tid < KC) wl[buf][tid] = wst;
+  };
+  auto compute = [&](int buf) {
+    if (!active) return;
+    const double* PI = &lds[buf][0][0][0];
+    const double* PJ = &lds[buf][1][0][0];
+#pragma unroll
+    for (int s = 0; s < KC / 4; ++s) {
+      const int kk = 4 * s + (lane >> 4);
+      double fa[4], fb[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) fa[mi] = PI[kk * SA + wr * 64 + mi * 16 + (lane & 15)];
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) fb[nj] = PJ[kk * SA + wc * 64 + nj * 16 + (lane & 15)];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = MFMA64(fa[mi], fb[nj], acc[mi][nj]);
+    }
   };
 
-  gload(min(c0, kchunks - 1));
-  swrite(0);
+  d2 sa[8], sb[8];
+  double wa[4], wb[4];
+  gload(sa, wa, c0);
+  swrite(sa, wa, 0);
+  gload(sb, wb, c0 + 1);
   __syncthreads();
-  for (int c = c0; c < c1; ++c) {
-    const int buf = (c - c0) & 1;
-    gload(min(c + 1, kchunks - 1));  // unconditional (the last one is a harmless re-read)
-    if (active) {
-      const double* PI = &lds[buf][0][0][0];
-      const double* PJ = diag ? PI : &lds[buf][1][0][0];
-#pragma unroll
-      for (int s = 0; s < KC / 4; ++s) {
-        const int kk = 4 * s + (lane >> 4);
-        const double wk = wl[buf][kk];
-        double fa[4], fb[4];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) fa[mi] = PI[kk * SA + wr * 64 + mi * 16 + (lane & 15)];
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj) fb[nj] = wk * PJ[kk * SA + wc * 64 + nj * 16 + (lane & 15)];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = MFMA64(fa[mi], fb[nj], acc[mi][nj]);
-      }
-    }
-    swrite(buf ^ 1);
+  for (int c = c0; c < c1; c += 2) {
+    gload(sa, wa, c + 2);
+    compute(0);
+    swrite(sb, wb, 1);
+    __syncthreads();
+    if (c + 1 >= c1) break;
+    gload(sb, wb, c + 3);
+    compute(1);
+    swrite(sa, wa, 0);
     __syncthreads();
   }
   if (!active) return;

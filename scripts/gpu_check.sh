@@ -28,6 +28,14 @@ for st in $STAGES; do
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --steps 10 --warmup 2 > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
       rc=$?; cd "$GRAFT_REPO_ROOT"; stop_if_fault $rc prof ;;
+    pmc)
+      # HBM traffic counters, one counter group per pass (FETCH_SIZE and WRITE_SIZE do not fit together)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_fetch" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --steps 3 --warmup 1 > "$GRAFT_REPO_ROOT/gpurun_out/pmc_fetch.log" 2>&1
+      rc=$?; cd "$GRAFT_REPO_ROOT"; stop_if_fault $rc pmc_fetch
+      cd /tmp
+      timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_write" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --steps 3 --warmup 1 > "$GRAFT_REPO_ROOT/gpurun_out/pmc_write.log" 2>&1
+      rc=$?; cd "$GRAFT_REPO_ROOT"; stop_if_fault $rc pmc_write ;;
   esac
 done
 echo "[gpu_check] done" | tee -a gpurun_out/status.log
