@@ -23,6 +23,7 @@ struct DevCtrl {
   int not_strict;                 // # rows failing g_i*(1+3e-16) < ub_i
   int chol_info;                  // 1-based global pivot index of the first non-positive pivot, 0 = ok
   int ruiz_sweeps;                // Ruiz sweeps executed
+  int df_status;                  // dataflow Cholesky: 2 = a dependency wait timed out (scheduling bug)
   unsigned long long min_diag;    // bits of min diag(L) (positive doubles order like uint64)
   unsigned long long ruiz_rho[RUIZ_MAX + 2];
   double sc[32];                  // reduced scalars, see SC_* below

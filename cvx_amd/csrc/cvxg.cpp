@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <limits>
+#include <queue>
 #include <string>
 #include <vector>
 
@@ -64,6 +65,13 @@ struct cvxg_ctx {
   int ntiles = 0, nsplit = 1;
   int ntiles_main = 0;  // tiles assembled without K split (whole waves of slots); the rest use nsplit
   int chol_outer = 4;  // 64-blocks per outer Cholesky panel (trailing update width 256)
+  int chol_dataflow = 1;  // 1: persistent tile-DAG factorization (k_dataflow.hip); 0: kernel per step
+  int ncu = 256;
+  unsigned* df_tasks = nullptr;
+  int df_ntasks = 0;
+  int* df_work = nullptr;
+  unsigned long long* df_trace = nullptr;  // CVXG_DF_TRACE=<file>: per-task timeline of the last factorization
+  std::string df_trace_path;
   DevCtrl* ctrl = nullptr;
   DevCtrl* hctrl = nullptr;
   double* hls = nullptr;  // pinned: [LS_TRIALS] logs then [2*LS_TRIALS] counts as ints
@@ -210,6 +218,116 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
   return tl;
 }
 
+// Task order of the persistent dataflow Cholesky (k_dataflow.hip) for nb x nb tiles: the DAG
+// POTRF(k) -> TRSM(i,k) -> UPDATE(i,j,k) -> UPDATE(i,j,k+1) | POTRF(j) | TRSM(i,j) is list-scheduled on
+// `workers` simulated workgroups with estimated task times, highest bottom level (longest path to the
+// end) first among the ready tasks; the emitted order is the simulated start order, hence topological.
+// The critical chain tasks are simulated but not emitted (workgroup 0 runs them in sequence); every
+// transitive dependency of a chain task still precedes that task's dependents in the emitted order, which
+// keeps the launch deadlock-free.
+static std::vector<unsigned> build_chol_schedule(int nb, int workers) {
+  struct Task {
+    int type, i, j, k;
+    double dur, bl, avail;
+    int npred;
+  };
+  std::vector<Task> T;
+  std::vector<int> potrf_id(nb), trsm_id((size_t)nb * nb, -1);
+  std::vector<int> upd_base((size_t)nb * (nb + 1) / 2);
+  auto tri = [](int i, int j) { return i * (i + 1) / 2 + j; };
+  // per-tile update ids: upd_base[tri(i,j)] + k, allocated lazily in topological enumeration order
+  std::vector<int> upd_id;
+  {
+    size_t tot = 0;
+    for (int i = 0; i < nb; ++i)
+      for (int j = 0; j <= i; ++j) {
+        upd_base[tri(i, j)] = (int)tot;
+        tot += j;
+      }
+    upd_id.assign(tot, -1);
+  }
+  const double d_potrf = 29.0, d_trsm = 6.0, d_upd = 5.5;  // us, measured (scripts/df_trace.py)
+  for (int k = 0; k < nb; ++k) {  // (k, type) order is a topological order
+    potrf_id[k] = (int)T.size();
+    T.push_back({0, k, k, k, d_potrf, 0, 0, k > 0 ? 1 : 0});
+    for (int i = k + 1; i < nb; ++i) {
+      trsm_id[(size_t)i * nb + k] = (int)T.size();
+      T.push_back({1, i, k, k, d_trsm, 0, 0, 1 + (k > 0 ? 1 : 0)});
+    }
+    for (int j = k + 1; j < nb; ++j)
+      for (int i = j; i < nb; ++i) {
+        upd_id[upd_base[tri(i, j)] + k] = (int)T.size();
+        T.push_back({2, i, j, k, i == j ? 0.75 * d_upd : d_upd, 0, 0, (i == j ? 1 : 2) + (k > 0 ? 1 : 0)});
+      }
+  }
+  auto succ = [&](int t, std::vector<int>& out) {
+    out.clear();
+    const Task& x = T[t];
+    if (x.type == 0) {
+      for (int i = x.k + 1; i < nb; ++i) out.push_back(trsm_id[(size_t)i * nb + x.k]);
+    } else if (x.type == 1) {
+      const int i = x.i, k = x.k;
+      for (int j = k + 1; j <= i; ++j) out.push_back(upd_id[upd_base[tri(i, j)] + k]);
+      for (int r = i + 1; r < nb; ++r) out.push_back(upd_id[upd_base[tri(r, i)] + k]);
+    } else {
+      const int i = x.i, j = x.j, k = x.k;
+      if (k + 1 < j) out.push_back(upd_id[upd_base[tri(i, j)] + k + 1]);
+      else if (i == j) out.push_back(potrf_id[j]);
+      else out.push_back(trsm_id[(size_t)i * nb + j]);
+    }
+  };
+  std::vector<int> sv;
+  for (int t = (int)T.size() - 1; t >= 0; --t) {
+    succ(t, sv);
+    double m = 0.0;
+    for (int s : sv) m = std::max(m, T[s].bl);
+    T[t].bl = T[t].dur + m;
+  }
+  // list scheduling
+  typedef std::pair<double, int> DI;
+  std::priority_queue<DI, std::vector<DI>, std::greater<DI>> pending, wfree;  // by avail time / free time
+  std::priority_queue<DI> ready;                                               // by bottom level
+  for (int w = 0; w < workers; ++w) wfree.push({0.0, w});
+  pending.push({0.0, potrf_id[0]});
+  std::vector<unsigned> order;
+  order.reserve(T.size());
+  size_t nsched = 0;
+  while (nsched < T.size()) {
+    DI wk = wfree.top();
+    wfree.pop();
+    double now = wk.first;
+    while (!pending.empty() && pending.top().first <= now) {
+      ready.push({T[pending.top().second].bl, pending.top().second});
+      pending.pop();
+    }
+    if (ready.empty()) {
+      now = pending.top().first;
+      while (!pending.empty() && pending.top().first <= now) {
+        ready.push({T[pending.top().second].bl, pending.top().second});
+        pending.pop();
+      }
+    }
+    const int t = ready.top().second;
+    ready.pop();
+    const Task& x = T[t];
+    now = std::max(now, x.avail);  // a task moved to `ready` by a later worker is not available earlier
+    // the critical chain POTRF(k) -> TRSM(k+1,k) -> UPDATE(k+1,k+1,k) -> POTRF(k+1) runs on workgroup 0
+    // (k_dataflow.hip) and is left out of the claimed order
+    const bool chain = x.type == 0 || (x.type == 1 && x.i == x.k + 1) || (x.type == 2 && x.i == x.j && x.j == x.k + 1);
+    if (!chain)
+      order.push_back(((unsigned)x.type << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j);
+    ++nsched;
+    const double fin = now + x.dur;
+    wfree.push({fin, wk.second});
+    succ(t, sv);
+    for (int s : sv) {
+      T[s].avail = std::max(T[s].avail, fin);
+      if (--T[s].npred == 0) pending.push({T[s].avail, s});
+    }
+  }
+  return order;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Device pipeline pieces
 // ------------------------------------------------------------------------------------------------
@@ -295,18 +413,39 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs) {
   // remaining panel columns are updated (K = 64); the trailing matrix is then updated once with K = the
   // whole panel width, so it is read-modify-written nblk/chol_outer times instead of nblk times.
   const int np = ctx->np, ow = ctx->chol_outer;
-  for (int K0 = 0; K0 < ctx->nblk; K0 += ow) {
-    const int K1 = std::min(K0 + ow, ctx->nblk);
-    for (int k = K0; k < K1; ++k) {
-      launch_potrf_diag(s, ctx->L, np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
-      launch_trsm_mfma(s, ctx->L, np, np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
-      if (k + 1 < K1) launch_chol_update(s, ctx->L, np, np, k * NB, NB, (k + 1) * NB, (k + 1) * NB, K1 * NB, ctx->ctrl);
+  if (ctx->chol_dataflow) {
+    launch_chol_dataflow(s, ctx->L, np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
+                         ctx->df_ntasks, ctx->ncu, ctx->df_trace);
+  } else {
+    for (int K0 = 0; K0 < ctx->nblk; K0 += ow) {
+      const int K1 = std::min(K0 + ow, ctx->nblk);
+      for (int k = K0; k < K1; ++k) {
+        launch_potrf_diag(s, ctx->L, np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
+        launch_trsm_mfma(s, ctx->L, np, np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
+        if (k + 1 < K1)
+          launch_chol_update(s, ctx->L, np, np, k * NB, NB, (k + 1) * NB, (k + 1) * NB, K1 * NB, ctx->ctrl);
+      }
+      if (K1 < ctx->nblk)
+        launch_chol_update(s, ctx->L, np, np, K0 * NB, (K1 - K0) * NB, K1 * NB, K1 * NB, np, ctx->ctrl);
     }
-    if (K1 < ctx->nblk)
-      launch_chol_update(s, ctx->L, np, np, K0 * NB, (K1 - K0) * NB, K1 * NB, K1 * NB, np, ctx->ctrl);
   }
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
+  if (ctx->hctrl->df_status != 0)
+    return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
+  if (ctx->df_trace) {  // instrumentation only: task order + timeline of this factorization
+    std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk));
+    std::vector<unsigned> ord(ctx->df_ntasks);
+    CHK(copy_sync(ctx, tr.data(), ctx->df_trace, tr.size() * 8, hipMemcpyDeviceToHost));
+    CHK(copy_sync(ctx, ord.data(), ctx->df_tasks, ord.size() * 4, hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(ctx->df_trace_path.c_str(), "wb")) {
+      fwrite(&ctx->df_ntasks, 4, 1, f);
+      fwrite(&ctx->nblk, 4, 1, f);
+      fwrite(ord.data(), 4, ord.size(), f);
+      fwrite(tr.data(), 8, tr.size(), f);
+      fclose(f);
+    }
+  }
   return CVXG_OK;
 }
 
@@ -659,6 +798,23 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   CHK(dalloc(ctx, &ctx->H, np * np));
   CHK(dalloc(ctx, &ctx->L, np * np));
   CHK(dalloc(ctx, &ctx->Linv, (size_t)ctx->nblk * NB * NB));
+  {  // dataflow Cholesky: task order for this tile count, work words
+    (void)hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device);
+    ctx->ncu = std::max(ctx->ncu, 1);
+    if (const char* e = getenv("CVXG_CHOL")) ctx->chol_dataflow = strcmp(e, "blocked") != 0;
+    if (ctx->nblk > 1023) ctx->chol_dataflow = 0;  // task encoding holds 10-bit tile indices
+    if (ctx->chol_dataflow) {
+      std::vector<unsigned> order = build_chol_schedule(ctx->nblk, ctx->ncu);
+      ctx->df_ntasks = (int)order.size();
+      CHK(dalloc(ctx, &ctx->df_tasks, order.size()));
+      CHK(copy_sync(ctx, ctx->df_tasks, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+      CHK(dalloc(ctx, &ctx->df_work, chol_dataflow_work_ints(ctx->nblk)));
+      if (const char* e = getenv("CVXG_DF_TRACE")) {
+        ctx->df_trace_path = e;
+        CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk)));
+      }
+    }
+  }
   CHK(dalloc(ctx, &ctx->rhs, np * MAX_RHS));
   CHK(dalloc(ctx, &ctx->sol, np * MAX_RHS));
   // SYRK tile list and wave plan (syrk_tile_plan): full-K tiles in whole waves of workgroup slots, the
@@ -704,7 +860,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
                   ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
-                  ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl};
+                  ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);

@@ -1,0 +1,285 @@
+// k_dataflow.hip — the whole regularized-Cholesky factorization (right-looking dpotrf('L'),
+// MatrixUtils.scala:452-461) with the fused forward solve, as ONE persistent launch over a tile DAG.
+//
+// Tiles are 64 x 64 (NB).  Tasks, in an order fixed on the host by list-scheduling the DAG with its
+// critical-path priorities (cvxg.cpp, build_chol_schedule):
+//   POTRF(k)      factor the diagonal tile, L_kk^-1 into Linv[k], forward-solve rhs block k
+//   TRSM(i,k)     L_ik = A_ik L_kk^-T (MFMA, product with L_kk^-1); rhs_i -= L_ik w_k
+//   UPDATE(i,j,k) A_ij -= L_ik L_jk^T (MFMA), k < j <= i
+// Per lower tile (i,j) one state word counts the operations applied to it: UPDATE(i,j,k) needs
+// state(i,j) == k, state(i,k) == state(j,k) == k + 1; POTRF(k) / TRSM(i,k) need state == k (and the
+// finished diagonal tile).  Workgroups (one per CU) claim tasks with an atomic counter; a task only waits
+// on tasks earlier in the order, so the launch cannot deadlock whatever the residency.  Every wait is
+// bounded: on a timeout or a failed pivot the abort word is set and every workgroup drains.
+//
+// Inter-workgroup hand-off (MI355X_MICROARCH.md, visibility: Valid forms, row 1): every load and store of
+// handed-off bytes is an sc1 access (relaxed agent-scope atomics), each storing wave drains with
+// s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane stores the state word; the consumer polls the
+// word with sc1 loads, then a workgroup barrier, then sc1 loads of the data.  One workgroup per CU.
+#include "potrf_block.hpp"
+
+namespace cvxg {
+
+typedef double d4f __attribute__((ext_vector_type(4)));
+
+constexpr int DF_SP = NB + 2;  // LDS row stride (doubles) of a staged 64 x 64 operand: conflict-free fragments
+constexpr int DF_SMEM = 10240;  // doubles (80 KB): > half the CU's LDS, so one workgroup per CU
+
+__device__ __forceinline__ int df_tri(int i, int j) { return i * (i + 1) / 2 + j; }
+
+__device__ __forceinline__ int df_poll(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void df_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Thread 0 waits until state[idx] >= want.  Returns false when the launch aborts (failed pivot elsewhere)
+// or after ~2^22 polls (then it raises the abort word itself with code 2: a scheduling bug, not a hang).
+__device__ bool df_wait(const int* state, int idx, int want, int* abortw, DevCtrl* ctrl) {
+  for (unsigned spins = 0;; ++spins) {
+    if (df_poll(state + idx) >= want) return true;
+    if ((spins & 15) == 15 && df_poll(abortw)) return false;
+    if (spins > (1u << 22)) {
+      __hip_atomic_store(abortw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicExch(&ctrl->df_status, 2);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Stage a 64 x 64 tile (descriptor m, leading dimension ld) into LDS [64][DF_SP]: 8 x 16-B sc1 loads per thread.
+__device__ __forceinline__ void df_stage(double* __restrict__ dst, const Sc1Mem& m, int ld) {
+  const int tid = threadIdx.x;
+  f64x2 v[NB * NB / 512];
+#pragma unroll
+  for (int q = 0; q < NB * NB / 512; ++q) {
+    const int idx = q * 256 + tid;
+    v[q] = m.ld2((idx >> 5) * ld + 2 * (idx & 31));
+  }
+#pragma unroll
+  for (int q = 0; q < NB * NB / 512; ++q) {
+    const int idx = q * 256 + tid;
+    const int r = idx >> 5, c = 2 * (idx & 31);
+    dst[r * DF_SP + c] = v[q][0];
+    dst[r * DF_SP + c + 1] = v[q][1];
+  }
+}
+
+// acc (wave (wr, wc): 32 x 32 block = 2 x 2 MFMA tiles) += sgn * P_i[rows] . P_j[cols]^T over K = 64.
+__device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, const double* Pj, double sgn, int wr,
+                                        int wc, int lane) {
+#pragma unroll
+  for (int s = 0; s < NB / 4; ++s) {
+    const int kk = 4 * s + (lane >> 4);
+    double fa[2], fb[2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) fa[mi] = sgn * Pi[(wr * 32 + mi * 16 + (lane & 15)) * DF_SP + kk];
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) fb[nj] = Pj[(wc * 32 + nj * 16 + (lane & 15)) * DF_SP + kk];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+        acc[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi], fb[nj], acc[mi][nj], 0, 0, 0);
+  }
+}
+
+// UPDATE(i,j,k): A_ij -= L_ik L_jk^T.  On a diagonal tile the strictly-upper 32 x 32 wave block is skipped.
+__device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, double* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const bool active = !(i == j && wc > wr);
+  const Sc1Mem mC(L + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
+  d4f acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+        acc[mi][nj][r] = mC.ld(row * ld + col);
+      }
+  double* Pi = smem;
+  double* Pj = (i == j) ? smem : smem + NB * DF_SP;
+  df_stage(Pi, Sc1Mem(L + (size_t)i * NB * ld + (size_t)k * NB, tile_bytes(ld)), ld);
+  if (i != j) df_stage(Pj, Sc1Mem(L + (size_t)j * NB * ld + (size_t)k * NB, tile_bytes(ld)), ld);
+  __syncthreads();
+  if (active) {
+    df_mfma(acc, Pi, Pj, -1.0, wr, wc, lane);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+          mC.st(row * ld + col, acc[mi][nj][r]);
+        }
+  }
+}
+
+// TRSM(i,k): X = A_ik Linv_kk^T into tile (i,k); rhs_i -= X w_k (w_k = rhs block k after POTRF(k)).
+__device__ void df_trsm(double* __restrict__ L, int ld, int i, int k, double* __restrict__ rhs, int nrhs,
+                        double* __restrict__ Linv, double* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  double* Pi = smem;
+  double* Pj = smem + NB * DF_SP;
+  const Sc1Mem mA(L + (size_t)i * NB * ld + (size_t)k * NB, tile_bytes(ld));
+  const Sc1Mem mW(rhs + (size_t)k * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+  const Sc1Mem mR(rhs + (size_t)i * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+  df_stage(Pi, mA, ld);
+  df_stage(Pj, Sc1Mem(Linv + (size_t)k * NB * NB, tile_bytes(NB)), NB);
+  __syncthreads();
+  d4f acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = d4f{0.0, 0.0, 0.0, 0.0};
+  df_mfma(acc, Pi, Pj, 1.0, wr, wc, lane);
+  __syncthreads();  // every wave is done reading Pi / Pj: reuse them for X and w_k
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+        mA.st(row * ld + col, acc[mi][nj][r]);
+        Pi[row * DF_SP + col] = acc[mi][nj][r];
+      }
+  double* wk = Pj;  // [64][nrhs]
+  for (int t = tid; t < NB * nrhs; t += 256) wk[t] = mW.ld(t);
+  __syncthreads();
+  for (int t = tid; t < NB * nrhs; t += 256) {
+    const int row = t / nrhs, rho = t % nrhs;
+    double s = 0.0;
+#pragma unroll 8
+    for (int c = 0; c < NB; ++c) s = fma(Pi[row * DF_SP + c], wk[c * nrhs + rho], s);
+    mR.st(t, mR.ld(t) - s);
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L, int ld, double* __restrict__ rhs,
+                                                          int nrhs, double* __restrict__ Linv, DevCtrl* ctrl,
+                                                          int* __restrict__ work, const unsigned* __restrict__ tasks,
+                                                          int ntasks, int nblk, unsigned long long* __restrict__ trace) {
+  __shared__ __attribute__((aligned(16))) double smem[DF_SMEM];
+  __shared__ unsigned s_task;
+  __shared__ int s_ok;
+  int* counter = work;
+  int* abortw = work + 1;
+  int* state = work + 64;  // own cache lines
+  const int tid = threadIdx.x;
+  if (blockIdx.x == 0) {
+    // ---- workgroup 0: the critical chain POTRF(k) -> TRSM(k+1,k) -> UPDATE(k+1,k+1,k) -> POTRF(k+1) ----
+    for (int k = 0; k < nblk; ++k) {
+#pragma unroll 1
+      for (int step = 0; step < 3; ++step) {
+        if (step > 0 && k + 1 >= nblk) break;
+        if (tid == 0) {
+          bool ok;
+          if (step == 0) ok = df_wait(state, df_tri(k, k), k, abortw, ctrl);
+          else if (step == 1) ok = df_wait(state, df_tri(k + 1, k), k, abortw, ctrl);
+          else ok = df_wait(state, df_tri(k + 1, k + 1), k, abortw, ctrl);
+          s_ok = ok;
+          if (trace) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            trace[4 * (size_t)(ntasks + 3 * k + step)] = now;
+            trace[4 * (size_t)(ntasks + 3 * k + step) + 1] = now;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        if (!s_ok) return;
+        int done_idx;
+        if (step == 0) {
+          if (!potrf_block<Sc1Mem>(L, ld, k, rhs, nrhs, Linv, ctrl, *reinterpret_cast<PotrfSmem*>(smem))) {
+            if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+          }
+          done_idx = df_tri(k, k);
+        } else if (step == 1) {
+          df_trsm(L, ld, k + 1, k, rhs, nrhs, Linv, smem);
+          done_idx = df_tri(k + 1, k);
+        } else {
+          df_update(L, ld, k + 1, k + 1, k, smem);
+          done_idx = df_tri(k + 1, k + 1);
+        }
+        df_drain();
+        __syncthreads();
+        if (tid == 0) {
+          __hip_atomic_store(state + done_idx, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (trace) {
+            trace[4 * (size_t)(ntasks + 3 * k + step) + 2] = __builtin_amdgcn_s_memrealtime();
+            trace[4 * (size_t)(ntasks + 3 * k + step) + 3] = 0;
+          }
+        }
+      }
+    }
+    return;
+  }
+  // ---- workgroups 1..: claim the remaining tasks in the host-built order ---------------------------
+  int my_idx = -1;  // thread 0: claimed task index (trace)
+  for (;;) {
+    if (tid == 0) {
+      unsigned t = 0xffffffffu;
+      if (!df_poll(abortw)) {
+        const int idx = atomicAdd(counter, 1);
+        if (idx < ntasks) t = tasks[idx];
+        my_idx = idx;
+        if (trace && idx < ntasks) trace[4 * idx] = __builtin_amdgcn_s_memrealtime();
+      }
+      s_task = t;
+    }
+    __syncthreads();
+    const unsigned task = s_task;
+    if (task == 0xffffffffu) break;
+    const int type = task >> 30, k = (task >> 20) & 1023, i = (task >> 10) & 1023, j = task & 1023;
+    if (tid == 0) {
+      bool ok;
+      if (type == 1) {
+        ok = df_wait(state, df_tri(k, k), k + 1, abortw, ctrl) && df_wait(state, df_tri(i, k), k, abortw, ctrl);
+      } else {
+        ok = df_wait(state, df_tri(i, k), k + 1, abortw, ctrl) && df_wait(state, df_tri(j, k), k + 1, abortw, ctrl) &&
+             df_wait(state, df_tri(i, j), k, abortw, ctrl);
+      }
+      s_ok = ok;
+      if (trace) trace[4 * my_idx + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the data loads behind the poll
+    __syncthreads();
+    if (!s_ok) break;
+    int done_idx;
+    if (type == 1) {
+      df_trsm(L, ld, i, k, rhs, nrhs, Linv, smem);
+      done_idx = df_tri(i, k);
+    } else {
+      df_update(L, ld, i, j, k, smem);
+      done_idx = df_tri(i, j);
+    }
+    df_drain();  // every storing wave: its sc1 stores have left
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_store(state + done_idx, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (trace) {
+        trace[4 * my_idx + 2] = __builtin_amdgcn_s_memrealtime();
+        trace[4 * my_idx + 3] = blockIdx.x;
+      }
+    }
+  }
+}
+
+// work: [0] counter, [1] abort word, [64 ..) one state word per lower tile; zeroed before every launch.
+size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2; }
+
+void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
+                          int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
+                          unsigned long long* trace) {
+  (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
+  k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace);
+}
+
+}  // namespace cvxg

@@ -465,6 +465,7 @@ __global__ void k_ctrl_reset_eval(DevCtrl* ctrl) {
 }
 __global__ void k_ctrl_reset_chol(DevCtrl* ctrl) {
   ctrl->chol_info = 0;
+  ctrl->df_status = 0;
   ctrl->min_diag = (unsigned long long)__double_as_longlong(__builtin_inf());
 }
 void launch_ctrl_set(hipStream_t s, DevCtrl* ctrl, int which, double v) { k_ctrl_set<<<1, 1, 0, s>>>(ctrl, which, v); }

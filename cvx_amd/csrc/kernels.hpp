@@ -63,6 +63,12 @@ void launch_trsm_mfma(hipStream_t s, double* L, int ld, int np, int k, double* r
                       const DevCtrl* ctrl);
 void launch_chol_update(hipStream_t s, double* C, int ld, int np, int k0, int kw, int r0, int c0, int c1,
                         const DevCtrl* ctrl);
+// k_dataflow.hip: the whole factorization (potrf + trsm + updates + fused forward solve) as one persistent
+// launch over the 64x64 tile DAG in the host-built task order (build_chol_schedule in cvxg.cpp)
+size_t chol_dataflow_work_ints(int nblk);
+void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
+                          int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
+                          unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */);
 void launch_bwd_step(hipStream_t s, const double* L, int ld, const double* Linv, int k, double* rhs,
                      double* out, int nrhs, const DevCtrl* ctrl);
 
