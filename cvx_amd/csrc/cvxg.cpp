@@ -65,6 +65,7 @@ struct cvxg_ctx {
   int ntiles = 0, nsplit = 1;
   int ntiles_main = 0;  // tiles assembled without K split (whole waves of slots); the rest use nsplit
   int chol_outer = 4;  // 64-blocks per outer Cholesky panel (trailing update width 256)
+  int ruiz_full_rows = 0;  // 1: Ruiz sweeps over full rows of H (A/B reference for the lower-triangle sweep)
   int chol_dataflow = 1;  // 1: persistent tile-DAG factorization (k_dataflow.hip); 0: kernel per step
   int ncu = 256;
   unsigned* df_tasks = nullptr;
@@ -393,9 +394,14 @@ static int assemble_hessian(cvxg_ctx* ctx) {
 static void ruiz(cvxg_ctx* ctx) {
   hipStream_t s = ctx->s;
   launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl);
-  for (int k = 0; k < RUIZ_MAX; ++k)
-    launch_ruiz_sweep(s, ctx->H, ctx->np, ctx->n, (k & 1) ? ctx->ruiz1 : ctx->ruiz0, (k & 1) ? ctx->ruiz0 : ctx->ruiz1,
-                      ctx->ctrl, k);
+  for (int k = 0; k < RUIZ_MAX; ++k) {
+    const double* dc = (k & 1) ? ctx->ruiz1 : ctx->ruiz0;
+    double* dn = (k & 1) ? ctx->ruiz0 : ctx->ruiz1;
+    if (ctx->ruiz_full_rows)
+      launch_ruiz_sweep(s, ctx->H, ctx->np, ctx->n, dc, dn, ctx->ctrl, k);
+    else
+      launch_ruiz_sweep_tri(s, ctx->H, ctx->np, ctx->n, ctx->np, dc, dn, ctx->part, ctx->ctrl, k);
+  }
   launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl);
 }
 
@@ -769,6 +775,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   ctx->mp = round_up(std::max(m, 1), MPAD);
   ctx->nblk = ctx->np / NB;
   if (const char* e = getenv("CVXG_CHOL_OUTER")) ctx->chol_outer = std::max(1, atoi(e));
+  if (const char* e = getenv("CVXG_RUIZ_FULL")) ctx->ruiz_full_rows = atoi(e) != 0;  // A/B: full-row sweeps
   HIPC(ctx, hipSetDevice(device));
   HIPC(ctx, hipStreamCreateWithFlags(&ctx->s, hipStreamNonBlocking));
   const size_t np = ctx->np, mp = ctx->mp;
@@ -831,7 +838,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   ctx->nsplit = rest > 0 ? std::max(1, std::min(kchunks, slots / rest)) : 1;
   CHK(dalloc(ctx, &ctx->tiles, tl.size()));
   CHK(copy_sync(ctx, ctx->tiles, tl.data(), tl.size() * sizeof(int), hipMemcpyHostToDevice));
-  size_t part = (mp / 64) * np;
+  size_t part = std::max((mp / 64) * np, (size_t)ctx->nblk * np);  // coldot partials, Ruiz tile partials
   if (ctx->nsplit > 1)
     part = std::max(part, (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE);
   CHK(dalloc(ctx, &ctx->part, part));

@@ -229,6 +229,95 @@ void launch_ruiz_sweep(hipStream_t s, const double* H, int ld, int n, const doub
   k_ruiz_sweep<<<(n + 3) / 4, 256, 0, s>>>(H, ld, n, dcur, dnext, ctrl, k);
 }
 
+// Lower-triangle form of the sweep: H is exactly symmetric (the assembly mirrors its lower triangle), so
+// sum_j (d_j H_ij)^2 over a full row is assembled from the 64 x 64 tiles (I, J), J <= I, of the lower
+// triangle alone -- half the bytes per sweep.  Tile (I, J) writes
+//   S[J][i] = sum_{j in J} (d_j H_ij)^2   for its rows i in I      (row partials)
+//   S[I][j] = sum_{i in I} (d_i H_ij)^2   for its columns j in J   (column partials = rows of H_JI, I > J)
+// so every S[X][r] is written by exactly one tile, and k_ruiz_rows adds S[0..nbn)[r] in a fixed order.
+__global__ __launch_bounds__(256) void k_ruiz_tiles(const double* __restrict__ H, int ld, int nbn,
+                                                    const double* __restrict__ dcur, double* __restrict__ S,
+                                                    const DevCtrl* ctrl, int k) {
+  const double rho = __longlong_as_double((long long)ctrl->ruiz_rho[k]);
+  if (!(rho > 1e-6)) return;
+  // blockIdx.x -> (I, J), J <= I, row-major over the lower triangle
+  const int t = blockIdx.x;
+  int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  while (I * (I + 1) / 2 > t) --I;
+  const int J = t - I * (I + 1) / 2;
+  __shared__ double cred[4][NB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int c2 = tid & 31, g = tid >> 5;  // column pair 2*c2, row group g: rows g + 8q
+  const double* tile = H + (size_t)I * NB * ld + (size_t)J * NB;
+  vd2 h[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) h[q] = *reinterpret_cast<const vd2*>(tile + (size_t)(g + 8 * q) * ld + 2 * c2);
+  const vd2 dj = *reinterpret_cast<const vd2*>(dcur + J * NB + 2 * c2);
+  vd2 csum = {0.0, 0.0};
+  double rs[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const double di = dcur[I * NB + g + 8 * q];
+    const vd2 a = dj * h[q];
+    rs[q] = a[0] * a[0] + a[1] * a[1];
+    const vd2 b = h[q] * di;
+    csum = __builtin_elementwise_fma(b, b, csum);
+  }
+  // row partials: reduce over the 32 lanes of one row group
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    double v = rs[q];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    rs[q] = v;
+  }
+  if (c2 == 0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) S[(size_t)J * (nbn * NB) + I * NB + g + 8 * q] = rs[q];
+  }
+  if (I == J) return;  // a diagonal tile's rows already cover its columns
+  // column partials: the two row groups of this wave, then the four waves in order
+  csum[0] += __shfl_xor(csum[0], 32, 64);
+  csum[1] += __shfl_xor(csum[1], 32, 64);
+  if (lane < 32) {
+    cred[wid][2 * c2] = csum[0];
+    cred[wid][2 * c2 + 1] = csum[1];
+  }
+  __syncthreads();
+  if (tid < NB) S[(size_t)I * (nbn * NB) + J * NB + tid] = ((cred[0][tid] + cred[1][tid]) + cred[2][tid]) + cred[3][tid];
+}
+
+__global__ __launch_bounds__(256) void k_ruiz_rows(const double* __restrict__ S, int nbn, int n, int np,
+                                                   const double* __restrict__ dcur, double* __restrict__ dnext,
+                                                   DevCtrl* ctrl, int k) {
+  const double rho = __longlong_as_double((long long)ctrl->ruiz_rho[k]);
+  if (!(rho > 1e-6)) return;
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ldS = nbn * NB;
+  double m = 0.0;
+  if (row < n) {
+    double ssum = 0.0;
+    for (int X = 0; X < nbn; ++X) ssum += S[(size_t)X * ldS + row];
+    const double di = dcur[row];
+    const double u = sqrt(di * sqrt(ssum));        // sqrt(norm(Q(i,::)))   MatrixUtils.scala:258
+    const double v = (u > 0) ? 1.0 / u : 1.0;      // :259
+    dnext[row] = di * v;                           // :260
+    m = fabs(1.0 - u);                             // :261-262
+  } else if (row < np) {
+    dnext[row] = 1.0;
+  }
+  m = wave_max(m);  // every lane of the wave is live here (no early return above)
+  if ((threadIdx.x & 63) == 0 && m > 0.0) atomic_max_pos(&ctrl->ruiz_rho[k + 1], m);
+}
+
+void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np, const double* dcur, double* dnext,
+                           double* S, DevCtrl* ctrl, int k) {
+  const int nbn = (n + NB - 1) / NB;
+  k_ruiz_tiles<<<nbn * (nbn + 1) / 2, 256, 0, s>>>(H, ld, nbn, dcur, S, ctrl, k);
+  k_ruiz_rows<<<(np + 255) / 256, 256, 0, s>>>(S, nbn, n, np, dcur, dnext, ctrl, k);
+}
+
 __global__ void k_ruiz_final(const double* __restrict__ d0, const double* __restrict__ d1, int np,
                              double* __restrict__ dfin, DevCtrl* ctrl) {
   int K = RUIZ_MAX;

@@ -38,6 +38,9 @@ void launch_scale_vec(hipStream_t s, const double* u, const double* d, int n, do
 void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl);
 void launch_ruiz_sweep(hipStream_t s, const double* H, int ld, int n, const double* dcur, double* dnext,
                        DevCtrl* ctrl, int k);
+// The same sweep from the lower triangle only (64 x 64 tiles -> partials S[nbn][nbn*64] -> fixed-order row sums).
+void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np, const double* dcur, double* dnext,
+                           double* S, DevCtrl* ctrl, int k);
 void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl);
 // L[i][j] = d_i d_j H_ij (+reg on the diagonal), lower triangle; padded diagonal = 1.
 void launch_form_q(hipStream_t s, const double* H, double* L, int ld, int n, int np, const double* d,
