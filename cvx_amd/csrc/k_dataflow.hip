@@ -16,14 +16,21 @@
 // handed-off bytes is an sc1 access (relaxed agent-scope atomics), each storing wave drains with
 // s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane stores the state word; the consumer polls the
 // word with sc1 loads, then a workgroup barrier, then sc1 loads of the data.  One workgroup per CU.
-#include "potrf_block.hpp"
+#include "potrf64.hpp"
 
 namespace cvxg {
 
-typedef double d4f __attribute__((ext_vector_type(4)));
 
 constexpr int DF_SP = NB + 2;  // LDS row stride (doubles) of a staged 64 x 64 operand: conflict-free fragments
-constexpr int DF_SMEM = 10240;  // doubles (80 KB): > half the CU's LDS, so one workgroup per CU
+constexpr int DF_SMEM = 16384;  // doubles (128 KB): > half the CU's LDS, so one workgroup per CU
+
+// LDS of the critical-chain workgroup: POTRF's workspace (tile, L^-1, rhs) + the TRSM tile L_k+1,k + L' w_k
+struct ChainSmem {
+  Potrf64Smem p;
+  double Sa[NB * (NB + 2)];
+  double V[NB * MAX_RHS];
+};
+static_assert(sizeof(ChainSmem) <= DF_SMEM * sizeof(double), "chain workspace exceeds the dataflow LDS");
 
 __device__ __forceinline__ int df_tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
@@ -174,50 +181,106 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   int* state = work + 64;  // own cache lines
   const int tid = threadIdx.x;
   if (blockIdx.x == 0) {
-    // ---- workgroup 0: the critical chain POTRF(k) -> TRSM(k+1,k) -> UPDATE(k+1,k+1,k) -> POTRF(k+1) ----
+    // ---- workgroup 0: the critical chain POTRF(k) -> TRSM(k+1,k) -> UPDATE(k+1,k+1,k) -> POTRF(k+1), with the
+    // diagonal tile, L_kk^-1, w_k and L_k+1,k kept in LDS between the steps: the updated diagonal tile never
+    // leaves the workgroup (only POTRF's L_kk output is stored), and TRSM reads L_kk^-1 from POTRF's LDS.
+    ChainSmem& cs = *reinterpret_cast<ChainSmem*>(smem);
+    Potrf64Smem& ps = cs.p;
+    const int lane = tid & 63, wr = (tid >> 6) >> 1, wc = (tid >> 6) & 1;
+    auto mark = [&](int k, int step, int field) {
+      if (trace && tid == 0) trace[4 * (size_t)(ntasks + 3 * k + step) + field] = __builtin_amdgcn_s_memrealtime();
+    };
+    auto publish = [&](int idx, int v) {
+      df_drain();  // every storing wave: its sc1 stores have left
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(state + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto wait = [&](int idx, int want) -> bool {
+      if (tid == 0) s_ok = df_wait(state, idx, want, abortw, ctrl);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __syncthreads();
+      return s_ok;
+    };
+    potrf64_stage_tile<Sc1Mem>(L, ld, 0, ps);
+    potrf64_stage_rhs<Sc1Mem>(rhs, 0, nrhs, ps);
     for (int k = 0; k < nblk; ++k) {
-#pragma unroll 1
-      for (int step = 0; step < 3; ++step) {
-        if (step > 0 && k + 1 >= nblk) break;
-        if (tid == 0) {
-          bool ok;
-          if (step == 0) ok = df_wait(state, df_tri(k, k), k, abortw, ctrl);
-          else if (step == 1) ok = df_wait(state, df_tri(k + 1, k), k, abortw, ctrl);
-          else ok = df_wait(state, df_tri(k + 1, k + 1), k, abortw, ctrl);
-          s_ok = ok;
-          if (trace) {
-            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-            trace[4 * (size_t)(ntasks + 3 * k + step)] = now;
-            trace[4 * (size_t)(ntasks + 3 * k + step) + 1] = now;
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __syncthreads();
-        if (!s_ok) return;
-        int done_idx;
-        if (step == 0) {
-          if (!potrf_block<Sc1Mem>(L, ld, k, rhs, nrhs, Linv, ctrl, *reinterpret_cast<PotrfSmem*>(smem))) {
-            if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-          }
-          done_idx = df_tri(k, k);
-        } else if (step == 1) {
-          df_trsm(L, ld, k + 1, k, rhs, nrhs, Linv, smem);
-          done_idx = df_tri(k + 1, k);
-        } else {
-          df_update(L, ld, k + 1, k + 1, k, smem);
-          done_idx = df_tri(k + 1, k + 1);
-        }
-        df_drain();
-        __syncthreads();
-        if (tid == 0) {
-          __hip_atomic_store(state + done_idx, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (trace) {
-            trace[4 * (size_t)(ntasks + 3 * k + step) + 2] = __builtin_amdgcn_s_memrealtime();
-            trace[4 * (size_t)(ntasks + 3 * k + step) + 3] = 0;
-          }
-        }
+      mark(k, 0, 0);
+      mark(k, 0, 1);
+      if (!potrf64_factor<Sc1Mem>(L, ld, k, rhs, nrhs, Linv, ctrl, ps)) {
+        if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
       }
+      publish(df_tri(k, k), k + 1);
+      mark(k, 0, 2);
+      if (k + 1 >= nblk) break;
+      // TRSM(k+1,k): L' = A_k+1,k L_kk^-T (MFMA with L_kk^-1 from POTRF's LDS); V = L' w_k for the rhs
+      mark(k, 1, 0);
+      if (!wait(df_tri(k + 1, k), k)) return;
+      mark(k, 1, 1);
+      const Sc1Mem mA(L + (size_t)(k + 1) * NB * ld + (size_t)k * NB, tile_bytes(ld));
+      df_stage(cs.Sa, mA, ld);
+      __syncthreads();
+      d4f acc[2][2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = d4f{0.0, 0.0, 0.0, 0.0};
+      df_mfma(acc, cs.Sa, ps.X, 1.0, wr, wc, lane);
+      __syncthreads();  // every wave is done reading A from Sa
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+            mA.st(row * ld + col, acc[mi][nj][r]);
+            cs.Sa[row * DF_SP + col] = acc[mi][nj][r];
+          }
+      __syncthreads();
+      for (int t = tid; t < NB * nrhs; t += 256) {
+        const int row = t / nrhs, rho = t - row * nrhs;
+        double s0 = 0.0, s1 = 0.0;
+        for (int c = 0; c < NB; c += 2) {
+          s0 = fma(cs.Sa[row * DF_SP + c], ps.W[c * nrhs + rho], s0);
+          s1 = fma(cs.Sa[row * DF_SP + c + 1], ps.W[(c + 1) * nrhs + rho], s1);
+        }
+        cs.V[t] = s0 + s1;
+      }
+      publish(df_tri(k + 1, k), k + 1);
+      mark(k, 1, 2);
+      // UPDATE(k+1,k+1,k): the diagonal tile (all earlier updates applied by the queue) minus L' L'^T, into
+      // POTRF's staging area; the rhs block k+1 (all earlier TRSM updates applied) minus V
+      mark(k, 2, 0);
+      if (!wait(df_tri(k + 1, k + 1), k)) return;
+      mark(k, 2, 1);
+      if (wc <= wr) {
+        const Sc1Mem mC(L + (size_t)(k + 1) * NB * ld + (size_t)(k + 1) * NB, tile_bytes(ld));
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+              acc[mi][nj][r] = mC.ld(row * ld + col);
+            }
+        df_mfma(acc, cs.Sa, cs.Sa, -1.0, wr, wc, lane);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+              ps.S[row * P64_SP + col] = acc[mi][nj][r];
+            }
+      }
+      {
+        const Sc1Mem mR(rhs + (size_t)(k + 1) * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+        for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t) - cs.V[t];
+      }
+      mark(k, 2, 2);
     }
     return;
   }

@@ -1,14 +1,14 @@
-// k_potrf.hip — per-block launch of the 64x64 diagonal-block Cholesky (potrf_block.hpp), used by the
+// k_potrf.hip — per-block launch of the 64x64 diagonal-block Cholesky (potrf64.hpp), used by the
 // kernel-per-step blocked factorization (cvxg.cpp factor_attempt, CVXG_CHOL=blocked).
-#include "potrf_block.hpp"
+#include "potrf64.hpp"
 
 namespace cvxg {
 
 __global__ __launch_bounds__(256) void k_potrf_blocked(double* __restrict__ L, int ld, int k, double* __restrict__ rhs,
                                                        int nrhs, double* __restrict__ Linv, DevCtrl* ctrl) {
   if (ctrl->chol_info != 0) return;
-  __shared__ __attribute__((aligned(16))) PotrfSmem sm;
-  potrf_block<PlainMem>(L, ld, k, rhs, nrhs, Linv, ctrl, sm);
+  __shared__ __attribute__((aligned(16))) Potrf64Smem sm;
+  potrf64<PlainMem>(L, ld, k, rhs, nrhs, Linv, ctrl, sm);
 }
 
 void launch_potrf_diag(hipStream_t s, double* L, int ld, int k, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl) {

@@ -1,0 +1,330 @@
+// potrf64.hpp — 64x64 diagonal-block Cholesky (dpotrf 'L' semantics, MatrixUtils.scala:452-461 via Breeze
+// cholesky) with the block inverse and the fused forward substitution, built around the measured gfx950
+// latencies (microbench/lat.hip: v_readlane f64 ~44 cycles, rsq + 2 Newton ~50, FP64 FMA ~5, FP64 MFMA
+// 16x16x4 64 cycles, LDS store->load ~130).
+//
+// The 64 columns are processed as 4 steps of 16 (blocks kb = 0..3 of 16 x 16):
+//   P  wave 0 eliminates the 16 x 16 diagonal block D_kb with one lane per row: lanes 0-15 hold the rows
+//      of D (-> L16), lanes 16-31 the rows of the identity border (-> L16^-T), so ONE fma per column and
+//      element serves both, with the pivots and L_cj broadcast by v_readlane (no LDS, no barrier).
+//      Meanwhile waves 1..kb accumulate T_kb,j = sum_{m=j}^{kb-1} L_kb,m X_m,j (MFMA) for the off-diagonal
+//      blocks X_kb,j of L^-1 (block forward substitution of the inverse).
+//   T  waves 1..3: X_kb,j = -L16^-1 T_kb,j (the accumulator feeds the MFMA B operand directly: C layout
+//      register s is B slab s), or the panel TRSM L_ib,kb = A_ib,kb L16^-T (MFMA).
+//   U  A_ib,jb -= L_ib,kb L_jb,kb^T for kb < jb <= ib (MFMA); wave 0 takes the next diagonal block first
+//      and goes straight on to its elimination (no barrier between U and the next P).
+// Two workgroup barriers per step.  The rhs block is solved at the end as w = L^-1 b.
+//
+// potrf64<Mem> serves the per-block kernel (k_potrf.hip, plain accesses) and the persistent dataflow
+// factorization (k_dataflow.hip, sc1 accesses for inter-workgroup hand-offs).  256 threads.
+#pragma once
+#include <math.h>
+
+#include "kernels.hpp"
+
+namespace cvxg {
+
+typedef double d4f __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr int AUX_SC1 = 16;  // cache-policy bits of a buffer access: sc1 (L1 bypass, write-through)
+
+__device__ __forceinline__ double rsqrt_nr(double p) {
+  double y = __builtin_amdgcn_rsq(p);
+  const double h = 0.5 * p;
+  y = y * (1.5 - h * y * y);
+  y = y * (1.5 - h * y * y);
+  return y;
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Buffer descriptor over [base, base + bytes) built from values the compiler can see are wave-uniform
+// (otherwise each buffer op is wrapped in a readfirstlane waterfall loop).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const unsigned nb = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), 0, nb,
+                                           0x00020000);
+}
+
+// Memory policies over one region (a tile, a rhs block), addressed by double offsets.
+//   PlainMem: ordinary cached accesses (kernel boundaries order everything).
+//   Sc1Mem:   buffer_load/store ... sc1 — the inter-workgroup hand-off form used inside one launch
+//             (MI355X_MICROARCH.md, visibility: Valid forms, row 1).
+struct PlainMem {
+  double* p;
+  __device__ PlainMem(double* base, unsigned) : p(base) {}
+  __device__ __forceinline__ double ld(int off) const { return p[off]; }
+  __device__ __forceinline__ void st(int off, double v) const { p[off] = v; }
+  __device__ __forceinline__ f64x2 ld2(int off) const { return *reinterpret_cast<const f64x2*>(p + off); }
+};
+struct Sc1Mem {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ Sc1Mem(double* base, unsigned bytes) : r(uniform_rsrc(base, bytes)) {}
+  __device__ __forceinline__ double ld(int off) const {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off * 8, 0, AUX_SC1));
+  }
+  __device__ __forceinline__ void st(int off, double v) const {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off * 8, 0, AUX_SC1);
+  }
+  __device__ __forceinline__ f64x2 ld2(int off) const {  // 16 B, off even
+    return __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, off * 8, 0, AUX_SC1));
+  }
+};
+
+// bytes spanned by a 64 x 64 tile with leading dimension ld (for a tile descriptor)
+__host__ __device__ constexpr unsigned tile_bytes(int ld) { return (unsigned)((NB - 1) * ld + NB) * 8u; }
+
+// ---- 16 x 16 MFMA building blocks on LDS operands (f64 16x16x4: A lane l = (row l&15, k l>>4), B lane l =
+// (k l>>4, col l&15), C/D lane l reg i = (row (l>>4) + 4i, col l&15)) ----------------------------------------
+// acc += sgn * A B^T with A, B row-major 16 x 16 (B^T: the row of B is the column of the product)
+__device__ __forceinline__ d4f mfma16_abt(d4f acc, const double* a, int lda, const double* b, int ldb, double sgn,
+                                          int lane) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = 4 * s + (lane >> 4);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sgn * a[(lane & 15) * lda + k], b[(lane & 15) * ldb + k], acc, 0, 0, 0);
+  }
+  return acc;
+}
+// acc += sgn * A B with A, B row-major
+__device__ __forceinline__ d4f mfma16_ab(d4f acc, const double* a, int lda, const double* b, int ldb, double sgn,
+                                         int lane) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = 4 * s + (lane >> 4);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sgn * a[(lane & 15) * lda + k], b[k * ldb + (lane & 15)], acc, 0, 0, 0);
+  }
+  return acc;
+}
+__device__ __forceinline__ d4f c16_load(const double* c, int ldc, int lane) {
+  d4f v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = c[((lane >> 4) + 4 * i) * ldc + (lane & 15)];
+  return v;
+}
+__device__ __forceinline__ void c16_store(double* c, int ldc, d4f v, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[((lane >> 4) + 4 * i) * ldc + (lane & 15)] = v[i];
+}
+
+#ifdef POTRF_STAMPS  // microbench/potrf64_bench.hip: per-wave s_memtime stamps of the phases
+__device__ unsigned long long g_potrf_stamps[4][64];
+#define P64_STAMP(i)                                                          \
+  do {                                                                        \
+    if (lane == 0) g_potrf_stamps[w][(i)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+#else
+#define P64_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
+#ifndef P64_KB_UNROLL
+#define P64_KB_UNROLL 0
+#endif
+
+constexpr int P64_SP = NB + 2;  // LDS row stride (doubles) of the 64 x 64 work arrays: conflict-free fragments
+constexpr int P64_EP = 16 + 2;  // row stride of the 16 x 16 L16^-T blocks
+
+struct Potrf64Smem {
+  double S[NB * P64_SP];         // the tile: A -> L (lower blocks)
+  double X[NB * P64_SP];         // L^-1 (lower blocks)
+  double ET[4][16 * P64_EP];     // per step: L16^-T (row r = column r of L16^-1)
+  double B[NB * MAX_RHS];        // rhs block, row-major [64][nrhs]
+  double W[NB * MAX_RHS];        // forward-solved rhs block w = L^-1 b
+  int fail;
+};
+
+// Stage the 64 x 64 tile at (r0, c0) of L into sm.S (all 256 threads; no barrier).
+template <class M>
+__device__ __forceinline__ void potrf64_stage_tile(const double* L, int ld, size_t off, Potrf64Smem& sm) {
+  const int tid = threadIdx.x;
+  const M mL(const_cast<double*>(L) + off, tile_bytes(ld));
+  f64x2 v[NB * NB / 512];
+#pragma unroll
+  for (int q = 0; q < NB * NB / 512; ++q) {
+    const int idx = q * 256 + tid;
+    v[q] = mL.ld2((idx >> 5) * ld + 2 * (idx & 31));
+  }
+#pragma unroll
+  for (int q = 0; q < NB * NB / 512; ++q) {
+    const int idx = q * 256 + tid;
+    const int r = idx >> 5, c = 2 * (idx & 31);
+    sm.S[r * P64_SP + c] = v[q][0];
+    sm.S[r * P64_SP + c + 1] = v[q][1];
+  }
+}
+// Stage rhs block k into sm.B (no barrier).
+template <class M>
+__device__ __forceinline__ void potrf64_stage_rhs(const double* rhs, int k, int nrhs, Potrf64Smem& sm) {
+  const M mR(const_cast<double*>(rhs) + (size_t)k * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+  for (int t = threadIdx.x; t < NB * nrhs; t += 256) sm.B[t] = mR.ld(t);
+}
+
+// potrf64_factor: the tile is staged in sm.S and the rhs block in sm.B (barrier pending); on return sm.X holds
+// L^-1 (exact zeros above the diagonal) and sm.W the solved rhs block.
+template <class M>
+__device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __restrict__ rhs, int nrhs,
+                               double* __restrict__ Linv, DevCtrl* ctrl, Potrf64Smem& sm) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int base = k * NB;
+  const M mL(L + (size_t)base * ld + base, tile_bytes(ld));                         // the diagonal tile
+  const M mR(rhs + (size_t)base * nrhs, (unsigned)(NB * nrhs) * 8u);                // rhs block k
+  const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);                 // Linv[k]
+  double* S = sm.S;
+  double* X = sm.X;
+  {  // L^-1 is lower block-triangular: zero the six 16 x 16 blocks above the diagonal (read by callers' MFMAs)
+    for (int t = tid; t < 6 * 256; t += 256) {
+      const int b = t >> 8, e = t & 255;
+      const int ib = (b < 3) ? 0 : ((b < 5) ? 1 : 2), jb = (b < 3) ? 1 + b : ((b < 5) ? b - 1 : 3);
+      X[(16 * ib + (e >> 4)) * P64_SP + 16 * jb + (e & 15)] = 0.0;
+    }
+    if (tid == 0) sm.fail = 0;
+  }
+  double mind = __builtin_inf();
+  P64_STAMP(0);
+  __syncthreads();
+  P64_STAMP(1);
+
+#if P64_KB_UNROLL
+#pragma unroll
+#else
+#pragma unroll 1  // one copy of the step body: the instruction stream stays resident in the I-cache
+#endif
+  for (int kb = 0; kb < 4; ++kb) {
+    const int o = 16 * kb;
+    d4f T = {0.0, 0.0, 0.0, 0.0};
+    // ---- P: wave 0 eliminates D_kb; waves 1..kb accumulate T_kb,j (j = w - 1) --------------------------
+    if (w == 0) {
+      // lanes 0-15: row r of D (lower triangle), lanes 16-31: row r of the identity border.  Step j reads the
+      // still-unscaled column j (v_readlane, issued before the pivot's rsqrt chain, not after it) and
+      // applies  v_c -= (v_j / p) D_cj  for c > j, then scales v_j by p^-1/2 — one fma per element serves
+      // the L rows and the L^-T border rows alike.
+      const int r = lane & 15;
+      double a[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const double s = S[(o + r) * P64_SP + o + c];
+        a[c] = (lane < 16) ? ((c <= r) ? s : 0.0) : ((lane < 32 && c == r) ? 1.0 : 0.0);
+      }
+      int firstbad = -1;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        double lc[16];
+#pragma unroll
+        for (int c = j; c < 16; ++c) lc[c] = readlane_d(a[j], c);  // D_cj, c >= j (lower: lane c, column j)
+        const double piv = lc[j];
+        if (!(piv > 0.0) && firstbad < 0) firstbad = j;
+        const double rl = rsqrt_nr(piv);
+        mind = fmin(mind, piv * rl);
+        const double t = a[j] * (rl * rl);
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) a[c] = fma(-t, lc[c], a[c]);
+        a[j] *= rl;
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) S[(o + r) * P64_SP + o + c] = (c <= r) ? a[c] : 0.0;
+      } else if (lane < 32) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          sm.ET[kb][r * P64_EP + c] = a[c];        // L16^-T row r
+          X[(o + c) * P64_SP + o + r] = a[c];      // L^-1 diagonal block: X[c][r] = (L16^-1)[c][r]
+        }
+      }
+      if (firstbad >= 0) {
+        if (lane == 0) atomicCAS(&ctrl->chol_info, 0, base + o + firstbad + 1);
+        sm.fail = 1;
+      }
+    } else if (w <= kb) {
+      const int j = w - 1;
+#pragma unroll
+      for (int m = j; m < kb; ++m)
+        T = mfma16_ab(T, S + o * P64_SP + 16 * m, P64_SP, X + 16 * m * P64_SP + 16 * j, P64_SP, 1.0, lane);
+    }
+    P64_STAMP(2 + 4 * kb);
+    __syncthreads();
+    P64_STAMP(3 + 4 * kb);
+    if (sm.fail) return false;  // uniform: every wave reads the same flag after the barrier
+    // ---- T: X_kb,j = -L16^-1 T (waves 1..kb) / panel TRSM L_ib,kb = A_ib,kb L16^-T (waves kb+1..3) --------
+    const double* ET = sm.ET[kb];
+    if (w >= 1 && w <= kb) {
+      const int j = w - 1;
+      d4f acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)  // A = L16^-1 (row r = column r of ET), B slab s = T register s
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ET[(4 * s + (lane >> 4)) * P64_EP + (lane & 15)], T[s], acc, 0, 0,
+                                                   0);
+      c16_store(X + o * P64_SP + 16 * j, P64_SP, acc, lane);
+    } else if (w > kb) {
+      const int ib = w;
+      d4f acc = {0.0, 0.0, 0.0, 0.0};
+      acc = mfma16_ab(acc, S + 16 * ib * P64_SP + o, P64_SP, ET, P64_EP, 1.0, lane);
+      c16_store(S + 16 * ib * P64_SP + o, P64_SP, acc, lane);
+    }
+    P64_STAMP(4 + 4 * kb);
+    __syncthreads();
+    // ---- U: A_ib,jb -= L_ib,kb L_jb,kb^T, kb < jb <= ib; wave 0 takes the next diagonal block ------------
+    if (kb < 3) {
+      int idx = 0;
+#pragma unroll
+      for (int jb = kb + 1; jb < 4; ++jb)
+#pragma unroll
+        for (int ib = jb; ib < 4; ++ib) {
+          const bool next_diag = (ib == kb + 1 && jb == kb + 1);
+          const int owner = next_diag ? 0 : 1 + (idx++ % 3);
+          if (w == owner) {
+            double* C = S + 16 * ib * P64_SP + 16 * jb;
+            d4f acc = c16_load(C, P64_SP, lane);
+            acc = mfma16_abt(acc, S + 16 * ib * P64_SP + o, P64_SP, S + 16 * jb * P64_SP + o, P64_SP, -1.0, lane);
+            c16_store(C, P64_SP, acc, lane);
+          }
+        }
+    }
+    P64_STAMP(5 + 4 * kb);
+  }
+  __syncthreads();
+  P64_STAMP(20);
+  // ---- outputs: L block (lower), Linv = L^-1 (zero above the diagonal blocks), w = L^-1 b ----------------
+  for (int t = tid; t < NB * NB; t += 256) {
+    const int r = t >> 6, c = t & 63;
+    if (c <= r) mL.st(r * ld + c, S[r * P64_SP + c]);
+    mI.st(t, X[r * P64_SP + c]);
+  }
+  for (int t = tid; t < NB * nrhs; t += 256) {
+    const int r = t / nrhs, rho = t - r * nrhs;
+    double s0 = 0.0, s1 = 0.0;
+    const int cend = (r | 15) + 1;  // X is zero beyond the diagonal block of row r
+    for (int c = 0; c < cend; c += 2) {
+      s0 = fma(X[r * P64_SP + c], sm.B[c * nrhs + rho], s0);
+      s1 = fma(X[r * P64_SP + c + 1], sm.B[(c + 1) * nrhs + rho], s1);
+    }
+    mR.st(t, s0 + s1);
+    sm.W[t] = s0 + s1;
+  }
+  if (tid == 0) atomic_min_pos(&ctrl->min_diag, mind);  // the pivots are wave-uniform on wave 0
+  P64_STAMP(21);
+  return true;
+}
+
+// Factor block k of L (lower part of the 64x64 diagonal block), write L_kk, Linv[k] = L_kk^-1 and the
+// forward-solved rhs block.  Returns false (uniformly) on a non-positive pivot, after recording the
+// 1-based global pivot index in ctrl->chol_info.  Needs blockDim.x == 256.
+template <class M>
+__device__ bool potrf64(double* __restrict__ L, int ld, int k, double* __restrict__ rhs, int nrhs,
+                        double* __restrict__ Linv, DevCtrl* ctrl, Potrf64Smem& sm) {
+  potrf64_stage_tile<M>(L, ld, (size_t)k * NB * ld + (size_t)k * NB, sm);
+  potrf64_stage_rhs<M>(rhs, k, nrhs, sm);
+  return potrf64_factor<M>(L, ld, k, rhs, nrhs, Linv, ctrl, sm);
+}
+
+}  // namespace cvxg
