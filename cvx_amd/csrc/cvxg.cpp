@@ -220,15 +220,17 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
 }
 
 // Task order of the persistent dataflow Cholesky (k_dataflow.hip) for nb x nb tiles: the DAG
-// POTRF(k) -> TRSM(i,k) -> UPDATE(i,j,k) -> UPDATE(i,j,k+1) | POTRF(j) | TRSM(i,j) is list-scheduled on
-// `workers` simulated workgroups with estimated task times, highest bottom level (longest path to the
-// end) first among the ready tasks; the emitted order is the simulated start order, hence topological.
-// The critical chain tasks are simulated but not emitted (workgroup 0 runs them in sequence); every
-// transitive dependency of a chain task still precedes that task's dependents in the emitted order, which
-// keeps the launch deadlock-free.
-static std::vector<unsigned> build_chol_schedule(int nb, int workers) {
+// POTRF(k) -> TRSM(i,k) -> UPDATE(i,j,k..) -> next UPDATE of tile (i,j) | POTRF(j) | TRSM(i,j) is list-scheduled on
+// `workers` simulated workgroups with estimated task times, highest bottom level (longest path to the end)
+// first among the ready tasks; the emitted order is the simulated start order, hence topological.  A tile's
+// updates from panels k < j - `singles` are grouped four at a time (UPDATE4: one read-modify-write of the
+// tile for four panels); the last `singles` panels stay single so that a tile's final update is not held
+// back by its group.  The critical chain tasks POTRF(k), TRSM(k+1,k), UPDATE(k+1,k+1,k) are simulated but
+// not emitted (workgroup 0 runs them in sequence); every transitive dependency of a chain task still precedes
+// that task's dependents in the emitted order, which keeps the launch deadlock-free.
+static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles) {
   struct Task {
-    int type, i, j, k;
+    int type, i, j, k, cnt;
     double dur, bl, avail;
     int npred;
   };
@@ -236,8 +238,7 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers) {
   std::vector<int> potrf_id(nb), trsm_id((size_t)nb * nb, -1);
   std::vector<int> upd_base((size_t)nb * (nb + 1) / 2);
   auto tri = [](int i, int j) { return i * (i + 1) / 2 + j; };
-  // per-tile update ids: upd_base[tri(i,j)] + k, allocated lazily in topological enumeration order
-  std::vector<int> upd_id;
+  std::vector<int> upd_id;  // per tile (i,j) and panel k < j: the id of the update task that covers k
   {
     size_t tot = 0;
     for (int i = 0; i < nb; ++i)
@@ -247,18 +248,25 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers) {
       }
     upd_id.assign(tot, -1);
   }
-  const double d_potrf = 29.0, d_trsm = 6.0, d_upd = 5.5;  // us, measured (scripts/df_trace.py)
+  const double d_potrf = 18.0, d_trsm = 6.0, d_upd = 5.5, d_upd4 = 10.0;  // us (scripts/df_trace.py)
   for (int k = 0; k < nb; ++k) {  // (k, type) order is a topological order
     potrf_id[k] = (int)T.size();
-    T.push_back({0, k, k, k, d_potrf, 0, 0, k > 0 ? 1 : 0});
+    T.push_back({0, k, k, k, 1, d_potrf, 0, 0, k > 0 ? 1 : 0});
     for (int i = k + 1; i < nb; ++i) {
       trsm_id[(size_t)i * nb + k] = (int)T.size();
-      T.push_back({1, i, k, k, d_trsm, 0, 0, 1 + (k > 0 ? 1 : 0)});
+      T.push_back({1, i, k, k, 1, d_trsm, 0, 0, 1 + (k > 0 ? 1 : 0)});
     }
     for (int j = k + 1; j < nb; ++j)
       for (int i = j; i < nb; ++i) {
-        upd_id[upd_base[tri(i, j)] + k] = (int)T.size();
-        T.push_back({2, i, j, k, i == j ? 0.75 * d_upd : d_upd, 0, 0, (i == j ? 1 : 2) + (k > 0 ? 1 : 0)});
+        const bool grp = group && (k % 4 == 0) && (k + 4 <= j - singles);
+        const bool inside = group && (k % 4 != 0) && ((k & ~3) + 4 <= j - singles);
+        if (inside) continue;  // covered by the group starting at k & ~3
+        const int cnt = grp ? 4 : 1;
+        const int id = (int)T.size();
+        for (int kk = k; kk < k + cnt; ++kk) upd_id[upd_base[tri(i, j)] + kk] = id;
+        const int npanel = (i == j) ? cnt : 2 * cnt;
+        T.push_back({grp ? 3 : 2, i, j, k, cnt, (grp ? d_upd4 : d_upd) * (i == j ? 0.75 : 1.0), 0, 0,
+                     npanel + (k > 0 ? 1 : 0)});
       }
   }
   auto succ = [&](int t, std::vector<int>& out) {
@@ -266,13 +274,13 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers) {
     const Task& x = T[t];
     if (x.type == 0) {
       for (int i = x.k + 1; i < nb; ++i) out.push_back(trsm_id[(size_t)i * nb + x.k]);
-    } else if (x.type == 1) {
+    } else if (x.type == 1) {  // panel k of row i feeds tiles (i, j), k < j <= i, and (r, i), r > i
       const int i = x.i, k = x.k;
       for (int j = k + 1; j <= i; ++j) out.push_back(upd_id[upd_base[tri(i, j)] + k]);
       for (int r = i + 1; r < nb; ++r) out.push_back(upd_id[upd_base[tri(r, i)] + k]);
     } else {
-      const int i = x.i, j = x.j, k = x.k;
-      if (k + 1 < j) out.push_back(upd_id[upd_base[tri(i, j)] + k + 1]);
+      const int i = x.i, j = x.j, k1 = x.k + x.cnt;
+      if (k1 < j) out.push_back(upd_id[upd_base[tri(i, j)] + k1]);
       else if (i == j) out.push_back(potrf_id[j]);
       else out.push_back(trsm_id[(size_t)i * nb + j]);
     }
@@ -312,8 +320,6 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers) {
     ready.pop();
     const Task& x = T[t];
     now = std::max(now, x.avail);  // a task moved to `ready` by a later worker is not available earlier
-    // the critical chain POTRF(k) -> TRSM(k+1,k) -> UPDATE(k+1,k+1,k) -> POTRF(k+1) runs on workgroup 0
-    // (k_dataflow.hip) and is left out of the claimed order
     const bool chain = x.type == 0 || (x.type == 1 && x.i == x.k + 1) || (x.type == 2 && x.i == x.j && x.j == x.k + 1);
     if (!chain)
       order.push_back(((unsigned)x.type << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j);
@@ -811,7 +817,10 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     if (const char* e = getenv("CVXG_CHOL")) ctx->chol_dataflow = strcmp(e, "blocked") != 0;
     if (ctx->nblk > 1023) ctx->chol_dataflow = 0;  // task encoding holds 10-bit tile indices
     if (ctx->chol_dataflow) {
-      std::vector<unsigned> order = build_chol_schedule(ctx->nblk, ctx->ncu);
+      int group = 1, singles = 2;
+      if (const char* e = getenv("CVXG_DF_GROUP")) group = atoi(e) != 0;
+      if (const char* e = getenv("CVXG_DF_SINGLES")) singles = std::max(1, atoi(e));
+      std::vector<unsigned> order = build_chol_schedule(ctx->nblk, ctx->ncu, group, singles);
       ctx->df_ntasks = (int)order.size();
       CHK(dalloc(ctx, &ctx->df_tasks, order.size()));
       CHK(copy_sync(ctx, ctx->df_tasks, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));

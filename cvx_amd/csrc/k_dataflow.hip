@@ -22,7 +22,7 @@ namespace cvxg {
 
 
 constexpr int DF_SP = NB + 2;  // LDS row stride (doubles) of a staged 64 x 64 operand: conflict-free fragments
-constexpr int DF_SMEM = 16384;  // doubles (128 KB): > half the CU's LDS, so one workgroup per CU
+constexpr int DF_SMEM = 4 * NB * (NB + 2);  // doubles (132 KB: two double-buffered operand pairs): > half the CU's LDS, so one workgroup per CU
 
 // LDS of the critical-chain workgroup: POTRF's workspace (tile, L^-1, rhs) + the TRSM tile L_k+1,k + L' w_k
 struct ChainSmem {
@@ -73,6 +73,25 @@ __device__ __forceinline__ void df_stage(double* __restrict__ dst, const Sc1Mem&
   }
 }
 
+// The two halves of df_stage, for software pipelining: loads into registers, then LDS stores.
+__device__ __forceinline__ void df_load(f64x2 (&v)[NB * NB / 512], const Sc1Mem& m, int ld) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < NB * NB / 512; ++q) {
+    const int idx = q * 256 + tid;
+    v[q] = m.ld2((idx >> 5) * ld + 2 * (idx & 31));
+  }
+}
+__device__ __forceinline__ void df_put(double* __restrict__ dst, const f64x2 (&v)[NB * NB / 512]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < NB * NB / 512; ++q) {
+    const int idx = q * 256 + tid;
+    const int r = idx >> 5, c = 2 * (idx & 31);
+    *reinterpret_cast<f64x2*>(dst + r * DF_SP + c) = v[q];
+  }
+}
+
 // acc (wave (wr, wc): 32 x 32 block = 2 x 2 MFMA tiles) += sgn * P_i[rows] . P_j[cols]^T over K = 64.
 __device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, const double* Pj, double sgn, int wr,
                                         int wc, int lane) {
@@ -115,6 +134,59 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
   __syncthreads();
   if (active) {
     df_mfma(acc, Pi, Pj, -1.0, wr, wc, lane);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+          mC.st(row * ld + col, acc[mi][nj][r]);
+        }
+  }
+}
+
+// UPDATE4(i,j,k0): A_ij -= sum_{k=k0}^{k0+3} L_ik L_jk^T — one read-modify-write of the tile for four panels,
+// with the operand tiles of panel k+1 loaded into registers while the MFMAs of panel k run (two LDS buffers).
+__device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0, double* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const bool active = !(i == j && wc > wr);
+  const bool diag = (i == j);
+  const Sc1Mem mC(L + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
+  d4f acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+        acc[mi][nj][r] = mC.ld(row * ld + col);
+      }
+  f64x2 vi[NB * NB / 512], vj[NB * NB / 512];
+  auto tile = [&](int r, int k) { return Sc1Mem(L + (size_t)r * NB * ld + (size_t)k * NB, tile_bytes(ld)); };
+  df_load(vi, tile(i, k0), ld);
+  if (!diag) df_load(vj, tile(j, k0), ld);
+  df_put(smem, vi);
+  if (!diag) df_put(smem + NB * DF_SP, vj);
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q) {
+    double* Pi = smem + (q & 1) * 2 * NB * DF_SP;
+    double* Pj = diag ? Pi : Pi + NB * DF_SP;
+    if (q < 3) {
+      df_load(vi, tile(i, k0 + q + 1), ld);
+      if (!diag) df_load(vj, tile(j, k0 + q + 1), ld);
+    }
+    __syncthreads();  // panel q staged; every wave is done with panel q - 1 (the other buffer)
+    if (active) df_mfma(acc, Pi, Pj, -1.0, wr, wc, lane);
+    if (q < 3) {
+      double* Ni = smem + ((q + 1) & 1) * 2 * NB * DF_SP;
+      df_put(Ni, vi);
+      if (!diag) df_put(Ni + NB * DF_SP, vj);
+    }
+  }
+  if (active) {
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -305,6 +377,9 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       bool ok;
       if (type == 1) {
         ok = df_wait(state, df_tri(k, k), k + 1, abortw, ctrl) && df_wait(state, df_tri(i, k), k, abortw, ctrl);
+      } else if (type == 3) {  // panels k..k+3: TRSM(., k+3) done implies the earlier ones (tile order)
+        ok = df_wait(state, df_tri(i, k + 3), k + 4, abortw, ctrl) &&
+             df_wait(state, df_tri(j, k + 3), k + 4, abortw, ctrl) && df_wait(state, df_tri(i, j), k, abortw, ctrl);
       } else {
         ok = df_wait(state, df_tri(i, k), k + 1, abortw, ctrl) && df_wait(state, df_tri(j, k), k + 1, abortw, ctrl) &&
              df_wait(state, df_tri(i, j), k, abortw, ctrl);
@@ -315,10 +390,14 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the data loads behind the poll
     __syncthreads();
     if (!s_ok) break;
-    int done_idx;
+    int done_idx, done_val = k + 1;
     if (type == 1) {
       df_trsm(L, ld, i, k, rhs, nrhs, Linv, smem);
       done_idx = df_tri(i, k);
+    } else if (type == 3) {
+      df_update4(L, ld, i, j, k, smem);
+      done_idx = df_tri(i, j);
+      done_val = k + 4;
     } else {
       df_update(L, ld, i, j, k, smem);
       done_idx = df_tri(i, j);
@@ -326,7 +405,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     df_drain();  // every storing wave: its sc1 stores have left
     __syncthreads();
     if (tid == 0) {
-      __hip_atomic_store(state + done_idx, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(state + done_idx, done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (trace) {
         trace[4 * my_idx + 2] = __builtin_amdgcn_s_memrealtime();
         trace[4 * my_idx + 3] = blockIdx.x;

@@ -27,6 +27,7 @@ namespace cvxg {
 typedef double d4f __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int AUX_SC1 = 16;  // cache-policy bits of a buffer access: sc1 (L1 bypass, write-through)
 
 __device__ __forceinline__ double rsqrt_nr(double p) {
@@ -34,6 +35,13 @@ __device__ __forceinline__ double rsqrt_nr(double p) {
   const double h = 0.5 * p;
   y = y * (1.5 - h * y * y);
   y = y * (1.5 - h * y * y);
+  return y;
+}
+
+__device__ __forceinline__ double rcp_nr(double p) {
+  double y = __builtin_amdgcn_rcp(p);
+  y = y * (2.0 - p * y);
+  y = y * (2.0 - p * y);
   return y;
 }
 
@@ -65,6 +73,7 @@ struct PlainMem {
   __device__ __forceinline__ double ld(int off) const { return p[off]; }
   __device__ __forceinline__ void st(int off, double v) const { p[off] = v; }
   __device__ __forceinline__ f64x2 ld2(int off) const { return *reinterpret_cast<const f64x2*>(p + off); }
+  __device__ __forceinline__ void st2(int off, f64x2 v) const { *reinterpret_cast<f64x2*>(p + off) = v; }
 };
 struct Sc1Mem {
   __amdgpu_buffer_rsrc_t r;
@@ -77,6 +86,9 @@ struct Sc1Mem {
   }
   __device__ __forceinline__ f64x2 ld2(int off) const {  // 16 B, off even
     return __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, off * 8, 0, AUX_SC1));
+  }
+  __device__ __forceinline__ void st2(int off, f64x2 v) const {  // 16 B, off even
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off * 8, 0, AUX_SC1);
   }
 };
 
@@ -206,41 +218,64 @@ __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __
     // ---- P: wave 0 eliminates D_kb; waves 1..kb accumulate T_kb,j (j = w - 1) --------------------------
     if (w == 0) {
       // lanes 0-15: row r of D (lower triangle), lanes 16-31: row r of the identity border.  Step j reads the
-      // still-unscaled column j (v_readlane, issued before the pivot's rsqrt chain, not after it) and
-      // applies  v_c -= (v_j / p) D_cj  for c > j, then scales v_j by p^-1/2 — one fma per element serves
-      // the L rows and the L^-T border rows alike.
+      // still-unscaled column j with v_readlane and applies  v_c -= (v_j / p_j) D_cj  for c > j, then scales v_j
+      // by p_j^-1/2 — one fma per element serves the L rows and the L^-T border rows alike.  The next pivot is
+      // formed from uniform values, p_j+1 = D_j+1,j+1 - (D_j+1,j / p_j) D_j+1,j (bit-identical to lane j+1's own
+      // update), so the per-column dependency chain is only 1/p (rcp + Newton) and one fma; the rsqrt of the
+      // column scale and the element updates fill the issue slots beside it.
       const int r = lane & 15;
       double a[16];
+      {
+        const double* src = S + (o + r) * P64_SP + o;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const double s = S[(o + r) * P64_SP + o + c];
-        a[c] = (lane < 16) ? ((c <= r) ? s : 0.0) : ((lane < 32 && c == r) ? 1.0 : 0.0);
+        for (int c = 0; c < 16; c += 2) {
+          const f64x2 v = *reinterpret_cast<const f64x2*>(src + c);
+          a[c] = (lane < 16) ? ((c <= r) ? v[0] : 0.0) : ((lane < 32 && c == r) ? 1.0 : 0.0);
+          a[c + 1] = (lane < 16) ? ((c + 1 <= r) ? v[1] : 0.0) : ((lane < 32 && c + 1 == r) ? 1.0 : 0.0);
+        }
       }
+      P64_STAMP(22 + 3 * kb);
       int firstbad = -1;
+      double piv = readlane_d(a[0], 0);
+      double rinv = rcp_nr(piv);
+      double mypiv = 1.0;  // lane j keeps p_j: the column scales p_j^-1/2 are formed once, after the sweep
+      double pmin = piv;   // min_j L_jj = sqrt(min_j p_j)
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         double lc[16];
 #pragma unroll
-        for (int c = j; c < 16; ++c) lc[c] = readlane_d(a[j], c);  // D_cj, c >= j (lower: lane c, column j)
-        const double piv = lc[j];
+        for (int c = j + 1; c < 16; ++c) lc[c] = readlane_d(a[j], c);  // D_cj, c > j (lower: lane c, column j)
         if (!(piv > 0.0) && firstbad < 0) firstbad = j;
-        const double rl = rsqrt_nr(piv);
-        mind = fmin(mind, piv * rl);
-        const double t = a[j] * (rl * rl);
+        pmin = fmin(pmin, piv);
+        if (r == j) mypiv = piv;
+        const double rj = rinv;
+        if (j + 1 < 16) {
+          const double dn = readlane_d(a[j + 1], j + 1);
+          piv = fma(-(lc[j + 1] * rj), lc[j + 1], dn);
+          rinv = rcp_nr(piv);
+        }
+        const double t = a[j] * rj;
 #pragma unroll
         for (int c = j + 1; c < 16; ++c) a[c] = fma(-t, lc[c], a[c]);
-        a[j] *= rl;
       }
-      if (lane < 16) {
+      P64_STAMP(23 + 3 * kb);
+      {  // column scales: lane j forms p_j^-1/2, broadcast back per column
+        const double rlv = rsqrt_nr(mypiv);
+        mind = fmin(mind, pmin * rsqrt_nr(pmin));
 #pragma unroll
-        for (int c = 0; c < 16; ++c) S[(o + r) * P64_SP + o + c] = (c <= r) ? a[c] : 0.0;
-      } else if (lane < 32) {
+        for (int j = 0; j < 16; ++j) a[j] *= readlane_d(rlv, j);
+      }
+      if (lane < 32) {  // lanes 0-15: L16 row r -> S; lanes 16-31: L16^-T row r -> ET (one store stream)
+        double* dst = (lane < 16) ? S + (o + r) * P64_SP + o : sm.ET[kb] + r * P64_EP;
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          sm.ET[kb][r * P64_EP + c] = a[c];        // L16^-T row r
-          X[(o + c) * P64_SP + o + r] = a[c];      // L^-1 diagonal block: X[c][r] = (L16^-1)[c][r]
+        for (int c = 0; c < 16; c += 2) {
+          f64x2 v;
+          v[0] = (lane >= 16 || c <= r) ? a[c] : 0.0;
+          v[1] = (lane >= 16 || c + 1 <= r) ? a[c + 1] : 0.0;
+          *reinterpret_cast<f64x2*>(dst + c) = v;
         }
       }
+      P64_STAMP(24 + 3 * kb);
       if (firstbad >= 0) {
         if (lane == 0) atomicCAS(&ctrl->chol_info, 0, base + o + firstbad + 1);
         sm.fail = 1;
@@ -257,7 +292,13 @@ __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __
     if (sm.fail) return false;  // uniform: every wave reads the same flag after the barrier
     // ---- T: X_kb,j = -L16^-1 T (waves 1..kb) / panel TRSM L_ib,kb = A_ib,kb L16^-T (waves kb+1..3) --------
     const double* ET = sm.ET[kb];
-    if (w >= 1 && w <= kb) {
+    if (w == 0) {  // the L^-1 diagonal block is the transpose of L16^-T: X[o+c][o+r] = ET[r][c]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = lane + 64 * i, rr = e >> 4, cc = e & 15;
+        X[(o + cc) * P64_SP + o + rr] = ET[rr * P64_EP + cc];
+      }
+    } else if (w <= kb) {
       const int j = w - 1;
       d4f acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -294,22 +335,28 @@ __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __
   }
   __syncthreads();
   P64_STAMP(20);
-  // ---- outputs: L block (lower), Linv = L^-1 (zero above the diagonal blocks), w = L^-1 b ----------------
-  for (int t = tid; t < NB * NB; t += 256) {
-    const int r = t >> 6, c = t & 63;
-    if (c <= r) mL.st(r * ld + c, S[r * P64_SP + c]);
-    mI.st(t, X[r * P64_SP + c]);
+  // ---- outputs: L block (lower), Linv = L^-1, w = L^-1 b (4 threads per rhs entry) ------------------------
+  for (int t = tid; t < NB * NB / 2; t += 256) {
+    const int r = t >> 5, c = 2 * (t & 31);
+    const f64x2 l = *reinterpret_cast<const f64x2*>(S + r * P64_SP + c);
+    if (c + 1 <= r) mL.st2(r * ld + c, l);
+    else if (c <= r) mL.st(r * ld + c, l[0]);
+    mI.st2(r * NB + c, *reinterpret_cast<const f64x2*>(X + r * P64_SP + c));
   }
-  for (int t = tid; t < NB * nrhs; t += 256) {
-    const int r = t / nrhs, rho = t - r * nrhs;
-    double s0 = 0.0, s1 = 0.0;
-    const int cend = (r | 15) + 1;  // X is zero beyond the diagonal block of row r
-    for (int c = 0; c < cend; c += 2) {
-      s0 = fma(X[r * P64_SP + c], sm.B[c * nrhs + rho], s0);
-      s1 = fma(X[r * P64_SP + c + 1], sm.B[(c + 1) * nrhs + rho], s1);
+  for (int t0 = 0; t0 < NB * nrhs * 4; t0 += 256) {
+    const int t = t0 + tid, q = t & 3, e = t >> 2;
+    const int r = e / nrhs, rho = e - r * nrhs;
+    double s = 0.0;
+    if (e < NB * nrhs) {
+      const int c0 = 16 * q, cend = min(c0 + 16, (r | 15) + 1);  // X is zero beyond the diagonal block of row r
+      for (int c = c0; c < cend; ++c) s = fma(X[r * P64_SP + c], sm.B[c * nrhs + rho], s);
     }
-    mR.st(t, s0 + s1);
-    sm.W[t] = s0 + s1;
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (q == 0 && e < NB * nrhs) {
+      mR.st(e, s);
+      sm.W[e] = s;
+    }
   }
   if (tid == 0) atomic_min_pos(&ctrl->min_diag, mind);  // the pivots are wave-uniform on wave 0
   P64_STAMP(21);

@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_potrf_stamps), sizeof(st)));
   for (int wv = 0; wv < 4; ++wv) {
     printf("wave %d:", wv);
-    for (int i = 1; i < 22; ++i) printf(" %lld", (long long)(st[wv][i] - st[0][0]));
+    for (int i = 1; i < 38; ++i) printf(" %lld", (long long)(st[wv][i] - st[0][0]));
     printf("\n");
   }
 #endif

@@ -33,7 +33,7 @@ def main(path):
     span = done.max()
     nwg = int(tr[:, 3].max()) + 1
     print(f"tasks {n}  span {span:.1f} us  workgroups {nwg}")
-    for t, name in enumerate(["POTRF", "TRSM", "UPDATE"]):
+    for t, name in enumerate(["POTRF", "TRSM", "UPDATE", "UPDATE4"]):
         m = typ == t
         if m.any():
             print(f"{name:7s} n={m.sum():6d} run avg {np.mean(done[m] - ready[m]):7.2f} us  "
