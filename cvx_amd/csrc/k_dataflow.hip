@@ -252,13 +252,16 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   int* abortw = work + 1;
   int* state = work + 64;  // own cache lines
   const int tid = threadIdx.x;
-  if (blockIdx.x == 0) {
-    // ---- workgroup 0: the critical chain POTRF(k) -> TRSM(k+1,k) -> UPDATE(k+1,k+1,k) -> POTRF(k+1), with the
-    // diagonal tile, L_kk^-1, w_k and L_k+1,k kept in LDS between the steps: the updated diagonal tile never
-    // leaves the workgroup (only POTRF's L_kk output is stored), and TRSM reads L_kk^-1 from POTRF's LDS.
+  if (blockIdx.x < 2) {
+    // ---- workgroups 0 and 1: the critical chain, ping-pong.  Workgroup c factors the diagonal blocks b = c,
+    // c + 2, ...  Before POTRF(b) it runs TRSM(b, b-1) and UPDATE(b, b, b-1) in four 16-column slices, each
+    // started as soon as the other workgroup's POTRF(b-1) has published that row-block of L_b-1^-1
+    // (chain flags), so the next factorization starts ~one slice after the previous one ends.  The updated
+    // diagonal tile goes straight from the MFMA accumulators into this workgroup's POTRF workspace.
     ChainSmem& cs = *reinterpret_cast<ChainSmem*>(smem);
     Potrf64Smem& ps = cs.p;
-    const int lane = tid & 63, wr = (tid >> 6) >> 1, wc = (tid >> 6) & 1;
+    const int lane = tid & 63, wv = tid >> 6;
+    int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published
     auto mark = [&](int k, int step, int field) {
       if (trace && tid == 0) trace[4 * (size_t)(ntasks + 3 * k + step) + field] = __builtin_amdgcn_s_memrealtime();
     };
@@ -267,96 +270,122 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       __syncthreads();
       if (tid == 0) __hip_atomic_store(state + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    auto wait = [&](int idx, int want) -> bool {
-      if (tid == 0) s_ok = df_wait(state, idx, want, abortw, ctrl);
+    auto wait = [&](const int* base, int idx, int want) -> bool {
+      if (tid == 0) s_ok = df_wait(base, idx, want, abortw, ctrl);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       __syncthreads();
       return s_ok;
     };
-    potrf64_stage_tile<Sc1Mem>(L, ld, 0, ps);
-    potrf64_stage_rhs<Sc1Mem>(rhs, 0, nrhs, ps);
-    for (int k = 0; k < nblk; ++k) {
-      mark(k, 0, 0);
-      mark(k, 0, 1);
-      if (!potrf64_factor<Sc1Mem>(L, ld, k, rhs, nrhs, Linv, ctrl, ps)) {
+    // the 10 lower 16 x 16 blocks of a 64 x 64 tile, 3 / 3 / 2 / 2 per wave
+    constexpr int NBLK16 = 3;
+    const int blk_ib[4][NBLK16] = {{0, 3, 3}, {1, 3, 2}, {1, 3, -1}, {2, 2, -1}};
+    const int blk_jb[4][NBLK16] = {{0, 0, 3}, {0, 1, 2}, {1, 2, -1}, {0, 1, -1}};
+    for (int b = blockIdx.x; b < nblk; b += 2) {
+      if (b == 0) {
+        potrf64_stage_tile<Sc1Mem>(L, ld, 0, ps);
+        potrf64_stage_rhs<Sc1Mem>(rhs, 0, nrhs, ps);
+      } else {
+        const int k = b - 1;
+        mark(k, 1, 0);
+        if (!wait(state, df_tri(b, k), k)) return;
+        const Sc1Mem mA(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
+        df_stage(cs.Sa, mA, ld);
+        if (!wait(state, df_tri(b, b), k)) return;
+        mark(k, 1, 1);
+        d4f dacc[NBLK16];
+        {
+          const Sc1Mem mD(L + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
+#pragma unroll
+          for (int q = 0; q < NBLK16; ++q) {
+            const int ib = blk_ib[wv][q], jb = blk_jb[wv][q];
+            if (ib >= 0) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                dacc[q][r] = mD.ld((16 * ib + (lane >> 4) + 4 * r) * ld + 16 * jb + (lane & 15));
+            }
+          }
+        }
+        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
+        double* E = ps.ET[0];   // 16 rows of L_kk^-1, row stride DF_SP
+        double* Lp = ps.X;      // L_b,k, row stride DF_SP
+#pragma unroll 1
+        for (int cb = 0; cb < 4; ++cb) {
+          if (!wait(cflag, k, cb + 1)) return;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int e = tid + 256 * q, rr = e >> 5, cc = 2 * (e & 31);
+            *reinterpret_cast<f64x2*>(E + rr * DF_SP + cc) = mI.ld2((16 * cb + rr) * NB + cc);
+          }
+          __syncthreads();
+          {  // L'[16 wv.., 16 cb..] = A[16 wv.., :] L^-1[16 cb.., :]^T, K = 16 (cb + 1)
+            d4f acc = {0.0, 0.0, 0.0, 0.0};
+            const double* Ar = cs.Sa + 16 * wv * DF_SP;
+            for (int s = 0; s < 4 * (cb + 1); ++s) {
+              const int kk = 4 * s + (lane >> 4);
+              acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ar[(lane & 15) * DF_SP + kk], E[(lane & 15) * DF_SP + kk], acc,
+                                                         0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
+              Lp[row * DF_SP + col] = acc[r];
+              mA.st(row * ld + col, acc[r]);
+            }
+          }
+          __syncthreads();
+#pragma unroll
+          for (int q = 0; q < NBLK16; ++q) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
+            const int ib = blk_ib[wv][q], jb = blk_jb[wv][q];
+            if (ib >= 0)
+              dacc[q] = mfma16_abt(dacc[q], Lp + 16 * ib * DF_SP + 16 * cb, DF_SP, Lp + 16 * jb * DF_SP + 16 * cb, DF_SP,
+                                   -1.0, lane);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < NBLK16; ++q) {
+          const int ib = blk_ib[wv][q], jb = blk_jb[wv][q];
+          if (ib >= 0) c16_store(ps.S + 16 * ib * P64_SP + 16 * jb, P64_SP, dacc[q], lane);
+        }
+        publish(df_tri(b, k), k + 1);  // L_b,k stored
+        mark(k, 1, 2);
+        // rhs block b: all earlier TRSM updates are in (state(b,b) >= k), minus L_b,k w_k (w_k: POTRF(k) done)
+        mark(k, 2, 0);
+        if (!wait(state, df_tri(k, k), k + 1)) return;
+        mark(k, 2, 1);
+        {
+          const Sc1Mem mW(rhs + (size_t)k * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+          const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+          for (int t = tid; t < NB * nrhs; t += 256) ps.W[t] = mW.ld(t);
+          __syncthreads();
+          for (int t0 = 0; t0 < NB * nrhs * 4; t0 += 256) {
+            const int t = t0 + tid, q = t & 3, e = t >> 2;
+            const int r = e / nrhs, rho = e - r * nrhs;
+            double sv = 0.0;
+            if (e < NB * nrhs) {
+              for (int c = 16 * q; c < 16 * q + 16; ++c) sv = fma(Lp[r * DF_SP + c], ps.W[c * nrhs + rho], sv);
+            }
+            sv += __shfl_xor(sv, 1, 64);
+            sv += __shfl_xor(sv, 2, 64);
+            if (q == 0 && e < NB * nrhs) ps.B[e] = mR.ld(e) - sv;
+          }
+        }
+        mark(k, 2, 2);
+      }
+      // POTRF(b): tile and rhs block staged in LDS; L_bb^-1 row-blocks published progressively
+      mark(b, 0, 0);
+      mark(b, 0, 1);
+      if (!potrf64_factor<Sc1Mem>(L, ld, b, rhs, nrhs, Linv, ctrl, ps, cflag + b)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
-      publish(df_tri(k, k), k + 1);
-      mark(k, 0, 2);
-      if (k + 1 >= nblk) break;
-      // TRSM(k+1,k): L' = A_k+1,k L_kk^-T (MFMA with L_kk^-1 from POTRF's LDS); V = L' w_k for the rhs
-      mark(k, 1, 0);
-      if (!wait(df_tri(k + 1, k), k)) return;
-      mark(k, 1, 1);
-      const Sc1Mem mA(L + (size_t)(k + 1) * NB * ld + (size_t)k * NB, tile_bytes(ld));
-      df_stage(cs.Sa, mA, ld);
-      __syncthreads();
-      d4f acc[2][2];
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = d4f{0.0, 0.0, 0.0, 0.0};
-      df_mfma(acc, cs.Sa, ps.X, 1.0, wr, wc, lane);
-      __syncthreads();  // every wave is done reading A from Sa
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 2; ++nj)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
-            mA.st(row * ld + col, acc[mi][nj][r]);
-            cs.Sa[row * DF_SP + col] = acc[mi][nj][r];
-          }
-      __syncthreads();
-      for (int t = tid; t < NB * nrhs; t += 256) {
-        const int row = t / nrhs, rho = t - row * nrhs;
-        double s0 = 0.0, s1 = 0.0;
-        for (int c = 0; c < NB; c += 2) {
-          s0 = fma(cs.Sa[row * DF_SP + c], ps.W[c * nrhs + rho], s0);
-          s1 = fma(cs.Sa[row * DF_SP + c + 1], ps.W[(c + 1) * nrhs + rho], s1);
-        }
-        cs.V[t] = s0 + s1;
-      }
-      publish(df_tri(k + 1, k), k + 1);
-      mark(k, 1, 2);
-      // UPDATE(k+1,k+1,k): the diagonal tile (all earlier updates applied by the queue) minus L' L'^T, into
-      // POTRF's staging area; the rhs block k+1 (all earlier TRSM updates applied) minus V
-      mark(k, 2, 0);
-      if (!wait(df_tri(k + 1, k + 1), k)) return;
-      mark(k, 2, 1);
-      if (wc <= wr) {
-        const Sc1Mem mC(L + (size_t)(k + 1) * NB * ld + (size_t)(k + 1) * NB, tile_bytes(ld));
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int nj = 0; nj < 2; ++nj)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
-              acc[mi][nj][r] = mC.ld(row * ld + col);
-            }
-        df_mfma(acc, cs.Sa, cs.Sa, -1.0, wr, wc, lane);
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int nj = 0; nj < 2; ++nj)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
-              ps.S[row * P64_SP + col] = acc[mi][nj][r];
-            }
-      }
-      {
-        const Sc1Mem mR(rhs + (size_t)(k + 1) * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-        for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t) - cs.V[t];
-      }
-      mark(k, 2, 2);
+      publish(df_tri(b, b), b + 1);  // w_b and L_bb^-1 stored
+      mark(b, 0, 2);
+      potrf64_store_L<Sc1Mem>(L, ld, b, ps);  // only the final backward solve reads L_bb
+      __syncthreads();  // the potrf workspace is reused by the next TRSM slices
     }
     return;
   }
-  // ---- workgroups 1..: claim the remaining tasks in the host-built order ---------------------------
+  // ---- workgroups 2..: claim the remaining tasks in the host-built order ---------------------------
   int my_idx = -1;  // thread 0: claimed task index (trace)
   for (;;) {
     if (tid == 0) {
@@ -414,8 +443,9 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   }
 }
 
-// work: [0] counter, [1] abort word, [64 ..) one state word per lower tile; zeroed before every launch.
-size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2; }
+// work: [0] counter, [1] abort word, [64 ..) one state word per lower tile, then one chain flag per diagonal
+// block; zeroed before every launch.
+size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + nblk; }
 
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,

@@ -184,12 +184,16 @@ __device__ __forceinline__ void potrf64_stage_rhs(const double* rhs, int k, int 
 
 // potrf64_factor: the tile is staged in sm.S and the rhs block in sm.B (barrier pending); on return sm.X holds
 // L^-1 (exact zeros above the diagonal) and sm.W the solved rhs block.
+//
+// lflag != nullptr (dataflow chain): row-block kb of L^-1 is stored to Linv[k] as soon as it is final (after step
+// kb's T phase) by wave 3, which then raises *lflag = kb + 1 (sc1 hand-off: its own stores drained first), so
+// the other chain workgroup can start the next TRSM while this one is still factoring.  The L_kk tile is not
+// stored here in either case: potrf64_store_L.
 template <class M>
 __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __restrict__ rhs, int nrhs,
-                               double* __restrict__ Linv, DevCtrl* ctrl, Potrf64Smem& sm) {
+                               double* __restrict__ Linv, DevCtrl* ctrl, Potrf64Smem& sm, int* lflag = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
-  const M mL(L + (size_t)base * ld + base, tile_bytes(ld));                         // the diagonal tile
   const M mR(rhs + (size_t)base * nrhs, (unsigned)(NB * nrhs) * 8u);                // rhs block k
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);                 // Linv[k]
   double* S = sm.S;
@@ -314,6 +318,13 @@ __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __
     }
     P64_STAMP(4 + 4 * kb);
     __syncthreads();
+    if (lflag && w == 3) {  // publish row-block kb of L^-1 (final after the T phase)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int e = lane + 64 * q, rr = o + (e >> 5), cc = 2 * (e & 31);
+        mI.st2(rr * NB + cc, *reinterpret_cast<const f64x2*>(X + rr * P64_SP + cc));
+      }
+    }
     // ---- U: A_ib,jb -= L_ib,kb L_jb,kb^T, kb < jb <= ib; wave 0 takes the next diagonal block ------------
     if (kb < 3) {
       int idx = 0;
@@ -331,17 +342,20 @@ __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __
           }
         }
     }
+    if (lflag && w == 3) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(lflag, kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     P64_STAMP(5 + 4 * kb);
   }
   __syncthreads();
   P64_STAMP(20);
-  // ---- outputs: L block (lower), Linv = L^-1, w = L^-1 b (4 threads per rhs entry) ------------------------
-  for (int t = tid; t < NB * NB / 2; t += 256) {
-    const int r = t >> 5, c = 2 * (t & 31);
-    const f64x2 l = *reinterpret_cast<const f64x2*>(S + r * P64_SP + c);
-    if (c + 1 <= r) mL.st2(r * ld + c, l);
-    else if (c <= r) mL.st(r * ld + c, l[0]);
-    mI.st2(r * NB + c, *reinterpret_cast<const f64x2*>(X + r * P64_SP + c));
+  // ---- outputs: Linv = L^-1 (unless published progressively), w = L^-1 b (4 threads per rhs entry) --------
+  if (!lflag) {
+    for (int t = tid; t < NB * NB / 2; t += 256) {
+      const int r = t >> 5, c = 2 * (t & 31);
+      mI.st2(r * NB + c, *reinterpret_cast<const f64x2*>(X + r * P64_SP + c));
+    }
   }
   for (int t0 = 0; t0 < NB * nrhs * 4; t0 += 256) {
     const int t = t0 + tid, q = t & 3, e = t >> 2;
@@ -363,6 +377,18 @@ __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __
   return true;
 }
 
+// Store the factored diagonal tile L_kk (lower triangle) from sm.S (after potrf64_factor).
+template <class M>
+__device__ __forceinline__ void potrf64_store_L(double* __restrict__ L, int ld, int k, const Potrf64Smem& sm) {
+  const M mL(L + (size_t)k * NB * ld + (size_t)k * NB, tile_bytes(ld));
+  for (int t = threadIdx.x; t < NB * NB / 2; t += 256) {
+    const int r = t >> 5, c = 2 * (t & 31);
+    const f64x2 l = *reinterpret_cast<const f64x2*>(sm.S + r * P64_SP + c);
+    if (c + 1 <= r) mL.st2(r * ld + c, l);
+    else if (c <= r) mL.st(r * ld + c, l[0]);
+  }
+}
+
 // Factor block k of L (lower part of the 64x64 diagonal block), write L_kk, Linv[k] = L_kk^-1 and the
 // forward-solved rhs block.  Returns false (uniformly) on a non-positive pivot, after recording the
 // 1-based global pivot index in ctrl->chol_info.  Needs blockDim.x == 256.
@@ -371,7 +397,9 @@ __device__ bool potrf64(double* __restrict__ L, int ld, int k, double* __restric
                         double* __restrict__ Linv, DevCtrl* ctrl, Potrf64Smem& sm) {
   potrf64_stage_tile<M>(L, ld, (size_t)k * NB * ld + (size_t)k * NB, sm);
   potrf64_stage_rhs<M>(rhs, k, nrhs, sm);
-  return potrf64_factor<M>(L, ld, k, rhs, nrhs, Linv, ctrl, sm);
+  if (!potrf64_factor<M>(L, ld, k, rhs, nrhs, Linv, ctrl, sm)) return false;
+  potrf64_store_L<M>(L, ld, k, sm);
+  return true;
 }
 
 }  // namespace cvxg
