@@ -65,6 +65,9 @@ struct cvxg_ctx {
   int ntiles = 0, nsplit = 1;
   int ntiles_main = 0;  // tiles assembled without K split (whole waves of slots); the rest use nsplit
   int chol_outer = 4;  // 64-blocks per outer Cholesky panel (trailing update width 256)
+  int bwd_dataflow = 1;  // 1: one-launch backward substitution (k_bwd_dataflow); 0: one launch per block
+  int* bwd_flags = nullptr;
+  int bwd_gen = 0;
   int ruiz_full_rows = 0;  // 1: Ruiz sweeps over full rows of H (A/B reference for the lower-triangle sweep)
   int chol_dataflow = 1;  // 1: persistent tile-DAG factorization (k_dataflow.hip); 0: kernel per step
   int ncu = 256;
@@ -486,6 +489,11 @@ static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regula
 }
 
 static void backward_solve(cvxg_ctx* ctx, int nrhs) {
+  if (ctx->bwd_dataflow) {
+    launch_bwd_dataflow(ctx->s, ctx->L, ctx->np, ctx->Linv, ctx->rhs, ctx->sol, nrhs, ctx->nblk, ctx->bwd_flags,
+                        ++ctx->bwd_gen, ctx->ctrl);
+    return;
+  }
   for (int k = ctx->nblk - 1; k >= 0; --k)
     launch_bwd_step(ctx->s, ctx->L, ctx->np, ctx->Linv, k, ctx->rhs, ctx->sol, nrhs, ctx->ctrl);
 }
@@ -831,6 +839,8 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
       }
     }
   }
+  if (const char* e = getenv("CVXG_BWD")) ctx->bwd_dataflow = strcmp(e, "steps") != 0;
+  CHK(dalloc(ctx, &ctx->bwd_flags, ctx->nblk));
   CHK(dalloc(ctx, &ctx->rhs, np * MAX_RHS));
   CHK(dalloc(ctx, &ctx->sol, np * MAX_RHS));
   // SYRK tile list and wave plan (syrk_tile_plan): full-K tiles in whole waves of workgroup slots, the
@@ -876,7 +886,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
                   ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
-                  ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace};
+                  ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);

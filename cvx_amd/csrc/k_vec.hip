@@ -293,12 +293,29 @@ __global__ __launch_bounds__(256) void k_ruiz_rows(const double* __restrict__ S,
                                                    DevCtrl* ctrl, int k) {
   const double rho = __longlong_as_double((long long)ctrl->ruiz_rho[k]);
   if (!(rho > 1e-6)) return;
-  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  // 64 rows per workgroup; wave q adds the partials X = q, q + 4, ... (independent loads in flight), then the
+  // four wave sums are added in a fixed order.
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int row = blockIdx.x * 64 + lane;
   const int ldS = nbn * NB;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (row < n) {
+    int X = q;
+    for (; X + 12 < nbn; X += 16) {
+      s0 += S[(size_t)X * ldS + row];
+      s1 += S[(size_t)(X + 4) * ldS + row];
+      s2 += S[(size_t)(X + 8) * ldS + row];
+      s3 += S[(size_t)(X + 12) * ldS + row];
+    }
+    for (; X < nbn; X += 4) s0 += S[(size_t)X * ldS + row];
+  }
+  red[q][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (q != 0) return;
   double m = 0.0;
   if (row < n) {
-    double ssum = 0.0;
-    for (int X = 0; X < nbn; ++X) ssum += S[(size_t)X * ldS + row];
+    const double ssum = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
     const double di = dcur[row];
     const double u = sqrt(di * sqrt(ssum));        // sqrt(norm(Q(i,::)))   MatrixUtils.scala:258
     const double v = (u > 0) ? 1.0 / u : 1.0;      // :259
@@ -307,15 +324,15 @@ __global__ __launch_bounds__(256) void k_ruiz_rows(const double* __restrict__ S,
   } else if (row < np) {
     dnext[row] = 1.0;
   }
-  m = wave_max(m);  // every lane of the wave is live here (no early return above)
-  if ((threadIdx.x & 63) == 0 && m > 0.0) atomic_max_pos(&ctrl->ruiz_rho[k + 1], m);
+  m = wave_max(m);  // every lane of wave 0 is live here
+  if (lane == 0 && m > 0.0) atomic_max_pos(&ctrl->ruiz_rho[k + 1], m);
 }
 
 void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np, const double* dcur, double* dnext,
                            double* S, DevCtrl* ctrl, int k) {
   const int nbn = (n + NB - 1) / NB;
   k_ruiz_tiles<<<nbn * (nbn + 1) / 2, 256, 0, s>>>(H, ld, nbn, dcur, S, ctrl, k);
-  k_ruiz_rows<<<(np + 255) / 256, 256, 0, s>>>(S, nbn, n, np, dcur, dnext, ctrl, k);
+  k_ruiz_rows<<<(np + 63) / 64, 256, 0, s>>>(S, nbn, n, np, dcur, dnext, ctrl, k);
 }
 
 __global__ void k_ruiz_final(const double* __restrict__ d0, const double* __restrict__ d1, int np,

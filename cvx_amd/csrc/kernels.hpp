@@ -74,6 +74,9 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                           unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */);
 void launch_bwd_step(hipStream_t s, const double* L, int ld, const double* Linv, int k, double* rhs,
                      double* out, int nrhs, const DevCtrl* ctrl);
+// the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
+void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,
+                         int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl);
 
 // ---- line search ----------------------------------------------------------------------------------
 // For trials k in [0, LS_TRIALS): t_k = tbase*beta^k; g_i = c_i + t_k e_i; per-block partials of
