@@ -22,12 +22,13 @@ namespace cvxg {
 
 
 constexpr int DF_SP = NB + 2;  // LDS row stride (doubles) of a staged 64 x 64 operand: conflict-free fragments
-constexpr int DF_SMEM = 4 * NB * (NB + 2);  // doubles (132 KB: two double-buffered operand pairs): > half the CU's LDS, so one workgroup per CU
+constexpr int DF_SMEM = 4 * NB * (NB + 2) + 2 * 16 * (NB + 2) + 512;  // doubles (~142 KB): > half the CU's LDS, so one workgroup per CU
 
 // LDS of the critical-chain workgroup: POTRF's workspace (tile, L^-1, rhs) + the TRSM tile L_k+1,k + L' w_k
 struct ChainSmem {
   Potrf64Smem p;
-  double Sa[NB * (NB + 2)];
+  double Sa[NB * (NB + 2)];       // A_b,b-1 during the TRSM slices, then L_b,b-1 (for the last rhs correction)
+  double E2[2][16 * (NB + 2)];    // double-buffered row-blocks of L_b-1,b-1^-1
   double V[NB * MAX_RHS];
 };
 static_assert(sizeof(ChainSmem) <= DF_SMEM * sizeof(double), "chain workspace exceeds the dataflow LDS");
@@ -306,22 +307,47 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           }
         }
         const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
-        double* E = ps.ET[0];   // 16 rows of L_kk^-1, row stride DF_SP
         double* Lp = ps.X;      // L_b,k, row stride DF_SP
-#pragma unroll 1
-        for (int cb = 0; cb < 4; ++cb) {
-          if (!wait(cflag, k, cb + 1)) return;
+        // row-block cb of L_kk^-1 (published by the other workgroup's POTRF(k) as cflag[k] reaches cb + 1) is
+        // loaded into registers one slice ahead when it is already published, so its latency hides behind the
+        // MFMAs of the current slice
+        f64x2 er[2];
+        auto eload = [&](int cb) {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
-            const int e = tid + 256 * q, rr = e >> 5, cc = 2 * (e & 31);
-            *reinterpret_cast<f64x2*>(E + rr * DF_SP + cc) = mI.ld2((16 * cb + rr) * NB + cc);
+            const int e = tid + 256 * q;
+            er[q] = mI.ld2((16 * cb + (e >> 5)) * NB + 2 * (e & 31));
+          }
+        };
+        if (!wait(cflag, k, 1)) return;
+        eload(0);
+        bool have_next = false;
+#pragma unroll 1
+        for (int cb = 0; cb < 4; ++cb) {
+          double* E = cs.E2[cb & 1];
+          if (cb > 0 && !have_next) {
+            if (!wait(cflag, k, cb + 1)) return;
+            eload(cb);
+          }
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int e = tid + 256 * q;
+            *reinterpret_cast<f64x2*>(E + (e >> 5) * DF_SP + 2 * (e & 31)) = er[q];
+          }
+          have_next = false;
+          if (cb < 3) {  // non-blocking look at the next row-block
+            if (tid == 0) s_ok = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cb + 2;
           }
           __syncthreads();
+          if (cb < 3 && s_ok) {
+            have_next = true;
+            eload(cb + 1);
+          }
           {  // L'[16 wv.., 16 cb..] = A[16 wv.., :] L^-1[16 cb.., :]^T, K = 16 (cb + 1)
             d4f acc = {0.0, 0.0, 0.0, 0.0};
             const double* Ar = cs.Sa + 16 * wv * DF_SP;
-            for (int s = 0; s < 4 * (cb + 1); ++s) {
-              const int kk = 4 * s + (lane >> 4);
+            for (int s2 = 0; s2 < 4 * (cb + 1); ++s2) {
+              const int kk = 4 * s2 + (lane >> 4);
               acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ar[(lane & 15) * DF_SP + kk], E[(lane & 15) * DF_SP + kk], acc,
                                                          0, 0, 0);
             }
@@ -346,35 +372,49 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           const int ib = blk_ib[wv][q], jb = blk_jb[wv][q];
           if (ib >= 0) c16_store(ps.S + 16 * ib * P64_SP + 16 * jb, P64_SP, dacc[q], lane);
         }
+        // keep L_b,k for the rhs correction at the end of POTRF(b) (X is POTRF's workspace)
+        for (int t = tid; t < NB * NB / 2; t += 256) {
+          const int rr = t >> 5, cc = 2 * (t & 31);
+          *reinterpret_cast<f64x2*>(cs.Sa + rr * DF_SP + cc) = *reinterpret_cast<const f64x2*>(Lp + rr * DF_SP + cc);
+        }
+        {  // rhs block b with all earlier TRSM updates (state(b,b) >= k); minus L_b,k w_k inside POTRF(b)
+          const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+          for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
+        }
         publish(df_tri(b, k), k + 1);  // L_b,k stored
         mark(k, 1, 2);
-        // rhs block b: all earlier TRSM updates are in (state(b,b) >= k), minus L_b,k w_k (w_k: POTRF(k) done)
-        mark(k, 2, 0);
-        if (!wait(state, df_tri(k, k), k + 1)) return;
-        mark(k, 2, 1);
-        {
-          const Sc1Mem mW(rhs + (size_t)k * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-          const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-          for (int t = tid; t < NB * nrhs; t += 256) ps.W[t] = mW.ld(t);
-          __syncthreads();
-          for (int t0 = 0; t0 < NB * nrhs * 4; t0 += 256) {
-            const int t = t0 + tid, q = t & 3, e = t >> 2;
-            const int r = e / nrhs, rho = e - r * nrhs;
-            double sv = 0.0;
-            if (e < NB * nrhs) {
-              for (int c = 16 * q; c < 16 * q + 16; ++c) sv = fma(Lp[r * DF_SP + c], ps.W[c * nrhs + rho], sv);
-            }
-            sv += __shfl_xor(sv, 1, 64);
-            sv += __shfl_xor(sv, 2, 64);
-            if (q == 0 && e < NB * nrhs) ps.B[e] = mR.ld(e) - sv;
-          }
-        }
-        mark(k, 2, 2);
       }
-      // POTRF(b): tile and rhs block staged in LDS; L_bb^-1 row-blocks published progressively
+      // POTRF(b): tile and rhs block staged in LDS; L_bb^-1 row-blocks published progressively; before the
+      // forward solve, the rhs block gets its last correction  - L_b,b-1 w_b-1  (w_b-1: POTRF(b-1) done)
       mark(b, 0, 0);
       mark(b, 0, 1);
-      if (!potrf64_factor<Sc1Mem>(L, ld, b, rhs, nrhs, Linv, ctrl, ps, cflag + b)) {
+      auto fix = [&]() -> bool {
+        if (b == 0) return true;
+        const int k = b - 1;
+        mark(k, 2, 0);
+        if (tid == 0) s_ok = df_wait(state, df_tri(k, k), k + 1, abortw, ctrl);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        if (!s_ok) return false;
+        mark(k, 2, 1);
+        const Sc1Mem mW(rhs + (size_t)k * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+        for (int t = tid; t < NB * nrhs; t += 256) cs.V[t] = mW.ld(t);
+        __syncthreads();
+        for (int t0 = 0; t0 < NB * nrhs * 4; t0 += 256) {
+          const int t = t0 + tid, q = t & 3, e = t >> 2;
+          const int r = e / nrhs, rho = e - r * nrhs;
+          double sv = 0.0;
+          if (e < NB * nrhs) {
+            for (int c = 16 * q; c < 16 * q + 16; ++c) sv = fma(cs.Sa[r * DF_SP + c], cs.V[c * nrhs + rho], sv);
+          }
+          sv += __shfl_xor(sv, 1, 64);
+          sv += __shfl_xor(sv, 2, 64);
+          if (q == 0 && e < NB * nrhs) ps.B[e] -= sv;
+        }
+        mark(k, 2, 2);
+        return true;
+      };
+      if (!potrf64_factor<Sc1Mem>(L, ld, b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }

@@ -189,9 +189,16 @@ __device__ __forceinline__ void potrf64_stage_rhs(const double* rhs, int k, int 
 // kb's T phase) by wave 3, which then raises *lflag = kb + 1 (sc1 hand-off: its own stores drained first), so
 // the other chain workgroup can start the next TRSM while this one is still factoring.  The L_kk tile is not
 // stored here in either case: potrf64_store_L.
-template <class M>
+//
+// fix(): called by every thread after the last step, before the forward solve (barrier after it) — the chain uses
+// it to apply the last rhs correction, whose input (w of the other workgroup's block) is only ready by then.
+struct NoFix {
+  __device__ bool operator()() const { return true; }
+};
+template <class M, class Fix = NoFix>
 __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __restrict__ rhs, int nrhs,
-                               double* __restrict__ Linv, DevCtrl* ctrl, Potrf64Smem& sm, int* lflag = nullptr) {
+                               double* __restrict__ Linv, DevCtrl* ctrl, Potrf64Smem& sm, int* lflag = nullptr,
+                               Fix fix = Fix()) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mR(rhs + (size_t)base * nrhs, (unsigned)(NB * nrhs) * 8u);                // rhs block k
@@ -350,6 +357,8 @@ __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __
   }
   __syncthreads();
   P64_STAMP(20);
+  if (!fix()) return false;  // (uniform)
+  __syncthreads();
   // ---- outputs: Linv = L^-1 (unless published progressively), w = L^-1 b (4 threads per rhs entry) --------
   if (!lflag) {
     for (int t = tid; t < NB * NB / 2; t += 256) {
