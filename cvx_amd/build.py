@@ -8,7 +8,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcvxg.so")
-SOURCES = ["k_vec.hip", "k_syrk.hip", "k_chol.hip", "k_potrf.hip", "k_update.hip", "k_dataflow.hip", "cvxg.cpp"]
+SOURCES = ["k_vec.hip", "k_syrk.hip", "k_chol.hip", "k_potrf.hip", "k_update.hip", "k_dataflow.hip", "symsolve.cpp", "cvxg.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
@@ -24,7 +24,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not force and not needs_build():
         return OUT
     cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-pass-failed", "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+           "-Wno-pass-failed", "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + [
+        "-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True, cwd=CSRC)

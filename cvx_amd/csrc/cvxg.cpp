@@ -65,6 +65,11 @@ struct cvxg_ctx {
   int ntiles = 0, nsplit = 1;
   int ntiles_main = 0;  // tiles assembled without K split (whole waves of slots); the rest use nsplit
   int chol_outer = 4;  // 64-blocks per outer Cholesky panel (trailing update width 256)
+  // symSolve / kktSymSolve fallback buffers (allocated on first use; ldm = round_up(n + p, 128))
+  int eig_ldm = 0;
+  double *eig_M = nullptr, *eig_K = nullptr, *eig_d = nullptr, *eig_e = nullptr, *eig_dots = nullptr;
+  double *eig_a = nullptr, *eig_z = nullptr, *eig_b = nullptr, *eig_x = nullptr, *eig_part = nullptr;
+  int* eig_info = nullptr;
   int bwd_dataflow = 1;  // 1: one-launch backward substitution (k_bwd_dataflow); 0: one launch per block
   int* bwd_flags = nullptr;
   int bwd_gen = 0;
@@ -534,6 +539,64 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
   return CVXG_OK;
 }
 
+// MatrixUtils.symSolve(Mat, b, tol) (MatrixUtils.scala:734-751 -> diagonalizationSolve :603-706) on the device.
+// Mat: device row-major n2 x n2 with leading dimension eig_ldm and zero padding (kept for the residual);
+// b: host vector of length n2.  The solution is left in ctx->eig_x (length eig_ldm, zero padded).
+static int eig_alloc(cvxg_ctx* ctx) {
+  if (ctx->eig_M) return CVXG_OK;
+  const size_t l = (size_t)round_up(ctx->n + ctx->p, TILE);
+  ctx->eig_ldm = (int)l;
+  CHK(dalloc(ctx, &ctx->eig_M, l * l));
+  if (ctx->p > 0) CHK(dalloc(ctx, &ctx->eig_K, l * l));
+  for (double** v : {&ctx->eig_d, &ctx->eig_e, &ctx->eig_dots, &ctx->eig_a, &ctx->eig_z, &ctx->eig_b, &ctx->eig_x})
+    CHK(dalloc(ctx, v, l));
+  CHK(dalloc(ctx, &ctx->eig_part, (size_t)coldot_chunks((int)l) * l));
+  CHK(dalloc(ctx, &ctx->eig_info, 1));
+  return CVXG_OK;
+}
+
+static int sym_solve(cvxg_ctx* ctx, const double* Mat, int n2, const double* bdev, double tol) {
+  hipStream_t s = ctx->s;
+  const int l = ctx->eig_ldm;
+  const size_t bytes = (size_t)l * l * sizeof(double);
+  HIPC(ctx, hipMemcpyAsync(ctx->eig_M, Mat, bytes, hipMemcpyDeviceToDevice, s));
+  const int info = sym_eig(s, ctx->eig_M, n2, l, ctx->eig_d, ctx->eig_e, ctx->eig_info);
+  if (info != 0) return set_err(ctx, CVXG_E_UNSOLVABLE, "symSolve: eigSym failed (rocSOLVER dsyevd info %d)", info);
+  // eigenvector j = row j of the row-major view; rows >= n2 and eigenvalues >= n2 are padding
+  if (l > n2) {
+    HIPC(ctx, hipMemsetAsync(ctx->eig_M + (size_t)n2 * l, 0, (size_t)(l - n2) * l * sizeof(double), s));
+    HIPC(ctx, hipMemsetAsync(ctx->eig_d + n2, 0, (size_t)(l - n2) * sizeof(double), s));
+  }
+  // a_j = u_j.b (0 where d_j == 0), z_j = a_j / d_j
+  launch_rowdot(s, ctx->eig_M, l, l, l, bdev, ctx->eig_dots);
+  launch_eig_coeffs(s, ctx->eig_dots, ctx->eig_d, n2, l, ctx->eig_a, ctx->eig_z);
+  // b0 = U a: the projection of b onto Im(A); relativeSize(b - b0, b, tol) > tol -> unsolvable (:626-632)
+  launch_coldot_partials(s, ctx->eig_M, l, l, l, ctx->eig_a, ctx->eig_part);
+  launch_sum_chunks(s, ctx->eig_part, coldot_chunks(l), l, ctx->eig_dots);
+  launch_axpy(s, bdev, ctx->eig_dots, -1.0, l, ctx->eig_dots);
+  launch_dot(s, ctx->eig_dots, nullptr, l, ctx->ctrl, SC_RES2);
+  launch_dot(s, bdev, nullptr, l, ctx->ctrl, SC_B2);
+  // w = V z (:640), residual relativeSize(A w - b, b, tol) (:641)
+  launch_coldot_partials(s, ctx->eig_M, l, l, l, ctx->eig_z, ctx->eig_part);
+  launch_sum_chunks(s, ctx->eig_part, coldot_chunks(l), l, ctx->eig_x);
+  launch_rowdot(s, Mat, l, n2, l, ctx->eig_x, ctx->eig_dots);
+  launch_axpy(s, ctx->eig_dots, bdev, -1.0, n2, ctx->eig_dots);
+  launch_dot(s, ctx->eig_dots, nullptr, n2, ctx->ctrl, SC_RES2B);
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  const double nb = sqrt(ctx->hctrl->sc[SC_B2]);
+  const double f = nb < tol ? tol : tol + nb;
+  const double rel_dist = sqrt(ctx->hctrl->sc[SC_RES2]) / f, rel_err = sqrt(ctx->hctrl->sc[SC_RES2B]) / f;
+  if (rel_dist > tol)
+    return set_err(ctx, CVXG_E_UNSOLVABLE, "MatrixUtils.diagonalizationSolve: min_x||Ax-b||/||b|| = %.5g > tol = %g",
+                   rel_dist, tol);
+  if (rel_err > tol)  // the reference's regularization loop cannot change the outcome (see symsolve.cpp)
+    return set_err(ctx, CVXG_E_UNSOLVABLE,
+                   "MatrixUtils.diagonalizationSolve: system not solvable within tolerance tol = %g, error = %.5g",
+                   tol, rel_err);
+  return CVXG_OK;
+}
+
 // UnconstrainedSolver Newton direction with its fallback chain (UnconstrainedSolver.scala:54-67).
 static int newton_direction_p0(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
   int rc = cholesky_solve(ctx, pars->tolEqSolve, info);
@@ -548,8 +611,17 @@ static int newton_direction_p0(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step
   info->fallback = 1;
   if (rc == CVXG_OK || rc == CVXG_E_HIP) return rc;
   info->fallback = 2;
-  return set_err(ctx, CVXG_E_UNSOLVABLE,
-                 "symSolve fallback (eigen-decomposition, MatrixUtils.scala:734-751) reached: not in this build");
+  // symSolve(H, -y) (UnconstrainedSolver.scala:64)
+  CHK(eig_alloc(ctx));
+  HIPC(ctx, hipMemsetAsync(ctx->eig_b, 0, (size_t)ctx->eig_ldm * sizeof(double), ctx->s));
+  launch_axpy(ctx->s, ctx->eig_b, ctx->y, -1.0, ctx->n, ctx->eig_b);
+  CHK(sym_solve(ctx, ctx->H, ctx->n, ctx->eig_b, pars->tolEqSolve));
+  HIPC(ctx, hipMemsetAsync(ctx->dx, 0, (size_t)ctx->np * sizeof(double), ctx->s));
+  HIPC(ctx, hipMemcpyAsync(ctx->dx, ctx->eig_x, (size_t)ctx->n * sizeof(double), hipMemcpyDeviceToDevice, ctx->s));
+  launch_dot(ctx->s, ctx->dx, ctx->y, ctx->np, ctx->ctrl, SC_Q);
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  return CVXG_OK;
 }
 
 // KKTSystem.solvePD(Hm, Aeq, q, b) (KKTSystem.scala:200-246) with the block elimination of
@@ -628,7 +700,21 @@ static int newton_direction_kkt(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_ste
     return rc;
   }
   info->fallback = 2;
-  return set_err(ctx, CVXG_E_UNSOLVABLE, "kktSymSolve fallback (KKTSystem.scala:283-310) reached: not in this build");
+  // kktSymSolve(H, A, g = y, r = b - A x) (KKTSystem.scala:283-310): symSolve([H A'; A 0], (-g, r))
+  CHK(eig_alloc(ctx));
+  const int n = ctx->n, p = ctx->p, l = ctx->eig_ldm;
+  launch_kkt_matrix(s, ctx->H, ctx->np, ctx->Aeq, ctx->np, n, p, l, ctx->eig_K);
+  HIPC(ctx, hipMemsetAsync(ctx->eig_b, 0, (size_t)l * sizeof(double), s));
+  launch_axpy(s, ctx->eig_b, ctx->y, -1.0, n, ctx->eig_b);
+  HIPC(ctx, hipMemcpyAsync(ctx->eig_b + n, ctx->eqd, (size_t)p * sizeof(double), hipMemcpyDeviceToDevice, s));
+  CHK(sym_solve(ctx, ctx->eig_K, n + p, ctx->eig_b, pars->tolEqSolve));
+  HIPC(ctx, hipMemsetAsync(ctx->dx, 0, (size_t)ctx->np * sizeof(double), s));
+  HIPC(ctx, hipMemcpyAsync(ctx->dx, ctx->eig_x, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
+  HIPC(ctx, hipMemcpyAsync(ctx->kw, ctx->eig_x + n, (size_t)p * sizeof(double), hipMemcpyDeviceToDevice, s));
+  launch_dot(s, ctx->dx, ctx->y, ctx->np, ctx->ctrl, SC_Q);
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  return CVXG_OK;
 }
 
 static int newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
@@ -886,7 +972,9 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
                   ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
-                  ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags};
+                  ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
+                  ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
+                  ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);

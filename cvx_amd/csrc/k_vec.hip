@@ -165,6 +165,45 @@ void launch_axpy(hipStream_t s, const double* u, const double* v, double alpha, 
   k_axpy<<<(n + 255) / 256, 256, 0, s>>>(u, v, alpha, n, out);
 }
 
+// diagonalizationSolve coefficients (MatrixUtils.scala:625, 639): a_j = (|d_j| > 0) ? u_j.b : 0, z_j = a_j / d_j
+__global__ void k_eig_coeffs(const double* __restrict__ dots, const double* __restrict__ d, int n2, int npad,
+                             double* __restrict__ a, double* __restrict__ z) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= npad) return;
+  const bool nz = j < n2 && fabs(d[j]) > 0.0;
+  a[j] = nz ? dots[j] : 0.0;
+  z[j] = nz ? dots[j] / d[j] : 0.0;
+}
+void launch_eig_coeffs(hipStream_t s, const double* dots, const double* d, int n2, int npad, double* a, double* z) {
+  k_eig_coeffs<<<(npad + 255) / 256, 256, 0, s>>>(dots, d, n2, npad, a, z);
+}
+// out_i = sum_c part[c][i] in a fixed order (column-reduction partials of k_coldot_partials)
+__global__ void k_sum_chunks(const double* __restrict__ part, int nchunks, int cols, double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cols) return;
+  double s = 0.0;
+  for (int c = 0; c < nchunks; ++c) s += part[(size_t)c * cols + i];
+  out[i] = s;
+}
+void launch_sum_chunks(hipStream_t s, const double* part, int nchunks, int cols, double* out) {
+  k_sum_chunks<<<(cols + 255) / 256, 256, 0, s>>>(part, nchunks, cols, out);
+}
+// KKT matrix [H A'; A 0] (KKTSystem.scala kktMatrix), row-major (n + p) x (n + p) with leading dimension ld
+__global__ void k_kkt_matrix(const double* __restrict__ H, int ldh, const double* __restrict__ Aeq, int lda, int n,
+                             int p, int ld, double* __restrict__ K) {
+  const int i = blockIdx.y, j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ld) return;
+  double v = 0.0;
+  if (i < n && j < n) v = H[(size_t)i * ldh + j];
+  else if (i < n && j >= n && j < n + p) v = Aeq[(size_t)(j - n) * lda + i];
+  else if (i >= n && i < n + p && j < n) v = Aeq[(size_t)(i - n) * lda + j];
+  K[(size_t)i * ld + j] = v;
+}
+void launch_kkt_matrix(hipStream_t s, const double* H, int ldh, const double* Aeq, int lda, int n, int p, int ld,
+                       double* K) {
+  k_kkt_matrix<<<dim3((ld + 255) / 256, ld), 256, 0, s>>>(H, ldh, Aeq, lda, n, p, ld, K);
+}
+
 __global__ void k_scale_vec(const double* __restrict__ u, const double* __restrict__ d, int n,
                             double* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;

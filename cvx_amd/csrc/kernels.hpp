@@ -91,6 +91,13 @@ int ls_blocks(int m);
 void launch_kkt_schur(hipStream_t s, const double* X, int nrhs, const double* B, int ldb, int p, int n,
                       const double* bvec, double* w_out, double* xsol, DevCtrl* ctrl);
 
+// ---- symSolve / kktSymSolve fallback (symsolve.cpp, k_vec.hip) ----------------------------------------
+int sym_eig(hipStream_t s, double* M, int n2, int ldm, double* d, double* e_work, int* dinfo);
+void launch_eig_coeffs(hipStream_t s, const double* dots, const double* d, int n2, int npad, double* a, double* z);
+void launch_sum_chunks(hipStream_t s, const double* part, int nchunks, int cols, double* out);
+void launch_kkt_matrix(hipStream_t s, const double* H, int ldh, const double* Aeq, int lda, int n, int p, int ld,
+                       double* K);
+
 }  // namespace cvxg
 
 namespace cvxg {

@@ -299,3 +299,61 @@ def test_full_size_step_properties(mods, n, m):
     f2, _, _ = eng.barrier_eval(t, eng.get_x(), want_grad=False)
     assert f2 < f
     eng.close()
+
+
+# ---- failure-only fallbacks: symSolve / kktSymSolve on the device (rocSOLVER dsyevd + engine kernels) -------
+
+def _indefinite_qp(Z, n, m, instance):
+    """A QP whose objective Hessian has three negative eigenvalues: at t = 1e4 the barrier Hessian is
+    indefinite, both Cholesky attempts fail and the reference falls through to the eigen solve."""
+    spec = Z.random_qp(n, m, instance=instance)
+    rng = np.random.default_rng(100 + instance)
+    Q, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    lam = np.linspace(1.0, 3.0, n)
+    lam[-3:] = [-1.0, -2.0, -4.0]
+    P = (Q * lam) @ Q.T
+    spec["P"] = (P + P.T) / 2  # exactly symmetric
+    return spec
+
+
+def test_symsolve_fallback_vs_oracle(mods):
+    """UnconstrainedSolver.scala:54-67: choleskySolve(H) -> choleskySolve(H + 1e-9 I) -> symSolve(H, -y)."""
+    Z, SP, Engine, O = mods
+    spec = _indefinite_qp(Z, 30, 40, instance=61)
+    pb = _opb(O, spec)
+    eng = _engine(Engine, spec)
+    pars = SP.standardParams()
+    x, t = spec["x0"], 1e4
+    y = O.barrier_gradient(pb, t, x)
+    rec = O.NewtonStepRecord(x=x, grad=y, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
+    dref = O.newton_direction(pb, t, x, y, pars.tolEqSolve, rec)
+    assert rec.fallback == 2, "the test problem must reach the eigen fallback in the reference"
+    dx, _, info = eng.newton_direction(pars, t, x, grad=y)
+    assert info.fallback == 2
+    assert np.linalg.norm(dx - dref) / np.linalg.norm(dref) < 1e-8
+    assert abs(info.q - dx @ y) <= 1e-12 * abs(info.q)
+    eng.close()
+
+
+def test_kktsymsolve_fallback_vs_oracle(mods):
+    """KKTSystem.scala:43-66: solvePD(H) -> solvePD(H + A'A) -> kktSymSolve([H A'; A 0], (-g, r))."""
+    Z, SP, Engine, O = mods
+    n = 30
+    spec = _indefinite_qp(Z, n, 40, instance=62)
+    rng = np.random.default_rng(9)
+    spec["Aeq"] = rng.uniform(-1, 1, size=(2, n))
+    spec["beq"] = spec["Aeq"] @ np.full(n, 0.01)
+    pb = _opb(O, spec)
+    eng = _engine(Engine, spec)
+    pars = SP.standardParams()
+    x, t = np.zeros(n), 1e4
+    y = O.barrier_gradient(pb, t, x)
+    H = O.barrier_hessian(pb, t, x, literal=False)
+    info_ref = {}
+    dref, wref = O.kkt_solve(H, pb.Aeq, y, pb.beq - pb.Aeq @ x, pars.tolEqSolve, info_ref)
+    assert info_ref["fallback"] == 2
+    dx, w, info = eng.newton_direction(pars, t, x)
+    assert info.fallback == 2
+    assert np.linalg.norm(dx - dref) / np.linalg.norm(dref) < 1e-8
+    assert np.linalg.norm(w - wref) / np.linalg.norm(wref) < 1e-7
+    eng.close()
