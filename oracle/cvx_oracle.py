@@ -111,6 +111,10 @@ class Problem:
     ub: np.ndarray = None
     Aeq: Optional[np.ndarray] = None
     beq: Optional[np.ndarray] = None
+    # KL dual objective (Duality.objF over Dist_KL, Duality.scala:74-79): with B = kl_B (dualDim x n_outcomes),
+    # w = a0 and R = kl_R:  f(z) = w.z + R.exp(-B'z),  grad = w - B(R o exp(-B'z)),  Hessian = B diag(y) B'.
+    kl_B: Optional[np.ndarray] = None
+    kl_R: Optional[np.ndarray] = None
 
     @property
     def n(self) -> int:
@@ -121,9 +125,17 @@ class Problem:
         return self.A.shape[0]
 
 
+def kl_y(pb: Problem, z: np.ndarray) -> np.ndarray:
+    """Dist_KL.scala:163,170 — y = vec_R :* exp(-mat_B.t * z)."""
+    return pb.kl_R * np.exp(-(pb.kl_B.T @ z))
+
+
 def objective_value(pb: Problem, x: np.ndarray) -> float:
     """QuadraticObjectiveFunction.scala:31 — r + (a dot x) + (x dot (P*x))/2;
-    LinearObjectiveFunction.scala:19 — r + (a dot x)."""
+    LinearObjectiveFunction.scala:19 — r + (a dot x);
+    KL dual: -dualObjFAt(z) = (vec_w dot z) + (vec_R dot exp(-B'z)) (Dist_KL.scala:146-147, Duality.scala:76)."""
+    if pb.kl_B is not None:
+        return float(np.dot(pb.a0, x)) + float(np.dot(pb.kl_R, np.exp(-(pb.kl_B.T @ x))))
     v = pb.r0 + float(np.dot(pb.a0, x))
     if pb.P is not None:
         v = v + float(np.dot(x, pb.P @ x)) / 2
@@ -131,14 +143,22 @@ def objective_value(pb: Problem, x: np.ndarray) -> float:
 
 
 def objective_gradient(pb: Problem, x: np.ndarray) -> np.ndarray:
-    """QuadraticObjectiveFunction.scala:32 — a + P*x; LinearObjectiveFunction.scala:20 — a."""
+    """QuadraticObjectiveFunction.scala:32 — a + P*x; LinearObjectiveFunction.scala:20 — a;
+    KL dual: -gradientDualObjFAt(z) = vec_w - B*(vec_R :* exp(-B'z)) (Dist_KL.scala:152-153)."""
+    if pb.kl_B is not None:
+        return pb.a0 - pb.kl_B @ kl_y(pb, x)
     if pb.P is None:
         return pb.a0.copy()
     return pb.a0 + pb.P @ x
 
 
-def objective_hessian(pb: Problem) -> np.ndarray:
-    """QuadraticObjectiveFunction.scala:33 — P; LinearObjectiveFunction.scala:21 — zeros(n,n)."""
+def objective_hessian(pb: Problem, x: Optional[np.ndarray] = None) -> np.ndarray:
+    """QuadraticObjectiveFunction.scala:33 — P; LinearObjectiveFunction.scala:21 — zeros(n,n);
+    KL dual: -hessianDualObjFAt(z) = (B diag(y)) B' with the i,j loop of Dist_KL.scala:158-165."""
+    if pb.kl_B is not None:
+        y = kl_y(pb, x)
+        Bdy = pb.kl_B * y[None, :]
+        return -(-(Bdy @ pb.kl_B.T))
     if pb.P is None:
         return np.zeros((pb.n, pb.n))
     return pb.P
@@ -204,7 +224,7 @@ def barrier_hessian(pb: Problem, t: float, x: np.ndarray, literal: bool = True) 
     exact zeros (bit-identical result for d > 0).
     """
     n = pb.n
-    s = objective_hessian(pb) * t
+    s = objective_hessian(pb, x) * t
     for i in range(pb.m):
         d = pb.ub[i] - constraint_value(pb, i, x)
         if d <= 0:
@@ -736,3 +756,70 @@ def with_feasible_point(pb: Problem, x_where_defined: np.ndarray, pars: SolverPa
     if not is_in_set(pb, x_feas):
         raise ValueError("phase I point not strictly feasible")
     return x_feas
+
+
+# ----------------------------------------------------------------------------------------------
+# Kullback-Leibler distance minimisation via the dual barrier problem (Dist_KL.scala, Duality.scala)
+# ----------------------------------------------------------------------------------------------
+
+KL_E = 2.7182811828459045  # Dist_KL.scala:114 — NOT exp(1) = 2.718281828459045 (reference quirk, App. A 11)
+
+
+def kl_dual_problem(n: int, H: Optional[np.ndarray], u: Optional[np.ndarray], A: Optional[np.ndarray],
+                    r: Optional[np.ndarray]) -> Tuple[Problem, int]:
+    """Duality.dualProblem (Duality.scala:99-112) for Dist_KL (Dist_KL.scala:104-165): variables
+    z = (lambda, nu), dualDim = rows(H) + 1 + rows(A); objective -L_*(z); constraints lambda >= 0 as
+    firstCoordinatesPositive (Constraints.scala:26-48: a = -e_j, r = 0, ub = 0).  B = (H; 1'; A),
+    w = (u, 1, r), R_j = 1/(n e).  Returns (problem, numInequalities)."""
+    rows_B = []
+    w = []
+    if H is not None:
+        rows_B.append(np.asarray(H, dtype=np.float64))
+        w.append(np.asarray(u, dtype=np.float64))
+    rows_B.append(np.ones((1, n)))
+    w.append(np.ones(1))
+    if A is not None:
+        rows_B.append(np.asarray(A, dtype=np.float64))
+        w.append(np.asarray(r, dtype=np.float64))
+    B = np.vstack(rows_B)
+    wv = np.concatenate(w)
+    k = B.shape[0]
+    m = 0 if H is None else H.shape[0]
+    Ac = np.zeros((max(m, 0), k))
+    for j in range(m):
+        Ac[j, j] = -1.0
+    pb = Problem(a0=wv, r0=0.0, P=None, A=Ac, r=np.zeros(m), ub=np.zeros(m), kl_B=B,
+                 kl_R=np.full(n, 1.0 / (n * KL_E)))
+    return pb, m
+
+
+def kl_solve_dual(n: int, H, u, A, r, pars: SolverParams, record: bool = False):
+    """Duality.solveDual (Duality.scala:120-133): barrier solve of the dual from z0 = 0.001 (:106), then the
+    primal optimum Q = vec_R :* exp(-B'z) (Dist_KL.scala:170)."""
+    pb, m = kl_dual_problem(n, H, u, A, r)
+    z0 = np.full(pb.n, 0.001)
+    sol = barrier_solve(pb, z0, pars, record=record)
+    Q = kl_y(pb, sol.x)
+    return Q, sol, pb
+
+
+def kl1_analytic_solution(n: int) -> np.ndarray:
+    """OptimizationProblems.scala:136-141 (test fixture: the known minimiser of kl_1 / kl_1A)."""
+    j = np.arange(n)
+    if n <= 15:
+        return np.where(j < n // 2, 1.8 / n, 0.2 / n)
+    return np.where(j < 3, 0.12, np.where(j >= n // 2, 0.2 / n, 1.08 / (n - 6)))
+
+
+def kl1A_data(n: int):
+    """OptimizationProblems.scala:217-244: H = (-1_A; 1_B), u = (-0.36, 0.1), A = {0,1,2}, B = {n/2..n-1}."""
+    IA = (np.arange(n) < 3).astype(np.float64)
+    IB = (np.arange(n) >= n // 2).astype(np.float64)
+    return np.vstack([-IA, IB]), np.array([-0.36, 0.1])
+
+
+def kl2A_data(n: int):
+    """OptimizationProblems.scala:341-370: equalities (1_A; 1_B) Q = (0.36, 0.1)."""
+    IA = (np.arange(n) < 3).astype(np.float64)
+    IB = (np.arange(n) >= n // 2).astype(np.float64)
+    return np.vstack([IA, IB]), np.array([0.36, 0.1])

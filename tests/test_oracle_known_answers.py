@@ -161,3 +161,44 @@ def test_barrier_path_random_qp_small():
     assert sol.dualityGap < pars.tolSolver
     assert O.is_in_set(pb, sol.x)
     assert sol.newton_steps == len(sol.records) > 10
+
+
+# ---- Dist_KL via the dual barrier problem (Dist_KL.scala, Duality.scala) --------------------------------
+
+@pytest.mark.parametrize("n", [20, 2048])
+def test_kl1A_dual_known_minimizer(n):
+    """OptimizationProblems.kl_1A + MinimizationTests 'Solution via Duality with BarrierSolver': the primal
+    optimum from the dual matches kl1_analyticSolution (reference tolerance 1e-2; the restatement reaches ~1e-9)."""
+    H, u = O.kl1A_data(n)
+    Q, sol, pb = O.kl_solve_dual(n, H, u, None, None, O.standard_params())
+    assert pb.n == 3 and pb.m == 2
+    assert np.max(np.abs(Q - O.kl1_analytic_solution(n))) < 1e-6
+    assert abs(Q.sum() - 1.0) < 1e-8
+
+
+@pytest.mark.parametrize("n", [20, 2048])
+def test_kl2A_dual_known_minimizer(n):
+    """OptimizationProblems.kl_2A: equality-only KL problem, dual has no inequalities (one centering)."""
+    A, r = O.kl2A_data(n)
+    Q, sol, pb = O.kl_solve_dual(n, None, None, A, r, O.standard_params())
+    assert pb.m == 0
+    assert np.max(np.abs(Q - O.kl1_analytic_solution(n))) < 1e-6
+
+
+def test_kl_dual_oracles_are_consistent():
+    """Gradient and Hessian of the KL dual objective against central differences."""
+    rng = np.random.default_rng(4)
+    n = 50
+    H = rng.uniform(0, 1, size=(4, n))
+    pb, m = O.kl_dual_problem(n, H, rng.uniform(0.3, 0.6, 4), None, None)
+    z = rng.uniform(0.0, 0.5, pb.n)
+    g = O.objective_gradient(pb, z)
+    Hs = O.objective_hessian(pb, z)
+    h = 1e-6
+    for i in range(pb.n):
+        e = np.zeros(pb.n)
+        e[i] = h
+        assert abs((O.objective_value(pb, z + e) - O.objective_value(pb, z - e)) / (2 * h) - g[i]) < 1e-7
+        dg = (O.objective_gradient(pb, z + e) - O.objective_gradient(pb, z - e)) / (2 * h)
+        assert np.max(np.abs(dg - Hs[:, i])) < 1e-7
+    assert O.KL_E != np.e  # the reference's constant (Dist_KL.scala:114) is kept, not exp(1)
