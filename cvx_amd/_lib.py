@@ -67,6 +67,7 @@ SIGNATURES = {
     "cvxg_last_error": (C.c_char_p, [_P]),
     "cvxg_version": (C.c_char_p, []),
     "cvxg_set_objective": (C.c_int, [_P, _D, C.c_int, _D, C.c_double]),
+    "cvxg_set_objective_kl": (C.c_int, [_P, _D, C.c_int, C.c_int, C.c_int, _D, C.c_double]),
     "cvxg_set_ineq": (C.c_int, [_P, _D, C.c_int, C.c_int, _D, _D]),
     "cvxg_set_eq": (C.c_int, [_P, _D, C.c_int, C.c_int, _D]),
     "cvxg_set_x": (C.c_int, [_P, _D]),

@@ -56,6 +56,8 @@ class Solution:
     maxedOut: bool
     newtonSteps: int = 0
     outerIters: int = 0
+    lambda_: Optional[np.ndarray] = None  # dual solutions (Duality.solveDual, Duality.scala:127-131)
+    nu: Optional[np.ndarray] = None
 
 
 class ObjectiveFunction:
@@ -113,6 +115,29 @@ class LinearObjectiveFunction(ObjectiveFunction):
 
     def hessianAt(self, x):
         return np.zeros((self.dim, self.dim))
+
+
+class DualKLObjectiveFunction(ObjectiveFunction):
+    """Duality.objF over Dist_KL (Duality.scala:74-79, Dist_KL.scala:146-165): the convex form -L_*(z) of the
+    KL dual, z = (lambda, nu).  B = mat_B (dualDim x n), w = vec_w, R = vec_R's constant 1/(n e)."""
+
+    def __init__(self, B, w, R: float):
+        self.B = np.asarray(B, dtype=np.float64)
+        self.w = np.asarray(w, dtype=np.float64)
+        self.R = float(R)
+        super().__init__(self.B.shape[0])
+
+    def _y(self, z):
+        return self.R * np.exp(-(self.B.T @ np.asarray(z, dtype=np.float64)))
+
+    def valueAt(self, z):
+        return float(self.w @ z) + float(np.sum(self._y(z)))
+
+    def gradientAt(self, z):
+        return self.w - self.B @ self._y(z)
+
+    def hessianAt(self, z):
+        return (self.B * self._y(z)[None, :]) @ self.B.T
 
 
 class LinearConstraint:
@@ -252,8 +277,8 @@ class GpuBarrierSolver:
 
     def __init__(self, objF: ObjectiveFunction, cnts: ConstraintSet, eqs: Optional[EqualityConstraint],
                  pars: SolverParams, device: int = 0):
-        if not isinstance(objF, (QuadraticObjectiveFunction, LinearObjectiveFunction)):
-            raise TypeError("GPU barrier engine: objective must be Quadratic- or LinearObjectiveFunction")
+        if not isinstance(objF, (QuadraticObjectiveFunction, LinearObjectiveFunction, DualKLObjectiveFunction)):
+            raise TypeError("GPU barrier engine: objective must be Quadratic-, Linear- or DualKLObjectiveFunction")
         if cnts.feasiblePoint is None:
             raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
         p = 0 if eqs is None else eqs.A.shape[0]
@@ -264,7 +289,10 @@ class GpuBarrierSolver:
         self.startingPoint = cnts.feasiblePoint
         A, r, ub = cnts.packed()
         self.engine = Engine(cnts.dim, A.shape[0], p, device)
-        self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
+        if isinstance(objF, DualKLObjectiveFunction):
+            self.engine.set_objective_kl(objF.B, objF.w, objF.R)
+        else:
+            self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
         self.engine.set_ineq(A, r, ub)
         if p:
             self.engine.set_eq(eqs.A, eqs.b)
@@ -319,6 +347,68 @@ class OptimizationProblem:
         return OptimizationProblem.apply(id, objF, ineqs.withFeasiblePoint(eqs, pars), eqs, solverType, pars, device)
 
 
+class Dist_KL(OptimizationProblem):
+    """Dist_KL (Dist_KL.scala:68-177) with Duality (Duality.scala): argmin_Q dist_KL(Q, uniform) s.t. HQ <= u,
+    AQ = r, solved through the dual barrier problem on the MI355X engine.  The direct (primal) solve has a
+    non-quadratic objective and stays outside this engine."""
+
+    E = 2.7182811828459045  # Dist_KL.scala:114 (reference constant, not exp(1))
+
+    def __init__(self, id: str, n: int, H=None, u=None, A=None, r=None, device: int = 0):
+        assert n > 0, f"n={n} is not positive."
+        assert H is not None or A is not None, "Must have some inequality or equality constraints"
+        assert (H is None) == (u is None) and (A is None) == (r is None)
+        self.id, self.n, self.device = id, n, device
+        self.H = None if H is None else np.asarray(H, dtype=np.float64)
+        self.u = None if u is None else np.asarray(u, dtype=np.float64)
+        self.A = None if A is None else np.asarray(A, dtype=np.float64)
+        self.r = None if r is None else np.asarray(r, dtype=np.float64)
+        self.numInequalities = 0 if self.H is None else self.H.shape[0]
+        ones = np.ones((1, n))
+        self.mat_B = np.vstack(([self.H] if self.H is not None else []) + [ones] + ([self.A] if self.A is not None else []))
+        self.vec_w = np.concatenate(([self.u] if self.u is not None else []) + [np.ones(1)] +
+                                    ([self.r] if self.r is not None else []))
+        self.dualDim = self.mat_B.shape[0]
+        self.R = 1.0 / (n * Dist_KL.E)
+        super().__init__(id, None, None)
+
+    @staticmethod
+    def apply(id, n, H, u, A, r, solverType: str = "BR", pars=None, device: int = 0) -> "Dist_KL":
+        """Dist_KL.apply (Dist_KL.scala:264-315); solverType "BR" (the dual runs on the GPU engine)."""
+        if solverType not in ("BR", "GPU"):
+            raise ValueError(f"Unknown solver: {solverType}")
+        return Dist_KL(id, n, H, u, A, r, device)
+
+    def primalOptimum(self, z):
+        """Dist_KL.scala:170: Q = vec_R :* exp(-mat_B.t * z)."""
+        return self.R * np.exp(-(self.mat_B.T @ np.asarray(z, dtype=np.float64)))
+
+    def dualProblem(self, solverType: str, pars: SolverParams) -> OptimizationProblem:
+        """Duality.scala:99-112: min -L_*(z) s.t. lambda = z[:numInequalities] >= 0, from z0 = 0.001."""
+        k = self.dualDim
+        cnts = []
+        for j in range(self.numInequalities):  # Constraints.firstCoordinatesPositive (Constraints.scala:26-48)
+            a = np.zeros(k)
+            a[j] = -1.0
+            cnts.append(LinearConstraint(f"x_{j}>0", k, 0.0, 0.0, a))
+        ineqs = ConstraintSet(k, cnts, np.zeros(k)).addFeasiblePoint(np.full(k, 0.001))
+        objF = DualKLObjectiveFunction(self.mat_B, self.vec_w, self.R)
+        return OptimizationProblem.apply(self.id + " dual problem", objF, ineqs, None, solverType, pars, self.device)
+
+    def solveDual(self, solverType: str = "BR", pars: Optional[SolverParams] = None) -> Solution:
+        """Duality.scala:120-133: solve the dual, map z to the primal optimum."""
+        pars = pars or SolverParams.standardParams()
+        solD = self.dualProblem(solverType, pars).solve()
+        z = solD.x
+        solD.x = self.primalOptimum(z)
+        solD.lambda_ = z[:self.numInequalities]
+        solD.nu = z[self.numInequalities:] if self.dualDim > self.numInequalities else None
+        return solD
+
+    def solve(self, debugLevel: int = 0) -> Solution:
+        raise TypeError("Dist_KL direct solve: the primal KL objective is not on the GPU engine; use solveDual")
+
+
 def problem_from_spec(spec: dict):
     """(objF, ConstraintSet, EqualityConstraint|None) from a cvx_amd.problems spec dict."""
     n = spec["a0"].shape[0]
@@ -331,5 +421,6 @@ def problem_from_spec(spec: dict):
 
 
 __all__ = ["SolverParams", "Solution", "ObjectiveFunction", "QuadraticObjectiveFunction", "LinearObjectiveFunction",
+           "DualKLObjectiveFunction", "Dist_KL",
            "LinearConstraint", "EqualityConstraint", "ConstraintSet", "GpuBarrierSolver", "BarrierSolver",
            "OptimizationProblem", "problem_from_spec", "CvxgError", "NotStrictlyFeasible"]

@@ -42,6 +42,7 @@ enum {
   SC_EQ2,       // |b - Aeq x|^2
   SC_RES2B,     // second KKT residual |A x - b|^2
   SC_B2,        // |b|^2 (KKT)
+  SC_KLSUM,     // KL dual: sum_j R exp(-(B'z)_j)
   SC_COUNT
 };
 

@@ -42,6 +42,11 @@ struct cvxg_ctx {
   // problem
   double* P = nullptr;
   int hasP = 0;
+  // KL dual objective (cvxg_set_objective_kl): KB = B' (nout x n, row-major, padded noutp x np), R = 1/(n e)
+  int kl = 0, nout = 0, noutp = 0;
+  double kl_R = 0.0;
+  double *KB = nullptr, *kl_v = nullptr, *kl_y = nullptr, *kl_u = nullptr, *kl_negBy = nullptr;
+  double *kl_part = nullptr, *kl_ls = nullptr;
   double* a0 = nullptr;
   double r0 = 0.0;
   double *A = nullptr, *r = nullptr, *ub = nullptr;
@@ -347,6 +352,13 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
 // Device pipeline pieces
 // ------------------------------------------------------------------------------------------------
 
+// objF.valueAt(x) from the reduced scalars: r + a.x (+ x'Px/2) (QuadraticObjectiveFunction.scala:31), or the
+// KL dual  w.z + R.exp(-B'z)  (Dist_KL.scala:146-147 negated by Duality.scala:76)
+static double objective_from_ctrl(const cvxg_ctx* ctx, const DevCtrl& h) {
+  if (ctx->kl) return h.sc[SC_A0X] + h.sc[SC_KLSUM];
+  return ctx->r0 + h.sc[SC_A0X] + (ctx->hasP ? h.sc[SC_XPX] / 2 : 0.0);
+}
+
 // Barrier value / gradient pieces at the current x and ctrl->t (BarrierSolver.scala:280-301):
 // c, d, w, invd, logd, Px, y, eqDiff, and sc[A0X, XPX, SUMLOG, GG, EQ2].
 static int eval_at_x(cvxg_ctx* ctx) {
@@ -355,12 +367,21 @@ static int eval_at_x(cvxg_ctx* ctx) {
   launch_ctrl_reset_eval(s, ctx->ctrl);
   launch_constraint_eval(s, ctx->A, np, mp, np, ctx->x, ctx->r, ctx->ub, ctx->c, ctx->d, ctx->invd, ctx->w,
                          ctx->logd, ctx->ctrl);
-  if (ctx->hasP) launch_rowdot(s, ctx->P, np, np, np, ctx->x, ctx->Px);
+  const bool quad = ctx->hasP && !ctx->kl;
+  if (quad) launch_rowdot(s, ctx->P, np, np, np, ctx->x, ctx->Px);
+  if (ctx->kl) {  // v = B'z, y = R exp(-v), -B y (the KL dual gradient is w - B y), sum_j y_j
+    launch_rowdot(s, ctx->KB, np, ctx->noutp, np, ctx->x, ctx->kl_v);
+    launch_kl_eval(s, ctx->kl_v, ctx->nout, ctx->noutp, ctx->kl_R, ctx->kl_y);
+    launch_coldot_partials(s, ctx->KB, np, ctx->noutp, np, ctx->kl_y, ctx->kl_part);
+    launch_sum_chunks(s, ctx->kl_part, coldot_chunks(ctx->noutp), np, ctx->kl_negBy);
+    launch_axpy(s, ctx->kl_negBy, ctx->kl_negBy, -2.0, np, ctx->kl_negBy);  // -B y
+    launch_sum(s, ctx->kl_y, ctx->noutp, ctx->ctrl, SC_KLSUM);
+  }
   launch_coldot_partials(s, ctx->A, np, mp, np, ctx->invd, ctx->part);
-  launch_gradient_finalize(s, ctx->a0, ctx->hasP ? ctx->Px : nullptr, ctx->part, coldot_chunks(mp), np, ctx->ctrl,
-                           ctx->y);
+  launch_gradient_finalize(s, ctx->a0, quad ? ctx->Px : (ctx->kl ? ctx->kl_negBy : nullptr), ctx->part,
+                           coldot_chunks(mp), np, ctx->ctrl, ctx->y);
   launch_dot(s, ctx->a0, ctx->x, np, ctx->ctrl, SC_A0X);
-  if (ctx->hasP) launch_dot(s, ctx->x, ctx->Px, np, ctx->ctrl, SC_XPX);
+  if (quad) launch_dot(s, ctx->x, ctx->Px, np, ctx->ctrl, SC_XPX);
   launch_sum(s, ctx->logd, mp, ctx->ctrl, SC_SUMLOG);
   launch_dot(s, ctx->y, nullptr, np, ctx->ctrl, SC_GG);
   if (ctx->p > 0) {
@@ -371,7 +392,7 @@ static int eval_at_x(cvxg_ctx* ctx) {
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
   const DevCtrl& h = *ctx->hctrl;
-  const double f0 = ctx->r0 + h.sc[SC_A0X] + (ctx->hasP ? h.sc[SC_XPX] / 2 : 0.0);
+  const double f0 = objective_from_ctrl(ctx, h);
   ctx->f_at_x = ctx->t * f0 - h.sc[SC_SUMLOG];
   ctx->normGrad = sqrt(h.sc[SC_GG]);
   ctx->eqGap = ctx->p > 0 ? sqrt(h.sc[SC_EQ2]) : 0.0;
@@ -382,16 +403,16 @@ static int eval_at_x(cvxg_ctx* ctx) {
   return CVXG_OK;
 }
 
-static double objective_at_x(cvxg_ctx* ctx) {
-  const DevCtrl& h = *ctx->hctrl;
-  return ctx->r0 + h.sc[SC_A0X] + (ctx->hasP ? h.sc[SC_XPX] / 2 : 0.0);
-}
+static double objective_at_x(cvxg_ctx* ctx) { return objective_from_ctrl(ctx, *ctx->hctrl); }
 
 static int assemble_hessian(cvxg_ctx* ctx) {
   tstart(ctx, 5);
   // full tiles in whole waves of workgroup slots, then the leftover tiles split along K across all slots
   // (partials + ordered reduce) so the last wave is not a handful of tiles on an otherwise idle chip.
   const double* P = ctx->hasP ? ctx->P : nullptr;
+  if (ctx->kl)  // objF.hessianAt(z) = B diag(y) B' (Dist_KL.scala:158-165) into P: a weighted SYRK over the outcomes
+    launch_syrk_assemble(ctx->s, ctx->KB, ctx->np, ctx->kl_y, ctx->noutp, nullptr, ctx->ctrl, ctx->P, ctx->np,
+                         TileList{ctx->tiles, ctx->ntiles}, 1, ctx->part);
   if (ctx->ntiles_main > 0)
     launch_syrk_assemble(ctx->s, ctx->A, ctx->np, ctx->w, ctx->mp, P, ctx->ctrl, ctx->H, ctx->np,
                          TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->part);
@@ -740,14 +761,24 @@ static int newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_in
 struct TrialBatch {
   int k0 = -1;
   double logs[LS_TRIALS];
+  double kl[LS_TRIALS];  // KL dual: sum_j R exp(-(B'(x + t_k s))_j)
   int viol[LS_TRIALS], npos[LS_TRIALS];
 };
 
 static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch* b) {
   if (ctx->m == 0) {  // no inequality constraints: every trial is in C and contributes no log terms
+    if (ctx->kl) {
+      launch_ls_kl(ctx->s, ctx->kl_v, ctx->kl_u, ctx->nout, ctx->kl_R, tbase, beta, ctx->kl_part, ctx->kl_ls);
+      HIPC(ctx, hipMemcpyAsync(b->kl, ctx->kl_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
+      HIPC(ctx, hipStreamSynchronize(ctx->s));
+    }
     b->k0 = k0;
     for (int k = 0; k < LS_TRIALS; ++k) b->logs[k] = 0.0, b->viol[k] = 0, b->npos[k] = 0;
     return CVXG_OK;
+  }
+  if (ctx->kl) {
+    launch_ls_kl(ctx->s, ctx->kl_v, ctx->kl_u, ctx->nout, ctx->kl_R, tbase, beta, ctx->kl_part, ctx->kl_ls);
+    HIPC(ctx, hipMemcpyAsync(b->kl, ctx->kl_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
   }
   const int nb = ls_blocks(ctx->m);
   launch_ls_trials(ctx->s, ctx->c, ctx->e, ctx->ub, ctx->m, tbase, beta, ctx->ls_plog, ctx->ls_pcnt);
@@ -774,9 +805,11 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
   hipStream_t s = ctx->s;
   const double beta = pars->beta, alpha = pars->alpha;
   // e = A s, and the quadratic pieces of f0(x + s t)
-  launch_rowdot(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e);
+  if (ctx->m > 0) launch_rowdot(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e);
   launch_dot(s, ctx->a0, ctx->sdir, ctx->np, ctx->ctrl, SC_A0S);
-  if (ctx->hasP) {
+  if (ctx->kl) launch_rowdot(s, ctx->KB, ctx->np, ctx->noutp, ctx->np, ctx->sdir, ctx->kl_u);  // u = B's
+  const bool quad = ctx->hasP && !ctx->kl;
+  if (quad) {
     launch_rowdot(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps);
     launch_dot(s, ctx->sdir, ctx->Px, ctx->np, ctx->ctrl, SC_SPX);
     launch_dot(s, ctx->sdir, ctx->Ps, ctx->np, ctx->ctrl, SC_SPS);
@@ -785,9 +818,10 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
   CHK(sync_ctrl(ctx));
   const DevCtrl h = *ctx->hctrl;
   const double tb = ctx->t, f = ctx->f_at_x;
-  auto f0_at = [&](double tt) {  // r + a.(x+st) + (x+st)'P(x+st)/2
+  auto f0_at = [&](double tt, double klsum) {  // r + a.(x+st) + (x+st)'P(x+st)/2, or w.(z+st) + R.exp(-B'(z+st))
+    if (ctx->kl) return (h.sc[SC_A0X] + tt * h.sc[SC_A0S]) + klsum;
     double v = ctx->r0 + (h.sc[SC_A0X] + tt * h.sc[SC_A0S]);
-    if (ctx->hasP) v += (h.sc[SC_XPX] + 2 * tt * h.sc[SC_SPX] + tt * tt * h.sc[SC_SPS]) / 2;
+    if (quad) v += (h.sc[SC_XPX] + 2 * tt * h.sc[SC_SPX] + tt * tt * h.sc[SC_SPS]) / 2;
     return v;
   };
   TrialBatch b;
@@ -819,7 +853,7 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
     const int j = it - b.k0;
     if (b.npos[j] > 0)
       return set_err(ctx, CVXG_E_INFEASIBLE_X, "barrierFunction: x not strictly feasible in line search");
-    const double fv = tb * f0_at(tcur) - b.logs[j];
+    const double fv = tb * f0_at(tcur, b.kl[j]) - b.logs[j];
     if (!(fv > f + alpha * tcur * q)) break;
     tcur *= beta;
     ++it;
@@ -974,7 +1008,8 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
                   ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
-                  ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info};
+                  ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,
+                  ctx->kl_negBy, ctx->kl_part, ctx->kl_ls};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
@@ -1001,6 +1036,39 @@ int cvxg_set_objective(cvxg_ctx* ctx, const double* P, int ldP, const double* a,
   }
   CHK(upload_vec(ctx, ctx->a0, a, n, np));
   ctx->r0 = r;
+  ctx->kl = 0;
+  ctx->have_obj = 1;
+  ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+int cvxg_set_objective_kl(cvxg_ctx* ctx, const double* B, int ldB, int row_major, int nout, const double* w,
+                          double R) {
+  if (!ctx || !B || !w || nout <= 0) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  const int n = ctx->n, np = ctx->np;
+  if (ldB < (row_major ? nout : n)) return set_err(ctx, CVXG_E_DIM, "ldB too small");
+  const int noutp = round_up(nout, MPAD);
+  if (noutp != ctx->noutp) {
+    for (double** v : {&ctx->KB, &ctx->kl_v, &ctx->kl_y, &ctx->kl_u, &ctx->kl_negBy, &ctx->kl_part, &ctx->kl_ls})
+      if (*v) (void)hipFree(*v), *v = nullptr;
+    CHK(dalloc(ctx, &ctx->KB, (size_t)noutp * np));
+    for (double** v : {&ctx->kl_v, &ctx->kl_y, &ctx->kl_u}) CHK(dalloc(ctx, v, noutp));
+    CHK(dalloc(ctx, &ctx->kl_negBy, np));
+    CHK(dalloc(ctx, &ctx->kl_part, std::max((size_t)coldot_chunks(noutp) * np,
+                                            (size_t)((noutp + 255) / 256) * LS_TRIALS)));
+    CHK(dalloc(ctx, &ctx->kl_ls, LS_TRIALS));
+  }
+  // KB = B' (nout x n): B row-major (ldB) is B' column-major with the same ld, and vice versa
+  CHK(upload_mat(ctx, ctx->KB, np, noutp, B, nout, n, ldB, row_major ? 0 : 1));
+  if (!ctx->P) CHK(dalloc(ctx, &ctx->P, (size_t)np * np));
+  ctx->hasP = 1;  // the KL Hessian B diag(y) B' is assembled into P every step
+  CHK(upload_vec(ctx, ctx->a0, w, n, np));
+  ctx->r0 = 0.0;
+  ctx->kl = 1;
+  ctx->nout = nout;
+  ctx->noutp = noutp;
+  ctx->kl_R = R;
   ctx->have_obj = 1;
   ctx->x_eval_valid = 0;
   return CVXG_OK;

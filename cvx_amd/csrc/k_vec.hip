@@ -497,6 +497,44 @@ void launch_ls_trials(hipStream_t s, const double* c, const double* e, const dou
   k_ls_trials<<<ls_blocks(m), 256, 0, s>>>(c, e, ub, m, tbase, beta, part_log, part_cnt);
 }
 
+// KL dual objective along the trial steps: per trial k, sum_j R exp(-(v_j + t_k u_j)) (v = B'z, u = B's),
+// the vec_R dot exp(-B'(z + s t)) term of Dist_KL.dualObjFAt (Dist_KL.scala:146-147); t_k by repeated products.
+__global__ __launch_bounds__(256) void k_ls_kl(const double* __restrict__ v, const double* __restrict__ u, int nout,
+                                               double R, double tbase, double beta, double* __restrict__ part) {
+  __shared__ double sred[4][LS_TRIALS];
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool valid = j < nout;
+  const double vj = valid ? v[j] : 0.0, uj = valid ? u[j] : 0.0;
+  double t = tbase;
+  for (int k = 0; k < LS_TRIALS; ++k) {
+    const double y = valid ? R * exp(-(vj + t * uj)) : 0.0;
+    const double sw = wave_sum(y);
+    if (lane == 0) sred[wid][k] = sw;
+    t *= beta;
+  }
+  __syncthreads();
+  if (threadIdx.x < LS_TRIALS) {
+    const int k = threadIdx.x;
+    part[(size_t)blockIdx.x * LS_TRIALS + k] = ((sred[0][k] + sred[1][k]) + sred[2][k]) + sred[3][k];
+  }
+}
+void launch_ls_kl(hipStream_t s, const double* v, const double* u, int nout, double R, double tbase, double beta,
+                  double* part, double* out) {
+  const int nb = (nout + 255) / 256;
+  k_ls_kl<<<nb, 256, 0, s>>>(v, u, nout, R, tbase, beta, part);
+  k_sum_chunks<<<1, LS_TRIALS, 0, s>>>(part, nb, LS_TRIALS, out);
+}
+
+// KL dual at z (v = B'z given): y_j = R exp(-v_j) for j < nout (Dist_KL.scala:163, 170), 0 on the padding
+__global__ void k_kl_eval(const double* __restrict__ v, int nout, int noutp, double R, double* __restrict__ y) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < noutp) y[j] = (j < nout) ? R * exp(-v[j]) : 0.0;
+}
+void launch_kl_eval(hipStream_t s, const double* v, int nout, int noutp, double R, double* y) {
+  k_kl_eval<<<(noutp + 255) / 256, 256, 0, s>>>(v, nout, noutp, R, y);
+}
+
 __global__ void k_ls_finalize(const double* __restrict__ part_log, const int* __restrict__ part_cnt, int nblocks,
                               double* __restrict__ out_log, int* __restrict__ out_cnt) {
   const int k = threadIdx.x;

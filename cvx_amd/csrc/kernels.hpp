@@ -86,6 +86,10 @@ void launch_ls_trials(hipStream_t s, const double* c, const double* e, const dou
 void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_cnt, int nblocks,
                         double* out_log, int* out_cnt);
 int ls_blocks(int m);
+// KL dual objective (Dist_KL.scala:146-170): y = R exp(-v) (masked padding); trial sums of R exp(-(v + t_k u))
+void launch_kl_eval(hipStream_t s, const double* v, int nout, int noutp, double R, double* y);
+void launch_ls_kl(hipStream_t s, const double* v, const double* u, int nout, double R, double tbase, double beta,
+                  double* part, double* out);
 
 // ---- KKT Schur complement (p > 0) ------------------------------------------------------------------
 void launch_kkt_schur(hipStream_t s, const double* X, int nrhs, const double* B, int ldb, int p, int n,

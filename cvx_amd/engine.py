@@ -93,6 +93,14 @@ class Engine:
             self._check(self.lib.cvxg_set_objective(self.h, None, 0, _dp(a0), float(r0)))
         self._keep_obj = (a0, P)
 
+    def set_objective_kl(self, B, w, R: float):
+        """KL dual objective of Duality.dualProblem over Dist_KL: B = mat_B (n x nout, row-major), w = vec_w,
+        R = 1/(nout e) (cvxg_set_objective_kl)."""
+        B, w = _f64(B), _f64(w)
+        assert B.shape[0] == self.n and w.shape[0] == self.n
+        self._check(self.lib.cvxg_set_objective_kl(self.h, _dp(B), B.shape[1], 1, B.shape[1], _dp(w), float(R)))
+        self._keep_obj = (B, w)
+
     def set_ineq(self, A, r, ub):
         A, r, ub = _f64(A), _f64(r), _f64(ub)
         self._check(self.lib.cvxg_set_ineq(self.h, _dp(A), A.shape[1] if A.ndim == 2 else self.n, 1, _dp(r), _dp(ub)))
@@ -102,7 +110,10 @@ class Engine:
         self._check(self.lib.cvxg_set_eq(self.h, _dp(Aeq), Aeq.shape[1], 1, _dp(beq)))
 
     def load_problem(self, spec: dict):
-        self.set_objective(spec["a0"], spec.get("r0", 0.0), spec.get("P"))
+        if spec.get("kl_B") is not None:
+            self.set_objective_kl(spec["kl_B"], spec["a0"], float(np.asarray(spec["kl_R"]).ravel()[0]))
+        else:
+            self.set_objective(spec["a0"], spec.get("r0", 0.0), spec.get("P"))
         self.set_ineq(spec["A"], spec["r"], spec["ub"])
         if self.p > 0:
             self.set_eq(spec["Aeq"], spec["beq"])

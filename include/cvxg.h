@@ -107,6 +107,14 @@ const char* cvxg_version(void);
  * LinearObjectiveFunction(dim, r, a) (LinearObjectiveFunction.scala:7-21).  P must be symmetric. */
 int cvxg_set_objective(cvxg_ctx* ctx, const double* P, int ldP, const double* a, double r);
 
+/* The objective of Duality.dualProblem for Dist_KL (Duality.scala:74-79 over Dist_KL.scala:146-165): with z the
+ * n dual variables (lambda, nu), B the n x nout matrix mat_B = (H; 1'; A) (Dist_KL.scala:134-140), w = vec_w
+ * (:123-128) and R = 1/(nout e), e = 2.7182811828459045 (:114-116):
+ *   valueAt(z) = w.z + R.exp(-B'z),  gradientAt(z) = w - B(R o exp(-B'z)),  hessianAt(z) = B diag(y) B'.
+ * B is read row-major (row_major != 0, ldB >= nout) or column-major (ldB >= n). */
+int cvxg_set_objective_kl(cvxg_ctx* ctx, const double* B, int ldB, int row_major, int nout, const double* w,
+                          double R);
+
 /* The LinearConstraint list r_i + a_i.x <= ub_i (LinearConstraint.scala:7-32), A row i = a_i in LIST
  * order (fold and forall order matter: BarrierSolver.scala:280-315, ConstraintSet.scala:34-38). */
 int cvxg_set_ineq(cvxg_ctx* ctx, const double* A, int ldA, int row_major, const double* r,

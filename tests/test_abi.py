@@ -24,7 +24,7 @@ def lib():
 
 def test_header_declares_entry_points():
     syms = _header_symbols()
-    for s in ["cvxg_create", "cvxg_destroy", "cvxg_set_objective", "cvxg_set_ineq", "cvxg_set_eq",
+    for s in ["cvxg_create", "cvxg_destroy", "cvxg_set_objective", "cvxg_set_objective_kl", "cvxg_set_ineq", "cvxg_set_eq",
               "cvxg_newton_step", "cvxg_centering", "cvxg_barrier_solve", "cvxg_barrier_eval",
               "cvxg_newton_direction", "cvxg_last_error"]:
         assert s in syms

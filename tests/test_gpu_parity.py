@@ -357,3 +357,63 @@ def test_kktsymsolve_fallback_vs_oracle(mods):
     assert np.linalg.norm(dx - dref) / np.linalg.norm(dref) < 1e-8
     assert np.linalg.norm(w - wref) / np.linalg.norm(wref) < 1e-7
     eng.close()
+
+
+# ---- Dist_KL via the dual barrier problem (C4): KL dual objective on the device -----------------------------
+
+def _kl_spec(O, n, H=None, u=None, A=None, r=None):
+    pb, m = O.kl_dual_problem(n, H, u, A, r)
+    spec = {"a0": pb.a0, "r0": 0.0, "A": pb.A if m > 0 else np.zeros((0, pb.n)), "r": pb.r, "ub": pb.ub,
+            "kl_B": pb.kl_B, "kl_R": pb.kl_R[:1]}
+    return spec, pb
+
+
+@pytest.mark.parametrize("n,k", [(2048, 2), (2048, 64), (300, 130)])
+def test_kl_dual_barrier_oracles_match(mods, n, k):
+    """Dist_KL.dualObjFAt / gradientDualObjFAt / hessianDualObjFAt (negated by Duality.objF) inside the barrier
+    value, gradient and Hessian (BarrierSolver.scala:280-315), against the oracle at random feasible z."""
+    Z, SP, Engine, O = mods
+    rng = np.random.default_rng(n + k)
+    H = rng.uniform(0, 1, size=(k, n))
+    u = H.mean(axis=1) * rng.uniform(0.9, 1.1, k)
+    spec, pb = _kl_spec(O, n, H, u)
+    eng = Engine(pb.n, pb.m, 0)
+    eng.load_problem(spec)
+    for t in (1.0, 1e3):
+        z = np.concatenate([rng.uniform(0.01, 0.5, pb.m), rng.uniform(-0.5, 0.5, pb.n - pb.m)])
+        f, g, Hs = eng.barrier_eval(t, z, want_grad=True, want_hess=True)
+        fr, gr, Hr = O.barrier_value(pb, t, z), O.barrier_gradient(pb, t, z), O.barrier_hessian(pb, t, z, literal=False)
+        assert abs(f - fr) <= 1e-12 * max(1.0, abs(fr))
+        assert np.linalg.norm(g - gr) <= 1e-12 * np.linalg.norm(gr)
+        assert np.linalg.norm(Hs - Hr) <= 1e-12 * np.linalg.norm(Hr)
+        assert np.array_equal(Hs, Hs.T)
+    eng.close()
+
+
+def test_kl1A_dual_solve_on_gpu(mods):
+    """C4: kl_1A at n = 2048 (OptimizationProblems.scala:217-244) solved through Duality.solveDual with the
+    engine: primal optimum vs kl1_analyticSolution (reference tolerance 1e-2), dual z and Newton step count vs
+    the oracle's dual barrier path."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import Dist_KL
+    n = 2048
+    H, u = O.kl1A_data(n)
+    prob = Dist_KL.apply("dist_KL_1A", n, H, u, None, None, "BR")
+    sol = prob.solveDual("BR", SP.standardParams())
+    Qref, solref, pb = O.kl_solve_dual(n, H, u, None, None, O.standard_params())
+    assert np.max(np.abs(sol.x - O.kl1_analytic_solution(n))) < 1e-6
+    assert np.max(np.abs(sol.x - Qref)) < 1e-10
+    assert np.linalg.norm(sol.lambda_ - solref.x[:2]) <= 1e-6 * np.linalg.norm(solref.x[:2])
+    assert sol.newtonSteps == solref.newton_steps
+    assert sol.dualityGap < 1e-8
+
+
+def test_kl2A_dual_solve_on_gpu(mods):
+    """kl_2A: equality-only KL problem (the dual has no inequality constraints, one centering)."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import Dist_KL
+    n = 2048
+    A, r = O.kl2A_data(n)
+    sol = Dist_KL.apply("dist_KL_2A", n, None, None, A, r, "BR").solveDual("BR", SP.standardParams())
+    assert np.max(np.abs(sol.x - O.kl1_analytic_solution(n))) < 1e-6
+    assert sol.nu is not None and sol.nu.shape == (3,)
