@@ -63,6 +63,20 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_setObjective(JNIEnv* env, jclass 
   return rc;
 }
 
+/* Dist_KL dual objective (Duality.objF over Dist_KL): B = mat_B data (Breeze column-major, rowMajor = 0, ld =
+ * majorStride), w = vec_w, R = vec_R(0). */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_setObjectiveKL(JNIEnv* env, jclass cls, jlong h, jdoubleArray B,
+                                                              jint ldB, jint rowMajor, jint nout, jdoubleArray w,
+                                                              jdouble R) {
+  (void)cls;
+  double* pB = (*env)->GetPrimitiveArrayCritical(env, B, 0);
+  double* pw = (*env)->GetPrimitiveArrayCritical(env, w, 0);
+  jint rc = cvxg_set_objective_kl(CTX(h), pB, ldB, rowMajor, nout, pw, R);
+  (*env)->ReleasePrimitiveArrayCritical(env, w, pw, JNI_ABORT);
+  (*env)->ReleasePrimitiveArrayCritical(env, B, pB, JNI_ABORT);
+  return rc;
+}
+
 JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_setIneq(JNIEnv* env, jclass cls, jlong h, jdoubleArray A, jint ldA,
                                                        jint rowMajor, jdoubleArray r, jdoubleArray ub) {
   (void)cls;
