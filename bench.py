@@ -74,20 +74,22 @@ def cpu_baseline(spec, seconds_budget: float = 20.0):
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
 
 
-def pmc_traffic(kernel_prefix: str):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
-    (scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections); None if absent."""
+def pmc_traffic(kernel_prefixes):
+    """HBM bytes of one SYRK assembly phase from the committed rocprofv3 PMC passes (scripts/pmc_traffic.py:
+    FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections), summed over the launches the phase consists of (the main
+    wave, the split-K tail and the ordered reduce: the same region the HIP events time); None if absent."""
     try:
         doc = json.load(open(PMC_TRAFFIC))
     except (OSError, ValueError):
         return None, None
-    best = None
-    for k, v in doc.get("kernels", {}).items():
-        if k.startswith(kernel_prefix) and (best is None or v["hbm_bytes_per_launch"] > best[1]):
-            best = (k, v["hbm_bytes_per_launch"])
-    if best is None:
+    total, used = 0.0, []
+    for k, v in sorted(doc.get("kernels", {}).items()):
+        if any(k.startswith(p) for p in kernel_prefixes):
+            total += v["hbm_bytes_per_launch"]
+            used.append(k)
+    if not used:
         return None, None
-    return best[1], os.path.relpath(PMC_TRAFFIC, ROOT) + ":" + best[0]
+    return total, os.path.relpath(PMC_TRAFFIC, ROOT) + ":" + "+".join(used)
 
 
 def main():
@@ -167,7 +169,7 @@ def main():
         ach = flops_syrk / (syrk * 1e-3) / 1e12
         chol = float(np.mean(chol_ms))
         kkt_ms = float(np.mean(ruiz_ms)) + chol + float(np.mean(solve_ms))
-        traffic, traffic_src = pmc_traffic("cvxg::k_syrk_assemble")
+        traffic, traffic_src = pmc_traffic(("cvxg::k_syrk_assemble", "cvxg::k_syrk_reduce"))
         out = {
             "metric": METRIC,
             "value": value,
@@ -188,7 +190,7 @@ def main():
                                       "RCCL gather of results after the timed region"},
             "roofline": {"bound": "mfma", "kernel": "k_syrk_assemble (H = tP + A'diag(w)A)",
                          "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                         "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic, "traffic_unit": "bytes/assembly (main wave + split-K tail + reduce)",
                          "traffic_source": traffic_src,
                          "flops_per_launch": flops_syrk, "avg_launch_ms": syrk},
             "phases_ms": {"syrk": syrk, "ruiz": float(np.mean(ruiz_ms)), "cholesky_fused_fwd": chol,
