@@ -97,8 +97,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=4096)
-    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C3B", "C4"],
+                    help="C3 (default, the metric's config): random dense QP n=4096 m=8192; C2: n=1024 m=2048; "
+                         "C3B: C3 plus 9216 sparse bound / difference rows; C4: KL dual, 2048 outcomes, k=512")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--m", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
@@ -115,8 +118,24 @@ def main():
         D.init("nccl")
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    n, m = args.n, args.m
-    spec = Z.random_qp(n, m, instance=rank)
+    wl = args.workload
+    if wl == "C4":
+        nout, k = args.m or 2048, (args.n or 513) - 1
+        spec = Z.kl_dual_spec(nout, k, instance=rank)
+        n, m = k + 1, k
+        syrk_rows = nout  # the B diag(y) B' Hessian: a weighted SYRK over the outcomes; the bound rows are sparse
+        workload = (f"C4: KL dual barrier (Dist_KL via Duality), {nout} outcomes, dual dimension {n}, {k} bound rows"
+                    f", full barrier Newton iterations")
+    else:
+        n = args.n or (1024 if wl == "C2" else 4096)
+        m0 = args.m or (2048 if wl == "C2" else 8192)
+        spec = Z.random_qp_bounds(n, m0, instance=rank) if wl == "C3B" else Z.random_qp(n, m0, instance=rank)
+        m = spec["A"].shape[0]
+        syrk_rows = m0  # dense rows (the sparse rows' Hessian entries are per-entry sums, not SYRK work)
+        workload = (f"{wl}: random dense QP n={n} m={m0}" + (f" plus {m - m0} sparse bound/difference rows"
+                                                               if wl == "C3B" else "") +
+                    ", full barrier Newton iterations (assembly + Ruiz + Cholesky + solves + line search) on one "
+                    "MI355X per rank")
     pars = SolverParams.standardParams()
 
     eng = Engine(n, m, 0, device=local_rank)
@@ -165,11 +184,12 @@ def main():
         total_steps = args.steps * world
         value = total_steps / elapsed
         syrk = float(np.mean(syrk_ms))
-        flops_syrk = float(m) * n * (n + 1)  # lower triangle incl. diagonal
+        flops_syrk = float(syrk_rows) * n * (n + 1)  # lower triangle incl. diagonal
         ach = flops_syrk / (syrk * 1e-3) / 1e12
         chol = float(np.mean(chol_ms))
         kkt_ms = float(np.mean(ruiz_ms)) + chol + float(np.mean(solve_ms))
-        traffic, traffic_src = pmc_traffic(("cvxg::k_syrk_assemble", "cvxg::k_syrk_reduce"))
+        traffic, traffic_src = (pmc_traffic(("cvxg::k_syrk_assemble", "cvxg::k_syrk_reduce")) if wl == "C3"
+                                else (None, None))
         out = {
             "metric": METRIC,
             "value": value,
@@ -182,10 +202,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded random dense QP, SURVEY.md §8d generator)",
-            "config": {"workload": f"C3: random dense QP n={n} m={m}, full barrier Newton iterations "
-                                   "(assembly + Ruiz + Cholesky + solves + line search) on one MI355X per rank",
-                       "n": n, "m": m,
+            "data": "synthetic (seeded generators of cvx_amd/problems.py, SURVEY.md §8d)",
+            "config": {"workload": workload, "n": n, "m": m,
                        "parallelism": f"replicas x{world}: one independent QP per GPU (config C5), "
                                       "RCCL gather of results after the timed region"},
             "roofline": {"bound": "mfma", "kernel": "k_syrk_assemble (H = tP + A'diag(w)A)",
@@ -199,7 +217,7 @@ def main():
             "cholesky_tflops": (n ** 3 / 3) / (chol * 1e-3) / 1e12,
             "gathered_ranks": len(gathered),
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and wl == "C3":
             out["cpu_baseline"] = cpu_baseline(spec, args.cpu_budget)
         elif not args.no_cpu_baseline:
             out["cpu_baseline"] = None

@@ -17,6 +17,7 @@
 #include <queue>
 #include <string>
 #include <vector>
+#include <vector>
 
 #include "../../include/cvxg.h"
 #include "kernels.hpp"
@@ -70,6 +71,19 @@ struct cvxg_ctx {
   int ntiles = 0, nsplit = 1;
   int ntiles_main = 0;  // tiles assembled without K split (whole waves of slots); the rest use nsplit
   int chol_outer = 4;  // 64-blocks per outer Cholesky panel (trailing update width 256)
+  int slots = 512;     // SYRK workgroup slots (2 per CU)
+  // Sparse constraint rows (<= SPARSE_NNZ nonzeros: bounds, phase-I bound rows, box rows).  Their Hessian
+  // terms are per-entry sums (k_sparse_hess); only the dense rows, packed into As, go through the SYRK.
+  int sparse_rows = 1;          // CVXG_SPARSE_ROWS=0 disables the split (A/B)
+  int have_sparse = 0;          // set_ineq found sparse rows: the SYRK runs over As / wd / mdp
+  int ndense = 0, mdp = 0;      // dense rows, padded to MPAD (>= MPAD)
+  double *As = nullptr, *wd = nullptr;
+  int* didx = nullptr;          // As row -> constraint index
+  int sp_T = 0;                 // lower entries touched by sparse rows
+  int *sp_ptr = nullptr, *sp_pq = nullptr, *sp_row = nullptr;
+  double* sp_coef = nullptr;
+  int kl_nsplit = 1;            // K split of the KL SYRK's tail tiles over the outcomes
+  double* kl_spart = nullptr;   // its partials
   // symSolve / kktSymSolve fallback buffers (allocated on first use; ldm = round_up(n + p, 128))
   int eig_ldm = 0;
   double *eig_M = nullptr, *eig_K = nullptr, *eig_d = nullptr, *eig_e = nullptr, *eig_dots = nullptr;
@@ -410,16 +424,33 @@ static int assemble_hessian(cvxg_ctx* ctx) {
   // full tiles in whole waves of workgroup slots, then the leftover tiles split along K across all slots
   // (partials + ordered reduce) so the last wave is not a handful of tiles on an otherwise idle chip.
   const double* P = ctx->hasP ? ctx->P : nullptr;
-  if (ctx->kl)  // objF.hessianAt(z) = B diag(y) B' (Dist_KL.scala:158-165) into P: a weighted SYRK over the outcomes
-    launch_syrk_assemble(ctx->s, ctx->KB, ctx->np, ctx->kl_y, ctx->noutp, nullptr, ctx->ctrl, ctx->P, ctx->np,
-                         TileList{ctx->tiles, ctx->ntiles}, 1, ctx->part);
+  if (ctx->kl) {  // objF.hessianAt(z) = B diag(y) B' (Dist_KL.scala:158-165) into P: a weighted SYRK over the outcomes
+    if (ctx->ntiles_main > 0)
+      launch_syrk_assemble(ctx->s, ctx->KB, ctx->np, ctx->kl_y, ctx->noutp, nullptr, ctx->ctrl, ctx->P, ctx->np,
+                           TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->part);
+    if (ctx->ntiles > ctx->ntiles_main)  // the tail (all tiles for a small dual) split along the outcomes
+      launch_syrk_assemble(ctx->s, ctx->KB, ctx->np, ctx->kl_y, ctx->noutp, nullptr, ctx->ctrl, ctx->P, ctx->np,
+                           TileList{ctx->tiles + ctx->ntiles_main, ctx->ntiles - ctx->ntiles_main}, ctx->kl_nsplit,
+                           ctx->kl_spart);
+  }
+  const double* A = ctx->A;
+  const double* w = ctx->w;
+  int rows = ctx->mp;
+  if (ctx->have_sparse) {  // dense rows only; the sparse rows' entries are added below
+    launch_gather_w(ctx->s, ctx->w, ctx->didx, ctx->ndense, ctx->mdp, ctx->wd);
+    A = ctx->As;
+    w = ctx->wd;
+    rows = ctx->mdp;
+  }
   if (ctx->ntiles_main > 0)
-    launch_syrk_assemble(ctx->s, ctx->A, ctx->np, ctx->w, ctx->mp, P, ctx->ctrl, ctx->H, ctx->np,
+    launch_syrk_assemble(ctx->s, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
                          TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->part);
   if (ctx->ntiles > ctx->ntiles_main)
-    launch_syrk_assemble(ctx->s, ctx->A, ctx->np, ctx->w, ctx->mp, P, ctx->ctrl, ctx->H, ctx->np,
+    launch_syrk_assemble(ctx->s, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
                          TileList{ctx->tiles + ctx->ntiles_main, ctx->ntiles - ctx->ntiles_main}, ctx->nsplit,
                          ctx->part);
+  if (ctx->have_sparse)
+    launch_sparse_hess(ctx->s, ctx->sp_ptr, ctx->sp_pq, ctx->sp_row, ctx->sp_coef, ctx->w, ctx->sp_T, ctx->H, ctx->np);
   tstop(ctx, 5);
   HIPC(ctx, hipGetLastError());
   return CVXG_OK;
@@ -893,6 +924,12 @@ const char* cvxg_version(void) { return "cvxg 0.1 (gfx950, FP64 MFMA SYRK, block
 
 const char* cvxg_last_error(const cvxg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+// K split of the SYRK tail tiles: the leftover tiles share one wave of slots.
+static int syrk_nsplit(const cvxg_ctx* ctx, int kchunks) {
+  const int rest = ctx->ntiles - ctx->ntiles_main;
+  return rest > 0 ? std::max(1, std::min(kchunks, ctx->slots / rest)) : 1;
+}
+
 int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   if (!out) return CVXG_E_ARG;
   *out = nullptr;
@@ -969,12 +1006,13 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   int ncu = 256;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
   const int slots = 2 * std::max(ncu, 1);
+  ctx->slots = slots;
+  if (const char* e = getenv("CVXG_SPARSE_ROWS")) ctx->sparse_rows = atoi(e) != 0;
   const int kchunks = (int)(mp / KC);
   std::vector<int> tl = syrk_tile_plan(nt, slots, &ctx->ntiles_main);
   ctx->ntiles = (int)tl.size();
   if (const char* e = getenv("CVXG_SYRK_NOTAIL")) ctx->ntiles_main = atoi(e) ? ctx->ntiles : ctx->ntiles_main;
-  const int rest = ctx->ntiles - ctx->ntiles_main;
-  ctx->nsplit = rest > 0 ? std::max(1, std::min(kchunks, slots / rest)) : 1;
+  ctx->nsplit = syrk_nsplit(ctx, kchunks);
   CHK(dalloc(ctx, &ctx->tiles, tl.size()));
   CHK(copy_sync(ctx, ctx->tiles, tl.data(), tl.size() * sizeof(int), hipMemcpyHostToDevice));
   size_t part = std::max((mp / 64) * np, (size_t)ctx->nblk * np);  // coldot partials, Ruiz tile partials
@@ -1009,7 +1047,8 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,
-                  ctx->kl_negBy, ctx->kl_part, ctx->kl_ls};
+                  ctx->kl_negBy, ctx->kl_part, ctx->kl_ls, ctx->As, ctx->wd, ctx->didx, ctx->sp_ptr,
+                  ctx->sp_pq, ctx->sp_row, ctx->sp_coef, ctx->kl_spart};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
@@ -1063,6 +1102,15 @@ int cvxg_set_objective_kl(cvxg_ctx* ctx, const double* B, int ldB, int row_major
   CHK(upload_mat(ctx, ctx->KB, np, noutp, B, nout, n, ldB, row_major ? 0 : 1));
   if (!ctx->P) CHK(dalloc(ctx, &ctx->P, (size_t)np * np));
   ctx->hasP = 1;  // the KL Hessian B diag(y) B' is assembled into P every step
+  {
+    const int rest = ctx->ntiles - ctx->ntiles_main;
+    const int ns = syrk_nsplit(ctx, noutp / KC);
+    if (rest > 0 && (ns != ctx->kl_nsplit || !ctx->kl_spart)) {
+      if (ctx->kl_spart) (void)hipFree(ctx->kl_spart), ctx->kl_spart = nullptr;
+      CHK(dalloc(ctx, &ctx->kl_spart, (size_t)ns * rest * TILE * TILE));
+    }
+    ctx->kl_nsplit = ns;
+  }
   CHK(upload_vec(ctx, ctx->a0, w, n, np));
   ctx->r0 = 0.0;
   ctx->kl = 1;
@@ -1071,6 +1119,90 @@ int cvxg_set_objective_kl(cvxg_ctx* ctx, const double* B, int ldB, int row_major
   ctx->kl_R = R;
   ctx->have_obj = 1;
   ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+// Split the constraint rows into dense rows (packed into As for the SYRK) and sparse rows (at most SPARSE_NNZ
+// nonzeros), whose lower-triangle Hessian entries are listed per entry (p, q) with the rows in list order.
+static constexpr int SPARSE_NNZ = 4;
+static int plan_sparse_rows(cvxg_ctx* ctx, const double* A, int ldA, int row_major) {
+  const int n = ctx->n, m = ctx->m;
+  for (void** p : {(void**)&ctx->As, (void**)&ctx->wd, (void**)&ctx->didx, (void**)&ctx->sp_ptr, (void**)&ctx->sp_pq,
+                   (void**)&ctx->sp_row, (void**)&ctx->sp_coef}) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+  }
+  ctx->have_sparse = 0;
+  ctx->sp_T = 0;
+  ctx->nsplit = syrk_nsplit(ctx, ctx->mp / KC);
+  if (!ctx->sparse_rows) return CVXG_OK;
+  auto at = [&](int i, int j) { return row_major ? A[(size_t)i * ldA + j] : A[(size_t)j * ldA + i]; };
+  struct Term {
+    int p, q, row;
+    double coef;
+  };
+  std::vector<Term> terms;
+  std::vector<int> dense;
+  std::vector<int> nzc;
+  std::vector<double> nzv;
+  for (int i = 0; i < m; ++i) {
+    nzc.clear();
+    nzv.clear();
+    for (int j = 0; j < n && (int)nzc.size() <= SPARSE_NNZ; ++j) {
+      const double v = at(i, j);
+      if (v != 0.0) {
+        nzc.push_back(j);
+        nzv.push_back(v);
+      }
+    }
+    if ((int)nzc.size() > SPARSE_NNZ) {
+      dense.push_back(i);
+      continue;
+    }
+    for (size_t a = 0; a < nzc.size(); ++a)  // lower entries: p = nzc[a] >= q = nzc[b]
+      for (size_t b = 0; b <= a; ++b) terms.push_back({nzc[a], nzc[b], i, nzv[a] * nzv[b]});
+  }
+  if ((int)dense.size() == m) return CVXG_OK;  // no sparse rows: the SYRK keeps using A itself
+  std::stable_sort(terms.begin(), terms.end(),
+                   [](const Term& x, const Term& y) { return x.p != y.p ? x.p < y.p : x.q < y.q; });
+  std::vector<int> ptr, pq, row;
+  std::vector<double> coef;
+  for (size_t e = 0; e < terms.size(); ++e) {
+    if (e == 0 || terms[e].p != terms[e - 1].p || terms[e].q != terms[e - 1].q) {
+      ptr.push_back((int)e);
+      pq.push_back(terms[e].p);
+      pq.push_back(terms[e].q);
+    }
+    row.push_back(terms[e].row);
+    coef.push_back(terms[e].coef);
+  }
+  ptr.push_back((int)terms.size());
+  ctx->sp_T = (int)pq.size() / 2;
+  ctx->ndense = (int)dense.size();
+  ctx->mdp = std::max(round_up(ctx->ndense, MPAD), MPAD);
+  const size_t np = ctx->np;
+  CHK(dalloc(ctx, &ctx->As, (size_t)ctx->mdp * np));
+  CHK(dalloc(ctx, &ctx->wd, ctx->mdp));
+  CHK(dalloc(ctx, &ctx->didx, std::max(ctx->ndense, 1)));
+  {
+    std::vector<double> h((size_t)ctx->mdp * np, 0.0);
+    for (int r = 0; r < ctx->ndense; ++r)
+      for (int j = 0; j < n; ++j) h[(size_t)r * np + j] = at(dense[r], j);
+    CHK(copy_sync(ctx, ctx->As, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (ctx->ndense) CHK(copy_sync(ctx, ctx->didx, dense.data(), dense.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  if (ctx->sp_T > 0) {
+    CHK(dalloc(ctx, &ctx->sp_ptr, ptr.size()));
+    CHK(dalloc(ctx, &ctx->sp_pq, pq.size()));
+    CHK(dalloc(ctx, &ctx->sp_row, row.size()));
+    CHK(dalloc(ctx, &ctx->sp_coef, coef.size()));
+    CHK(copy_sync(ctx, ctx->sp_ptr, ptr.data(), ptr.size() * sizeof(int), hipMemcpyHostToDevice));
+    CHK(copy_sync(ctx, ctx->sp_pq, pq.data(), pq.size() * sizeof(int), hipMemcpyHostToDevice));
+    CHK(copy_sync(ctx, ctx->sp_row, row.data(), row.size() * sizeof(int), hipMemcpyHostToDevice));
+    CHK(copy_sync(ctx, ctx->sp_coef, coef.data(), coef.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
+  ctx->have_sparse = 1;
+  ctx->nsplit = syrk_nsplit(ctx, ctx->mdp / KC);
   return CVXG_OK;
 }
 
@@ -1086,6 +1218,7 @@ int cvxg_set_ineq(cvxg_ctx* ctx, const double* A, int ldA, int row_major, const 
     memcpy(uu.data(), ub, m * sizeof(double));
     CHK(copy_sync(ctx, ctx->r, rr.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
     CHK(copy_sync(ctx, ctx->ub, uu.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
+    CHK(plan_sparse_rows(ctx, A, ldA, row_major));
   }
   ctx->have_ineq = 1;
   ctx->x_eval_valid = 0;

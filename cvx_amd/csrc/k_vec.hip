@@ -745,4 +745,40 @@ void launch_btw_plus(hipStream_t s, const double* B, int ld, int p, const double
   k_btw_plus<<<(n + 255) / 256, 256, 0, s>>>(B, ld, p, w, u, n, y);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Sparse constraint rows (bounds x_j >= 0, phase-I rows (e_j, -1), box and difference rows): their Hessian
+// terms  a_ip a_iq / d_i^2  (BarrierSolver.scala:314) are summed per lower entry (p, q) over the rows that
+// touch it, in list order, one wave per entry, and added to H after the dense-row SYRK (both triangles).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sparse_hess(const int* __restrict__ ptr, const int* __restrict__ pq,
+                                                     const int* __restrict__ row, const double* __restrict__ coef,
+                                                     const double* __restrict__ w, int T, double* __restrict__ H,
+                                                     int ld) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (t >= T) return;
+  const int e0 = ptr[t], e1 = ptr[t + 1];
+  double s = 0.0;
+  for (int e = e0 + lane; e < e1; e += 64) s += coef[e] * w[row[e]];
+  s = wave_sum(s);
+  if (lane == 0) {
+    const int p = pq[2 * t], q = pq[2 * t + 1];
+    H[(size_t)p * ld + q] += s;
+    if (p != q) H[(size_t)q * ld + p] += s;
+  }
+}
+void launch_sparse_hess(hipStream_t s, const int* ptr, const int* pq, const int* row, const double* coef,
+                        const double* w, int T, double* H, int ld) {
+  if (T > 0) k_sparse_hess<<<(T + 3) / 4, 256, 0, s>>>(ptr, pq, row, coef, w, T, H, ld);
+}
+
+// wd[i] = w[idx[i]] for the dense rows packed for the SYRK (0 on the padding rows)
+__global__ void k_gather_w(const double* __restrict__ w, const int* __restrict__ idx, int nd, int ndp,
+                           double* __restrict__ wd) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < ndp) wd[i] = (i < nd) ? w[idx[i]] : 0.0;
+}
+void launch_gather_w(hipStream_t s, const double* w, const int* idx, int nd, int ndp, double* wd) {
+  k_gather_w<<<(ndp + 255) / 256, 256, 0, s>>>(w, idx, nd, ndp, wd);
+}
+
 }  // namespace cvxg

@@ -49,6 +49,11 @@ void launch_add_diag(hipStream_t s, double* H, int ld, int n, double v);
 void launch_copy_diag(hipStream_t s, const double* H, int ld, int n, double* out);
 void launch_set_diag(hipStream_t s, double* H, int ld, int n, const double* diag);
 
+// sparse constraint rows: H[p][q] (+ mirror) += sum over the rows i of entry t of coef_e * w[i] (fixed order)
+void launch_sparse_hess(hipStream_t s, const int* ptr, const int* pq, const int* row, const double* coef,
+                        const double* w, int T, double* H, int ld);
+void launch_gather_w(hipStream_t s, const double* w, const int* idx, int nd, int ndp, double* wd);
+
 // ---- MFMA SYRK (k_syrk.hip) -----------------------------------------------------------------------
 // H = t*P + A' diag(w) A over the lower tile list; split-K when nsplit > 1 (partials + ordered reduce).
 void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double* w, int mp, const double* P,

@@ -32,6 +32,62 @@ def random_qp(n: int, m: int, instance: int = 0, dtype=np.float64) -> Dict[str, 
                 r=np.zeros(m), ub=ub, Aeq=None, beq=None, x0=np.zeros(n))
 
 
+def random_qp_bounds(n: int, m: int, instance: int = 0) -> Dict[str, np.ndarray]:
+    """random_qp plus sparse constraint rows interleaved with the dense ones, x0 = 0 strictly feasible:
+    lower bounds -x_j <= 1 (the Constraints.singleCoordinatePositive shape, Constraints.scala:26-35, shifted),
+    upper bounds x_j <= 2, difference rows x_j - x_k <= 0.5 and phase-I style rows x_j - x_k - x_l <= 1
+    (ConstraintSet.scala:153-168: a constraint row with the extra -1 column).  Exercises the engine's split of
+    the Hessian into a dense-row SYRK and per-entry sums over the sparse rows."""
+    spec = random_qp(n, m, instance)
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 7919 + instance))
+    rows, ubs = [], []
+    for j in range(n):
+        a = np.zeros(n)
+        a[j] = -1.0
+        rows.append(a)
+        ubs.append(1.0)
+    for j in rng.choice(n, size=n // 2, replace=False):
+        a = np.zeros(n)
+        a[j] = 1.0
+        rows.append(a)
+        ubs.append(2.0)
+    for _ in range(n // 2):
+        j, k = rng.choice(n, size=2, replace=False)
+        a = np.zeros(n)
+        a[j], a[k] = 1.0, -1.0
+        rows.append(a)
+        ubs.append(0.5)
+    for _ in range(n // 4):
+        j, k, l = rng.choice(n, size=3, replace=False)
+        a = np.zeros(n)
+        a[j], a[k], a[l] = 1.0, -1.0, -1.0
+        rows.append(a)
+        ubs.append(1.0)
+    S = np.array(rows)
+    order = rng.permutation(m + S.shape[0])  # sparse rows interleaved with the dense rows (list order matters)
+    A = np.vstack([spec["A"], S])[order]
+    ub = np.concatenate([spec["ub"], np.array(ubs)])[order]
+    spec.update(id=f"random_qp_bounds(n={n},m={m},instance={instance})", A=A, ub=ub, r=np.zeros(A.shape[0]))
+    return spec
+
+
+def kl_dual_spec(nout: int, k: int, instance: int = 0) -> Dict[str, np.ndarray]:
+    """C4 throughput variant: Dist_KL with k random expectation rows H (entries U[0,1]) over
+    nout outcomes, u = row means x U[0.9, 1.1], no equalities, in the packing of its dual barrier problem
+    (Duality.dualProblem, Duality.scala:99-112; Dist_KL.scala:104-165): z = (lambda, nu) of dimension k + 1,
+    B = (H; 1'), w = (u, 1), R = 1/(nout e) with the reference's e, lambda >= 0 as k bound rows, z0 = 0.001."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 104729 + instance))
+    H = rng.uniform(0.0, 1.0, size=(k, nout))
+    u = H.mean(axis=1) * rng.uniform(0.9, 1.1, k)
+    B = np.vstack([H, np.ones((1, nout))])
+    w = np.concatenate([u, np.ones(1)])
+    A = np.zeros((k, k + 1))
+    A[np.arange(k), np.arange(k)] = -1.0
+    return dict(id=f"kl_dual(nout={nout},k={k},instance={instance})", a0=w, r0=0.0, P=None, A=A, r=np.zeros(k),
+                ub=np.zeros(k), Aeq=None, beq=None, x0=np.full(k + 1, 0.001), kl_B=B,
+                kl_R=np.array([1.0 / (nout * 2.7182811828459045)]))
+
+
 def _positivity(n: int):
     """Constraints.allCoordinatesPositive (Constraints.scala:26-69): -x_j <= 0, j = 0..n-1."""
     return -np.eye(n), np.zeros(n), np.zeros(n)

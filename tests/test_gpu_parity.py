@@ -58,6 +58,57 @@ def test_barrier_oracles_match(mods, n, m):
     eng.close()
 
 
+@pytest.mark.parametrize("n,m", [(40, 30), (300, 200)])
+def test_sparse_rows_hessian_and_direction(mods, n, m):
+    """Problems with bound / difference / phase-I style rows: the engine sums their Hessian entries apart from
+    the dense-row SYRK.  Barrier oracles vs the oracle (1e-12), the same H as the all-dense SYRK path
+    (CVXG_SPARSE_ROWS=0), and the Newton direction within 1e-8 of the oracle."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp_bounds(n, m, instance=5)
+    pb = _opb(O, spec)
+    eng = _engine(Engine, spec)
+    os.environ["CVXG_SPARSE_ROWS"] = "0"
+    try:
+        eng_dense = _engine(Engine, spec)
+    finally:
+        del os.environ["CVXG_SPARSE_ROWS"]
+    pars = SP.standardParams()
+    rng = np.random.default_rng(4)
+    x = 1e-3 * rng.uniform(-1.0, 1.0, n) / np.sqrt(n)
+    for t in (1.0, 1e2, 1e4):
+        f, g, H = eng.barrier_eval(t, x, want_grad=True, want_hess=True)
+        Hr = O.barrier_hessian(pb, t, x, literal=False)
+        assert abs(f - O.barrier_value(pb, t, x)) <= 1e-12 * max(1.0, abs(f))
+        assert np.linalg.norm(H - Hr) <= 1e-12 * np.linalg.norm(Hr)
+        assert np.array_equal(H, H.T)
+        _, _, Hd = eng_dense.barrier_eval(t, x, want_grad=False, want_hess=True)
+        assert np.linalg.norm(H - Hd) <= 1e-13 * np.linalg.norm(Hd)
+        y = O.barrier_gradient(pb, t, x)
+        dx, _, info = eng.newton_direction(pars, t, x, grad=y)
+        rec = O.NewtonStepRecord(x=x, grad=y, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
+        dref = O.newton_direction(pb, t, x, y, pars.tolEqSolve, rec)
+        assert np.linalg.norm(dx - dref) <= 1e-8 * np.linalg.norm(dref), t
+        assert info.regularized == rec.regularized
+    eng.close()
+    eng_dense.close()
+
+
+def test_sparse_rows_barrier_solve(mods):
+    """A whole barrier solve with sparse rows: the same final x and inner-step count as the oracle."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp_bounds(24, 16, instance=6)
+    pars = SP.standardParams()
+    eng = _engine(Engine, spec)
+    eng.set_x(spec["x0"])
+    sol = eng.barrier_solve(pars, termination=0)
+    x = eng.get_x()
+    eng.close()
+    ref = O.barrier_solve(_opb(O, spec), spec["x0"], pars)
+    assert np.linalg.norm(x - ref.x) <= 1e-6 * max(1.0, np.linalg.norm(ref.x))
+    assert sol.duality_gap < pars.tolSolver
+    assert abs(sol.newton_steps - ref.newton_steps) <= max(2, int(0.05 * ref.newton_steps))
+
+
 def test_linear_objective_and_constraint_values(mods):
     Z, SP, Engine, O = mods
     spec = Z.random_qp(70, 150, instance=12)
@@ -404,7 +455,10 @@ def test_kl1A_dual_solve_on_gpu(mods):
     assert np.max(np.abs(sol.x - O.kl1_analytic_solution(n))) < 1e-6
     assert np.max(np.abs(sol.x - Qref)) < 1e-10
     assert np.linalg.norm(sol.lambda_ - solref.x[:2]) <= 1e-6 * np.linalg.norm(solref.x[:2])
-    assert sol.newtonSteps == solref.newton_steps
+    # the inner loops stop on lambda^2/2 <= tol: a last-bit difference in the Hessian's summation order (the
+    # engine splits B diag(y) B' along the outcomes) can move a borderline stop by one step, as in
+    # test_golden_full_solve
+    assert abs(sol.newtonSteps - solref.newton_steps) <= 1
     assert sol.dualityGap < 1e-8
 
 
