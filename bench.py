@@ -97,9 +97,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C3B", "C4"],
+    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C3B", "C4", "C2PD", "C3PD"],
                     help="C3 (default, the metric's config): random dense QP n=4096 m=8192; C2: n=1024 m=2048; "
-                         "C3B: C3 plus 9216 sparse bound / difference rows; C4: KL dual, 2048 outcomes, k=512")
+                         "C3B: C3 plus 9216 sparse bound / difference rows; C4: KL dual, 2048 outcomes, k=512; "
+                         "C2PD / C3PD: the primal-dual solver (solverType PD) on C2 / C3, steps = its KKT solves")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--m", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -127,15 +128,17 @@ def main():
         workload = (f"C4: KL dual barrier (Dist_KL via Duality), {nout} outcomes, dual dimension {n}, {k} bound rows"
                     f", full barrier Newton iterations")
     else:
-        n = args.n or (1024 if wl == "C2" else 4096)
-        m0 = args.m or (2048 if wl == "C2" else 8192)
+        n = args.n or (1024 if wl in ("C2", "C2PD") else 4096)
+        m0 = args.m or (2048 if wl in ("C2", "C2PD") else 8192)
         spec = Z.random_qp_bounds(n, m0, instance=rank) if wl == "C3B" else Z.random_qp(n, m0, instance=rank)
         m = spec["A"].shape[0]
         syrk_rows = m0  # dense rows (the sparse rows' Hessian entries are per-entry sums, not SYRK work)
         workload = (f"{wl}: random dense QP n={n} m={m0}" + (f" plus {m - m0} sparse bound/difference rows"
                                                                if wl == "C3B" else "") +
-                    ", full barrier Newton iterations (assembly + Ruiz + Cholesky + solves + line search) on one "
-                    "MI355X per rank")
+                    (", primal-dual iterations (PrimalDualSolver: KKT-matrix SYRK + 2x Ruiz + Cholesky + solves + "
+                     "residual line search)" if wl.endswith("PD") else
+                     ", full barrier Newton iterations (assembly + Ruiz + Cholesky + solves + line search)") +
+                    " on one MI355X per rank")
     pars = SolverParams.standardParams()
 
     eng = Engine(n, m, 0, device=local_rank)
@@ -155,14 +158,36 @@ def main():
             eng.centering_begin(state["t"])
         return st
 
-    for _ in range(args.warmup):
-        one_step()
-    eng.set_timing(True)
     syrk_ms, chol_ms, solve_ms, ruiz_ms, ls_ms = [], [], [], [], []
+
+    def pd_solve():  # one whole PrimalDualSolver.solve from x0; returns its KKT solves
+        eng.set_x(spec["x0"])
+        s_ = eng.pd_solve(pars)
+        ph = eng.phase_times()
+        syrk_ms.append(ph[5])
+        ruiz_ms.append(ph[1])
+        chol_ms.append(ph[2])
+        solve_ms.append(ph[3])
+        ls_ms.append(ph[4])
+        return s_.newton_steps
+
+    if wl.endswith("PD"):
+        eng.set_timing(True)
+        pd_solve()  # warm-up solve
+        syrk_ms.clear(), ruiz_ms.clear(), chol_ms.clear(), solve_ms.clear(), ls_ms.clear()
+    else:
+        for _ in range(args.warmup):
+            one_step()
+        eng.set_timing(True)
     D.barrier(device)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    if wl.endswith("PD"):  # whole solves until at least `steps` KKT solves were timed
+        done = 0
+        while done < args.steps:
+            done += pd_solve()
+        args.steps = done
+    for _ in range(0 if wl.endswith("PD") else args.steps):
         st = one_step()
         ph = eng.phase_times()
         syrk_ms.append(ph[5])

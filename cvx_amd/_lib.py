@@ -57,6 +57,17 @@ class cvxg_solution(C.Structure):
 
 
 _P = C.c_void_p
+class cvxg_pd_step_info(C.Structure):
+    _fields_ = [("t", C.c_double), ("s0", C.c_double), ("step", C.c_double), ("norm_residual", C.c_double),
+                ("rel_err", C.c_double), ("backtracks", C.c_int), ("fallback", C.c_int), ("ruiz_sweeps", C.c_int),
+                ("regularized", C.c_int)]
+
+
+class cvxg_pd_solution(C.Structure):
+    _fields_ = [("duality_gap", C.c_double), ("norm_dual_residual", C.c_double), ("objective", C.c_double),
+                ("iter", C.c_int), ("maxed_out", C.c_int), ("newton_steps", C.c_int)]
+
+
 _D = C.POINTER(C.c_double)
 _I = C.POINTER(C.c_int)
 
@@ -81,6 +92,10 @@ SIGNATURES = {
     "cvxg_newton_step": (C.c_int, [_P, C.POINTER(cvxg_params), C.POINTER(cvxg_step_info)]),
     "cvxg_centering": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, C.POINTER(cvxg_centering_info)]),
     "cvxg_barrier_solve": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_int, C.POINTER(cvxg_solution)]),
+    "cvxg_pd_direction": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, _D, _D, _D, _D,
+                                    C.POINTER(cvxg_pd_step_info)]),
+    "cvxg_pd_solve": (C.c_int, [_P, C.POINTER(cvxg_params), C.POINTER(cvxg_pd_solution)]),
+    "cvxg_get_lambda": (C.c_int, [_P, _D]),
     "cvxg_set_timing": (C.c_int, [_P, C.c_int]),
     "cvxg_get_phase_times": (C.c_int, [_P, _D, C.c_int]),
 }

@@ -56,8 +56,9 @@ class Solution:
     maxedOut: bool
     newtonSteps: int = 0
     outerIters: int = 0
-    lambda_: Optional[np.ndarray] = None  # dual solutions (Duality.solveDual, Duality.scala:127-131)
+    lambda_: Optional[np.ndarray] = None  # dual solutions (Duality.solveDual, Duality.scala:127-131; PD solver)
     nu: Optional[np.ndarray] = None
+    normDualResidual: Optional[float] = None  # PrimalDualSolver (Solution.scala:24)
 
 
 class ObjectiveFunction:
@@ -327,6 +328,43 @@ class BarrierSolver:
         return GpuBarrierSolver(objF, cnts, eqs, pars, device)
 
 
+class GpuPrimalDualSolver:
+    """PrimalDualSolver (PrimalDualSolver.scala:18-460) on the MI355X engine: each iteration's KKT matrix, its
+    SymmetricLinearSystem solve, dlambda and the residual line-search trials run on the device
+    (cvxg_pd_solve).  Quadratic or linear objective, LinearConstraint list, no equality constraints (the
+    reference's solve_withEQs is not built, see include/cvxg.h)."""
+
+    def __init__(self, objF: ObjectiveFunction, cnts: ConstraintSet, eqs: Optional[EqualityConstraint],
+                 pars: SolverParams, device: int = 0):
+        if not isinstance(objF, (QuadraticObjectiveFunction, LinearObjectiveFunction)):
+            raise TypeError("GPU primal-dual engine: objective must be Quadratic- or LinearObjectiveFunction")
+        if eqs is not None:
+            raise TypeError("GPU primal-dual engine: equality constraints are not supported (solve_withEQs)")
+        if cnts.feasiblePoint is None:
+            raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
+        self.objF, self.cnts, self.eqs, self.pars = objF, cnts, eqs, pars
+        self.dim = cnts.dim
+        self.startingPoint = cnts.feasiblePoint
+        A, r, ub = cnts.packed()
+        self.engine = Engine(cnts.dim, A.shape[0], 0, device)
+        self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
+        self.engine.set_ineq(A, r, ub)
+
+    def solve(self, debugLevel: int = 0) -> Solution:
+        """PrimalDualSolver.solve (:628-633): standard criterion gap < tol and |r_dual| < tol."""
+        self.engine.set_x(self.startingPoint)
+        s = self.engine.pd_solve(self.pars)
+        return Solution(self.engine.get_x(), None, s.duality_gap, None, None, s.iter, bool(s.maxed_out),
+                        s.newton_steps, 0, lambda_=self.engine.get_lambda(), normDualResidual=s.norm_dual_residual)
+
+
+class PrimalDualSolver:
+    @staticmethod
+    def apply(objF, cnts, eqs, pars, device: int = 0) -> GpuPrimalDualSolver:
+        """PrimalDualSolver.apply (PrimalDualSolver.scala:718-728)."""
+        return GpuPrimalDualSolver(objF, cnts, eqs, pars, device)
+
+
 class OptimizationProblem:
     def __init__(self, id: str, objectiveFunction, solver):
         self.id, self.objectiveFunction, self.solver = id, objectiveFunction, solver
@@ -336,9 +374,11 @@ class OptimizationProblem:
 
     @staticmethod
     def apply(id, objF, ineqs: ConstraintSet, eqs, solverType: str, pars, device: int = 0):
-        """OptimizationProblem.scala:133-157 (solverType "BR")."""
-        if solverType not in ("BR", "GPU"):
+        """OptimizationProblem.scala:133-157: solverType "BR" (barrier) or "PD" (primal-dual), both on the engine."""
+        if solverType not in ("BR", "GPU", "PD"):
             raise ValueError(f"Unknown solverType = {solverType}")
+        if solverType == "PD":
+            return OptimizationProblem(id, objF, PrimalDualSolver.apply(objF, ineqs, eqs, pars, device))
         return OptimizationProblem(id, objF, BarrierSolver.apply(objF, ineqs, eqs, pars, device))
 
     @staticmethod
@@ -423,4 +463,5 @@ def problem_from_spec(spec: dict):
 __all__ = ["SolverParams", "Solution", "ObjectiveFunction", "QuadraticObjectiveFunction", "LinearObjectiveFunction",
            "DualKLObjectiveFunction", "Dist_KL",
            "LinearConstraint", "EqualityConstraint", "ConstraintSet", "GpuBarrierSolver", "BarrierSolver",
+           "GpuPrimalDualSolver", "PrimalDualSolver",
            "OptimizationProblem", "problem_from_spec", "CvxgError", "NotStrictlyFeasible"]

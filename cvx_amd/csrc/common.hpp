@@ -25,6 +25,7 @@ struct DevCtrl {
   int ruiz_sweeps;                // Ruiz sweeps executed
   int df_status;                  // dataflow Cholesky: 2 = a dependency wait timed out (scheduling bug)
   unsigned long long min_diag;    // bits of min diag(L) (positive doubles order like uint64)
+  unsigned long long pd_s0;       // bits of the primal-dual step bound s0 (PrimalDualSolver.scala:331-338)
   unsigned long long ruiz_rho[RUIZ_MAX + 2];
   double sc[32];                  // reduced scalars, see SC_* below
 };

@@ -84,6 +84,10 @@ struct cvxg_ctx {
   double* sp_coef = nullptr;
   int kl_nsplit = 1;            // K split of the KL SYRK's tail tiles over the outcomes
   double* kl_spart = nullptr;   // its partials
+  // primal-dual solver state (PrimalDualSolver.scala; allocated on first use)
+  double *lam = nullptr, *dlam = nullptr, *pd_rc = nullptr, *pd_w = nullptr;  // mp
+  double *pd_rhs = nullptr, *pd_d1 = nullptr, *pd_R0 = nullptr, *pd_R1 = nullptr, *pd_tmp = nullptr;  // np
+  double *pd_part_rows = nullptr, *pd_part_cols = nullptr, *pd_out = nullptr, *pd_hout = nullptr;
   // symSolve / kktSymSolve fallback buffers (allocated on first use; ldm = round_up(n + p, 128))
   int eig_ldm = 0;
   double *eig_M = nullptr, *eig_K = nullptr, *eig_d = nullptr, *eig_e = nullptr, *eig_dots = nullptr;
@@ -419,8 +423,11 @@ static int eval_at_x(cvxg_ctx* ctx) {
 
 static double objective_at_x(cvxg_ctx* ctx) { return objective_from_ctrl(ctx, *ctx->hctrl); }
 
-static int assemble_hessian(cvxg_ctx* ctx) {
+// H = t P + A' diag(wts) A (+ the sparse rows' entries); wts = ctx->w = 1/d^2 for the barrier Hessian, or the
+// primal-dual KKT weights lambda/d (then ctrl->t = 1).
+static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr) {
   tstart(ctx, 5);
+  const double* wsrc = wts ? wts : ctx->w;
   // full tiles in whole waves of workgroup slots, then the leftover tiles split along K across all slots
   // (partials + ordered reduce) so the last wave is not a handful of tiles on an otherwise idle chip.
   const double* P = ctx->hasP ? ctx->P : nullptr;
@@ -434,10 +441,10 @@ static int assemble_hessian(cvxg_ctx* ctx) {
                            ctx->kl_spart);
   }
   const double* A = ctx->A;
-  const double* w = ctx->w;
+  const double* w = wsrc;
   int rows = ctx->mp;
   if (ctx->have_sparse) {  // dense rows only; the sparse rows' entries are added below
-    launch_gather_w(ctx->s, ctx->w, ctx->didx, ctx->ndense, ctx->mdp, ctx->wd);
+    launch_gather_w(ctx->s, wsrc, ctx->didx, ctx->ndense, ctx->mdp, ctx->wd);
     A = ctx->As;
     w = ctx->wd;
     rows = ctx->mdp;
@@ -450,7 +457,7 @@ static int assemble_hessian(cvxg_ctx* ctx) {
                          TileList{ctx->tiles + ctx->ntiles_main, ctx->ntiles - ctx->ntiles_main}, ctx->nsplit,
                          ctx->part);
   if (ctx->have_sparse)
-    launch_sparse_hess(ctx->s, ctx->sp_ptr, ctx->sp_pq, ctx->sp_row, ctx->sp_coef, ctx->w, ctx->sp_T, ctx->H, ctx->np);
+    launch_sparse_hess(ctx->s, ctx->sp_ptr, ctx->sp_pq, ctx->sp_row, ctx->sp_coef, wsrc, ctx->sp_T, ctx->H, ctx->np);
   tstop(ctx, 5);
   HIPC(ctx, hipGetLastError());
   return CVXG_OK;
@@ -1048,11 +1055,14 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,
                   ctx->kl_negBy, ctx->kl_part, ctx->kl_ls, ctx->As, ctx->wd, ctx->didx, ctx->sp_ptr,
-                  ctx->sp_pq, ctx->sp_row, ctx->sp_coef, ctx->kl_spart};
+                  ctx->sp_pq, ctx->sp_row, ctx->sp_coef, ctx->kl_spart, ctx->lam, ctx->dlam, ctx->pd_rc,
+                  ctx->pd_w, ctx->pd_rhs, ctx->pd_d1, ctx->pd_R0, ctx->pd_R1, ctx->pd_tmp, ctx->pd_part_rows,
+                  ctx->pd_part_cols, ctx->pd_out};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
   if (ctx->hls) (void)hipHostFree(ctx->hls);
+  if (ctx->pd_hout) (void)hipHostFree(ctx->pd_hout);
   for (int i = 0; i < NT; ++i) {
     if (ctx->tm.ev[i][0]) (void)hipEventDestroy(ctx->tm.ev[i][0]);
     if (ctx->tm.ev[i][1]) (void)hipEventDestroy(ctx->tm.ev[i][1]);
@@ -1500,6 +1510,217 @@ int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count) {
   if (!ctx || !ms) return CVXG_E_ARG;
   for (int i = 0; i < count && i < NT; ++i) ms[i] = ctx->tm.ms[i];
   return CVXG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Primal-dual interior-point solver (PrimalDualSolver.scala, no equality constraints).  The host keeps the
+// scalar loop; per iteration the device assembles H_pd with the shared SYRK (weights lambda_i/d_i), runs
+// SymmetricLinearSystem's Ruiz + scaling and the shared choleskySolve pipeline, forms dlambda, and evaluates the
+// residual-norm backtracking trials in batches of LS_TRIALS.
+// ------------------------------------------------------------------------------------------------
+static int pd_check(cvxg_ctx* ctx) {
+  CHK(check_ready(ctx));
+  if (ctx->p > 0)
+    return set_err(ctx, CVXG_E_UNSUPPORTED,
+                   "PrimalDualSolver.solve_withEQs is not built (its KKT right-hand side has the opposite sign of "
+                   "the no-equality system, PrimalDualSolver.scala:284)");
+  if (ctx->kl) return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: quadratic or linear objective only");
+  if (ctx->m == 0) return set_err(ctx, CVXG_E_ARG, "primal-dual solver needs inequality constraints");
+  if (ctx->lam) return CVXG_OK;
+  const size_t np = ctx->np, mp = ctx->mp;
+  for (double** v : {&ctx->lam, &ctx->dlam, &ctx->pd_rc, &ctx->pd_w}) CHK(dalloc(ctx, v, mp));
+  for (double** v : {&ctx->pd_rhs, &ctx->pd_d1, &ctx->pd_R0, &ctx->pd_R1, &ctx->pd_tmp}) CHK(dalloc(ctx, v, np));
+  CHK(dalloc(ctx, &ctx->pd_part_rows, (size_t)pd_row_blocks(ctx->m) * 2 * LS_TRIALS));
+  CHK(dalloc(ctx, &ctx->pd_part_cols, (size_t)((ctx->n + 255) / 256) * LS_TRIALS));
+  CHK(dalloc(ctx, &ctx->pd_out, 3 * LS_TRIALS));
+  HIPC(ctx, hipHostMalloc((void**)&ctx->pd_hout, 3 * LS_TRIALS * sizeof(double), hipHostMallocDefault));
+  return CVXG_OK;
+}
+
+// grad f(x) + A' v into out (the dual residual, :63-71); Px must hold P x (eval_at_x)
+static void pd_dual_residual(cvxg_ctx* ctx, const double* v, const double* a0, const double* Pv, double* out) {
+  launch_coldot_partials(ctx->s, ctx->A, ctx->np, ctx->mp, ctx->np, v, ctx->part);
+  launch_pd_finalize(ctx->s, a0, Pv, ctx->part, coldot_chunks(ctx->mp), ctx->np, out);
+}
+
+// Search direction at (t, ctx->x, ctx->lam) into ctx->dx / ctx->dlam (PrimalDualSolver.scala:421-425).
+static int pd_direction_dev(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg_pd_step_info* info) {
+  hipStream_t s = ctx->s;
+  const int n = ctx->n, np = ctx->np;
+  CHK(set_t(ctx, t));
+  CHK(eval_at_x(ctx));  // c, d, invd, Px, y = t grad f + A'(1/d); d <= 0 fails (kktMatrix_noEqs asserts f_i < 0)
+  launch_pd_rhs(s, ctx->y, t, n, np, ctx->pd_rhs);                       // rhs1 = -y / t        (:162-176)
+  launch_pd_weights(s, ctx->lam, ctx->d, ctx->m, ctx->mp, ctx->pd_w);    // lambda_i / d_i      (:226-238)
+  launch_ctrl_set(s, ctx->ctrl, 0, 1.0);                                 // hpd starts at objF.hessianAt(x)
+  CHK(assemble_hessian(ctx, ctx->pd_w));
+  launch_ctrl_set(s, ctx->ctrl, 0, t);
+  ctx->x_eval_valid = 0;  // y is reused below as the rhs of the shared choleskySolve
+  // SymmetricLinearSystem: d1 = Ruiz(H), Q = (d1 d1') o H, s = d1 o r (SymmetricLinearSystem.scala:20-23).  Q is
+  // exactly symmetric (H is mirrored, d_i d_j = d_j d_i), so checkSymmetric(Q, 1e-13) holds and choleskySolve runs.
+  tstart(ctx, 1);
+  ruiz(ctx);
+  tstop(ctx, 1);
+  HIPC(ctx, hipMemcpyAsync(ctx->pd_d1, ctx->dfin, (size_t)np * sizeof(double), hipMemcpyDeviceToDevice, s));
+  launch_scale_sym(s, ctx->H, np, np, ctx->pd_d1);
+  launch_neg_scaled(s, ctx->pd_d1, ctx->pd_rhs, np, ctx->y);  // the pipeline solves H x = -y: y = -s
+  launch_dot(s, ctx->y, nullptr, np, ctx->ctrl, SC_GG);
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
+  ctx->normGrad = sqrt(ctx->hctrl->sc[SC_GG]);  // |s| for relativeSize inside choleskySolve
+  cvxg_step_info si;
+  memset(&si, 0, sizeof(si));
+  int rc = cholesky_solve(ctx, pars->tolEqSolve, &si);  // choleskySolve(Q, s): Ruiz of Q, factor, solves, residual
+  info->fallback = 0;
+  info->regularized = si.regularized;
+  info->rel_err = si.rel_err;
+  if (rc == CVXG_E_HIP) return rc;
+  if (rc != CVXG_OK) {  // any exception of choleskySolve -> symSolve(Q, s)  (SymmetricLinearSystem.scala:34)
+    info->fallback = 2;
+    CHK(eig_alloc(ctx));
+    HIPC(ctx, hipMemsetAsync(ctx->eig_b, 0, (size_t)ctx->eig_ldm * sizeof(double), s));
+    launch_axpy(s, ctx->eig_b, ctx->y, -1.0, n, ctx->eig_b);
+    CHK(sym_solve(ctx, ctx->H, n, ctx->eig_b, pars->tolEqSolve));
+    HIPC(ctx, hipMemsetAsync(ctx->dx, 0, (size_t)np * sizeof(double), s));
+    HIPC(ctx, hipMemcpyAsync(ctx->dx, ctx->eig_x, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
+  }
+  launch_scale_vec(s, ctx->dx, ctx->pd_d1, np, ctx->dx);  // x = d :* u  (:54)
+  // deltaLambda (:184-209) with the step bound s0 and the central residual at (x, lambda)
+  launch_rowdot(s, ctx->A, np, ctx->mp, np, ctx->dx, ctx->e);
+  launch_pd_reset_s0(s, ctx->ctrl);
+  launch_pd_dlambda(s, ctx->c, ctx->ub, ctx->lam, ctx->e, t, ctx->m, ctx->mp, ctx->dlam, ctx->pd_rc, ctx->ctrl);
+  HIPC(ctx, hipGetLastError());
+  return CVXG_OK;
+}
+
+// lineSearch_noEQs (PrimalDualSolver.scala:311-374) from (ctx->x, ctx->lam) along (dx, dlam); on success
+// x += s dx, lambda += s dlam.  Needs ctx->c / ctx->Px at x (pd_direction_dev).
+static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg_pd_step_info* info) {
+  hipStream_t s = ctx->s;
+  const int np = ctx->np;
+  const double* Px = ctx->hasP ? ctx->Px : nullptr;
+  pd_dual_residual(ctx, ctx->lam, ctx->a0, Px, ctx->pd_R0);                      // r_dual(x, lambda)
+  if (ctx->hasP) launch_rowdot(s, ctx->P, np, np, np, ctx->dx, ctx->pd_tmp);     // P dx
+  pd_dual_residual(ctx, ctx->dlam, nullptr, ctx->hasP ? ctx->pd_tmp : nullptr, ctx->pd_R1);
+  launch_dot(s, ctx->pd_R0, nullptr, np, ctx->ctrl, SC_RES2);
+  launch_dot(s, ctx->pd_rc, nullptr, ctx->mp, ctx->ctrl, SC_RES2B);
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  double s0;
+  memcpy(&s0, &ctx->hctrl->pd_s0, sizeof(s0));
+  const double norm_rt = sqrt(ctx->hctrl->sc[SC_RES2] + ctx->hctrl->sc[SC_RES2B]);
+  info->s0 = s0;
+  info->norm_residual = norm_rt;
+  const double alpha = pars->alpha, beta = pars->beta;
+  const double maxIter = -30.0 / log(beta);  // a Double (:354)
+  const int kmax = (int)floor(maxIter) + 1;   // the last k the while loop evaluates
+  double sbase = 0.99 * s0;
+  int k = 0, K = -1;
+  double sK = 0.0;
+  while (K < 0) {
+    launch_pd_trials(s, ctx->c, ctx->e, ctx->ub, ctx->lam, ctx->dlam, ctx->m, ctx->pd_R0, ctx->pd_R1, ctx->n, sbase,
+                     beta, t, ctx->pd_part_rows, ctx->pd_part_cols, ctx->pd_out);
+    HIPC(ctx, hipGetLastError());
+    CHK(copy_sync(ctx, ctx->pd_hout, ctx->pd_out, 3 * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost));
+    double sk = sbase;
+    for (int j = 0; j < LS_TRIALS; ++j, ++k) {
+      const double cent = ctx->pd_hout[2 * j], viol = ctx->pd_hout[2 * j + 1], dual = ctx->pd_hout[2 * LS_TRIALS + j];
+      const bool ok = viol == 0.0 && sqrt(dual + cent) < (1 - alpha * sk) * norm_rt;
+      if (ok || k == kmax) {
+        K = k;
+        sK = sk;
+        if (!ok) K = kmax;
+        break;
+      }
+      sk *= beta;  // s *= beta (:358)
+    }
+    sbase = sk;
+  }
+  info->backtracks = K;
+  info->step = sK;
+  if (K >= maxIter) return set_err(ctx, CVXG_E_LINESEARCH, "PrimalDualSolver: Line search unsuccessful.");
+  launch_axpy(s, ctx->x, ctx->dx, sK, np, ctx->x);           // x + dx*s
+  launch_axpy(s, ctx->lam, ctx->dlam, sK, ctx->mp, ctx->lam);  // lambda + dLambda*s
+  HIPC(ctx, hipGetLastError());
+  ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+// gap = -h(x).lambda (:289-297) and |grad f + A' lambda| at the current (x, lambda)
+static int pd_state(cvxg_ctx* ctx, double* gap, double* norm_dual) {
+  CHK(eval_at_x(ctx));
+  pd_dual_residual(ctx, ctx->lam, ctx->a0, ctx->hasP ? ctx->Px : nullptr, ctx->pd_R0);
+  launch_dot(ctx->s, ctx->d, ctx->lam, ctx->mp, ctx->ctrl, SC_RES2B);
+  launch_dot(ctx->s, ctx->pd_R0, nullptr, ctx->np, ctx->ctrl, SC_RES2);
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  *gap = ctx->hctrl->sc[SC_RES2B];
+  *norm_dual = sqrt(ctx->hctrl->sc[SC_RES2]);
+  return CVXG_OK;
+}
+
+int cvxg_pd_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, const double* lambda,
+                      double* dx, double* dlambda, cvxg_pd_step_info* info) {
+  if (!ctx || !pars || !x || !lambda) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(pd_check(ctx));
+  cvxg_pd_step_info tmp;
+  if (!info) info = &tmp;
+  memset(info, 0, sizeof(*info));
+  info->t = t;
+  CHK(cvxg_set_x(ctx, x));
+  CHK(upload_vec(ctx, ctx->lam, lambda, ctx->m, ctx->mp));
+  CHK(pd_direction_dev(ctx, pars, t, info));
+  CHK(sync_ctrl(ctx));
+  memcpy(&info->s0, &ctx->hctrl->pd_s0, sizeof(double));
+  if (dx) CHK(copy_sync(ctx, dx, ctx->dx, ctx->n * sizeof(double), hipMemcpyDeviceToHost));
+  if (dlambda) CHK(copy_sync(ctx, dlambda, ctx->dlam, ctx->m * sizeof(double), hipMemcpyDeviceToHost));
+  return CVXG_OK;
+}
+
+int cvxg_pd_solve(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_pd_solution* sol) {
+  if (!ctx || !pars) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(pd_check(ctx));
+  const double tol = pars->tolSolver, mu = 10.0;
+  const double m = ctx->m;
+  // lambda = constraintSet.lambda(x) = -1/h (ConstraintSet.scala:116-120), gap = -h.lambda, t = mu m / gap
+  CHK(set_t(ctx, 1.0));
+  CHK(eval_at_x(ctx));
+  launch_pd_lambda0(ctx->s, ctx->invd, ctx->m, ctx->mp, ctx->lam);
+  double gap = 0.0, norm_dual = 0.0;
+  CHK(pd_state(ctx, &gap, &norm_dual));
+  norm_dual = std::numeric_limits<double>::max();  // OptimizationState(normDualResidual = Double.MaxValue)
+  double t = mu * m / gap;
+  const double maxIter = 2000.0 / mu;
+  int iter = 0;
+  while (!(gap < tol && norm_dual < tol) && iter < maxIter) {
+    cvxg_pd_step_info info;
+    memset(&info, 0, sizeof(info));
+    info.t = t;
+    CHK(pd_direction_dev(ctx, pars, t, &info));
+    CHK(pd_line_search(ctx, pars, t, &info));
+    CHK(pd_state(ctx, &gap, &norm_dual));
+    t = mu * m / gap;  // JVM Double semantics: a zero gap gives +Infinity
+    ++iter;
+    timing_collect(ctx);  // phase times of the last iteration (instrumentation, when enabled)
+  }
+  if (sol) {
+    sol->duality_gap = gap;
+    sol->norm_dual_residual = norm_dual;
+    sol->objective = objective_at_x(ctx);
+    sol->iter = iter - 1;
+    sol->maxed_out = iter == (int)maxIter;
+    sol->newton_steps = iter;
+  }
+  return CVXG_OK;
+}
+
+int cvxg_get_lambda(cvxg_ctx* ctx, double* lambda) {
+  if (!ctx || !lambda) return CVXG_E_ARG;
+  if (!ctx->lam) return set_err(ctx, CVXG_E_ARG, "no primal-dual iterate (call cvxg_pd_solve first)");
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  return copy_sync(ctx, lambda, ctx->lam, ctx->m * sizeof(double), hipMemcpyDeviceToHost);
 }
 
 }  // extern "C"

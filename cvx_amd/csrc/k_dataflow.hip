@@ -293,6 +293,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         df_stage(cs.Sa, mA, ld);
         if (!wait(state, df_tri(b, b), k)) return;
         mark(k, 1, 1);
+        {  // rhs block b with all earlier TRSM updates (state(b,b) >= k), loaded now so its latency hides behind the
+           // slices; minus L_b,k w_k inside POTRF(b).  (POTRF(b-2) of this workgroup is done with ps.B.)
+          const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+          for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
+        }
         d4f dacc[NBLK16];
         {
           const Sc1Mem mD(L + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
@@ -329,6 +334,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
           }
+          if (cb == 3) mark(k, 1, 3);  // trace: last row-block of L_kk^-1 in hand
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q;
@@ -377,10 +383,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           const int rr = t >> 5, cc = 2 * (t & 31);
           *reinterpret_cast<f64x2*>(cs.Sa + rr * DF_SP + cc) = *reinterpret_cast<const f64x2*>(Lp + rr * DF_SP + cc);
         }
-        {  // rhs block b with all earlier TRSM updates (state(b,b) >= k); minus L_b,k w_k inside POTRF(b)
-          const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-          for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
-        }
         publish(df_tri(b, k), k + 1);  // L_b,k stored
         mark(k, 1, 2);
       }
@@ -414,7 +416,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         mark(k, 2, 2);
         return true;
       };
-      if (!potrf64_factor<Sc1Mem>(L, ld, b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix)) {
+      if (!potrf64_factor<Sc1Mem>(L, ld, b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix,
+                                  trace ? trace + 4 * (size_t)(ntasks + 3 * b) + 3 : nullptr)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }

@@ -54,6 +54,22 @@ void launch_sparse_hess(hipStream_t s, const int* ptr, const int* pq, const int*
                         const double* w, int T, double* H, int ld);
 void launch_gather_w(hipStream_t s, const double* w, const int* idx, int nd, int ndp, double* wd);
 
+// ---- primal-dual iteration pieces (k_pd.hip) ---------------------------------------------------------
+void launch_pd_rhs(hipStream_t s, const double* y, double t, int n, int np, double* rhs);
+void launch_pd_weights(hipStream_t s, const double* lam, const double* d, int m, int mp, double* w);
+void launch_scale_sym(hipStream_t s, double* H, int ld, int np, const double* d);
+void launch_neg_scaled(hipStream_t s, const double* d, const double* r, int np, double* y);
+void launch_pd_dlambda(hipStream_t s, const double* c, const double* ub, const double* lam, const double* e, double t,
+                       int m, int mp, double* dlam, double* rc, DevCtrl* ctrl);
+void launch_pd_finalize(hipStream_t s, const double* a0, const double* Pv, const double* part, int nchunks, int cols,
+                        double* out);
+int pd_row_blocks(int m);
+void launch_pd_lambda0(hipStream_t s, const double* invd, int m, int mp, double* lam);
+void launch_pd_reset_s0(hipStream_t s, DevCtrl* ctrl);
+void launch_pd_trials(hipStream_t s, const double* c, const double* e, const double* ub, const double* lam,
+                      const double* dlam, int m, const double* R0, const double* R1, int n, double sbase, double beta,
+                      double t, double* part_rows, double* part_cols, double* out);
+
 // ---- MFMA SYRK (k_syrk.hip) -----------------------------------------------------------------------
 // H = t*P + A' diag(w) A over the lower tile list; split-K when nsplit > 1 (partials + ordered reduce).
 void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double* w, int mp, const double* P,

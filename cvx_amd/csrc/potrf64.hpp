@@ -198,7 +198,7 @@ struct NoFix {
 template <class M, class Fix = NoFix>
 __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __restrict__ rhs, int nrhs,
                                double* __restrict__ Linv, DevCtrl* ctrl, Potrf64Smem& sm, int* lflag = nullptr,
-                               Fix fix = Fix()) {
+                               Fix fix = Fix(), unsigned long long* pub_stamp = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mR(rhs + (size_t)base * nrhs, (unsigned)(NB * nrhs) * 8u);                // rhs block k
@@ -357,6 +357,7 @@ __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __
     if (lflag && w == 3) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(lflag, kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (pub_stamp && lane == 0 && kb == 3) *pub_stamp = __builtin_amdgcn_s_memrealtime();  // trace only
     }
     P64_STAMP(5 + 4 * kb);
   }

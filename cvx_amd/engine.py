@@ -177,6 +177,28 @@ class Engine:
         self._check(self.lib.cvxg_centering(self.h, C.byref(ps), float(t), C.byref(info)))
         return info
 
+    # --- primal-dual solver (PrimalDualSolver.scala, no equalities) -------------------------------
+    def pd_direction(self, pars, t: float, x, lam):
+        """(dx, dlambda, info) of one primal-dual KKT solve at (t, x, lambda) (cvxg_pd_direction)."""
+        x, lam = _f64(x), _f64(lam)
+        dx, dlam = np.zeros(self.n), np.zeros(self.m)
+        info = L.cvxg_pd_step_info()
+        ps = params_struct(pars)
+        self._check(self.lib.cvxg_pd_direction(self.h, C.byref(ps), float(t), _dp(x), _dp(lam), _dp(dx), _dp(dlam),
+                                               C.byref(info)))
+        return dx, dlam, info
+
+    def pd_solve(self, pars) -> L.cvxg_pd_solution:
+        sol = L.cvxg_pd_solution()
+        ps = params_struct(pars)
+        self._check(self.lib.cvxg_pd_solve(self.h, C.byref(ps), C.byref(sol)))
+        return sol
+
+    def get_lambda(self) -> np.ndarray:
+        lam = np.zeros(self.m)
+        self._check(self.lib.cvxg_get_lambda(self.h, _dp(lam)))
+        return lam
+
     def barrier_solve(self, pars, termination: int = 0) -> L.cvxg_solution:
         sol = L.cvxg_solution()
         ps = params_struct(pars)

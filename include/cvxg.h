@@ -167,6 +167,49 @@ int cvxg_centering(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg_center
  * CvxUtils.phase_I_TerminationCriterion (CvxUtils.scala:61-87). */
 int cvxg_barrier_solve(cvxg_ctx* ctx, const cvxg_params* pars, int termination, cvxg_solution* sol);
 
+/* ---- primal-dual interior-point solver (PrimalDualSolver.scala, solverType "PD") ---------------- */
+
+/* One primal-dual iteration as PrimalDualSolver.solve_noEQs runs it (PrimalDualSolver.scala:421-427). */
+typedef struct cvxg_pd_step_info {
+  double t;                 /* the barrier-analogue parameter t = mu m / gap */
+  double s0;                /* step bound min(1, -lambda_i / dlambda_i) (:331-338) */
+  double step;              /* accepted step s (0.99 s0 beta^k) */
+  double norm_residual;     /* |r_t| at (x, lambda) (:343, 350) */
+  double rel_err;           /* choleskySolve residual ratio */
+  int backtracks;           /* k of the accepted step */
+  int fallback;             /* 0 choleskySolve(Q, s), 2 symSolve(Q, s) (SymmetricLinearSystem.scala:28-35) */
+  int ruiz_sweeps;          /* SymmetricLinearSystem's own Ruiz sweeps (choleskySolve equilibrates Q again) */
+  int regularized;          /* regularizedCholesky used Q + 1e-10 I */
+} cvxg_pd_step_info;
+
+/* Solution of PrimalDualSolver.solve (PrimalDualSolver.scala:455-459). */
+typedef struct cvxg_pd_solution {
+  double duality_gap;       /* surrogate gap -h(x).lambda (:289-297) */
+  double norm_dual_residual;/* |grad f + Dg' lambda| (:63-71) */
+  double objective;         /* objF.valueAt(x) */
+  int iter;                 /* iterations - 1 (reference semantics, :458) */
+  int maxed_out;            /* iter == 2000/mu */
+  int newton_steps;         /* KKT solves performed (instrumentation) */
+} cvxg_pd_solution;
+
+/* The primal-dual search direction at (t, x, lambda) (PrimalDualSolver.scala:216-261, 184-209): the KKT
+ * matrix H_pd = hessian f + sum_i (lambda_i / -f_i) a_i a_i' (weighted SYRK), rhs1 = -grad f + sum_i a_i/(t f_i),
+ * SymmetricLinearSystem(H_pd, rhs1).solve(tolEqSolve) (Ruiz, then choleskySolve with its own Ruiz, symSolve on any
+ * failure), then dlambda.  lambda has m entries; dx (n) / dlambda (m) may be NULL.  No equality constraints. */
+int cvxg_pd_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, const double* lambda,
+                      double* dx, double* dlambda, cvxg_pd_step_info* info);
+
+/* PrimalDualSolver.solve (PrimalDualSolver.scala:628-633 -> solve_noEQs :381-460) from the current iterate
+ * (cvxg_set_x: a strictly feasible point): lambda0 = -1/h(x0) (ConstraintSet.scala:116-120), t = mu m / gap,
+ * residual-norm backtracking line search (:311-374), stop when gap < tolSolver and |r_dual| < tolSolver.
+ * The reference's solve_withEQs is not built (CVXG_E_UNSUPPORTED for p > 0): it passes q = rhs1 + A'nu to
+ * KKTSystem, which solves H dx + A'dnu = -q, the opposite sign of its own no-equality system ("FIX ME",
+ * PrimalDualSolver.scala:284), and its line search fails on the reference's known-answer problems. */
+int cvxg_pd_solve(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_pd_solution* sol);
+
+/* The dual iterate lambda (m entries) after cvxg_pd_solve. */
+int cvxg_get_lambda(cvxg_ctx* ctx, double* lambda);
+
 /* ---- instrumentation ----------------------------------------------------------------------------- */
 
 /* Per-phase device time of the last cvxg_newton_step (ms), measured with HIP events on the ctx

@@ -823,3 +823,253 @@ def kl2A_data(n: int):
     IA = (np.arange(n) < 3).astype(np.float64)
     IB = (np.arange(n) >= n // 2).astype(np.float64)
     return np.vstack([IA, IB]), np.array([0.36, 0.1])
+
+
+# ----------------------------------------------------------------------------------------------
+# Primal-dual interior-point solver (PrimalDualSolver.scala, SymmetricLinearSystem.scala)
+# ----------------------------------------------------------------------------------------------
+
+
+class LineSearchFailedException(Exception):
+    """LineSearchFailedException (PrimalDualSolver.scala:371, 540)."""
+
+
+def check_symmetric(Q: np.ndarray, tol: float) -> bool:
+    """MatrixUtils.scala:207-211 — Frobenius norm of Q - Q' below tol."""
+    diff = Q - Q.T
+    return math.sqrt(float(np.sum(diff * diff))) < tol
+
+
+@dataclass
+class PDStepRecord:
+    """One primal-dual iteration (what the GPU engine reports in cvxg_pd_step_info)."""
+
+    t: float
+    x: np.ndarray
+    lam: np.ndarray
+    dx: np.ndarray = None
+    dlam: np.ndarray = None
+    s0: float = float("nan")
+    step: float = float("nan")
+    backtracks: int = 0
+    fallback: int = 0          # 0 choleskySolve, 2 symSolve
+    ruiz_sweeps: int = 0       # SymmetricLinearSystem's Ruiz (the inner choleskySolve runs its own)
+    regularized: int = 0
+
+
+@dataclass
+class PDSolution:
+    """Solution.scala as filled by PrimalDualSolver.solve_noEQs (:455-459)."""
+
+    x: np.ndarray
+    lam: np.ndarray
+    dualityGap: float
+    normDualResidual: float
+    iter: int
+    maxedOut: bool
+    records: List[PDStepRecord] = field(default_factory=list)
+
+
+def symmetric_linear_system_solve(H: np.ndarray, r: np.ndarray, tol: float,
+                                  rec: Optional[PDStepRecord] = None) -> np.ndarray:
+    """SymmetricLinearSystem.scala:15-56 — Ruiz once here (d, Q = (dd')oH, s = d o r), then
+    checkSymmetric(Q, 1e-13) ? choleskySolve(Q, s) (which equilibrates Q AGAIN, MatrixUtils.scala:484) :
+    svdSolve; any exception of choleskySolve -> symSolve(Q, s); x = d o u."""
+    d, Q, sweeps = ruiz_equilibrate(H)
+    s = d * r
+    if not check_symmetric(Q, 1e-13):
+        raise NotImplementedError("svdSolve branch (Q not symmetric): H is assembled exactly symmetric here")
+    fb = 0
+    info = CholSolveInfo()
+    try:
+        u = cholesky_solve(Q, s, tol, info)
+    except Exception:
+        fb = 2
+        u = sym_solve(Q, s, tol)
+    if rec is not None:
+        rec.fallback, rec.ruiz_sweeps, rec.regularized = fb, sweeps, info.regularized
+    return d * u
+
+
+def pd_constraint_function(pb: Problem, x: np.ndarray) -> np.ndarray:
+    """ConstraintSet.constraintFunctionAt: h_i = g_i(x) - ub_i."""
+    return np.array([constraint_value(pb, i, x) - pb.ub[i] for i in range(pb.m)])
+
+
+def pd_kkt_matrix(pb: Problem, x: np.ndarray, lam: np.ndarray) -> np.ndarray:
+    """PrimalDualSolver.kktMatrix_noEqs (:216-240): hpd = objF.hessianAt(x); per constraint in list order
+    hpd += grad2_gi*li - (G G')*(li/fi) (grad2_gi = zeros for a LinearConstraint)."""
+    hpd = objective_hessian(pb, x).copy()
+    for i in range(pb.m):
+        li = lam[i]
+        fi = constraint_value(pb, i, x) - pb.ub[i]
+        assert fi < 0, "line search did not pull back into strictly feasible region"
+        G = pb.A[i]
+        hpd = hpd + (np.zeros_like(hpd) * li - np.outer(G, G) * (li / fi))
+    return hpd
+
+
+def pd_rhs1(pb: Problem, t: float, x: np.ndarray) -> np.ndarray:
+    """PrimalDualSolver.rhs1 (:162-176): -grad f + sum_i grad g_i / (t f_i)."""
+    res = -objective_gradient(pb, x)
+    for i in range(pb.m):
+        fx = constraint_value(pb, i, x) - pb.ub[i]
+        res = res + pb.A[i] / (t * fx)
+    return res
+
+
+def pd_central_residual(pb: Problem, t: float, x: np.ndarray, lam: np.ndarray) -> np.ndarray:
+    """:97-106 — -lambda_i g_i - 1/t (g = constraintFunctionAt)."""
+    g = pd_constraint_function(pb, x)
+    return -lam * g - 1.0 / t
+
+
+def pd_dual_residual(pb: Problem, x: np.ndarray, lam: np.ndarray) -> np.ndarray:
+    """:63-71 — grad f + Dg' lambda."""
+    return objective_gradient(pb, x) + pb.A.T @ lam
+
+
+def pd_residual(pb: Problem, t: float, x: np.ndarray, lam: np.ndarray) -> np.ndarray:
+    """:123-130 — (r_dual, r_central)."""
+    return np.concatenate([pd_dual_residual(pb, x, lam), pd_central_residual(pb, t, x, lam)])
+
+
+def pd_delta_lambda(pb: Problem, t: float, x: np.ndarray, dx: np.ndarray, lam: np.ndarray) -> np.ndarray:
+    """:184-209 — dlambda_i = (-lambda_i (Dg dx)_i + r_cent_i) / g_i."""
+    r_cent = pd_central_residual(pb, t, x, lam)
+    gx = pd_constraint_function(pb, x)
+    assert np.all(gx < 0), "line search did not pull back into strictly feasible region"
+    w = pb.A @ dx
+    return (-lam * w + r_cent) / gx
+
+
+def pd_direction(pb: Problem, t: float, x: np.ndarray, lam: np.ndarray, tolEqSolve: float,
+                 rec: Optional[PDStepRecord] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """One KKT solve of solve_noEQs (:421-425): kktSystem_noEqs + SymmetricLinearSystem.solve + deltaLambda."""
+    H = pd_kkt_matrix(pb, x, lam)
+    rhs = pd_rhs1(pb, t, x)
+    dx = symmetric_linear_system_solve(H, rhs, tolEqSolve, rec)
+    return dx, pd_delta_lambda(pb, t, x, dx, lam)
+
+
+def pd_line_search(pb: Problem, t: float, x: np.ndarray, lam: np.ndarray, dx: np.ndarray, dlam: np.ndarray,
+                   pars: SolverParams, rec: Optional[PDStepRecord] = None):
+    """lineSearch_noEQs (:311-374).  C.isInSet is the problem's domain (the whole space for the problems the
+    engine accepts); maxIter = -30/log(beta) as a Double; throws when iter >= maxIter."""
+    s0 = 1.0
+    for i in range(lam.shape[0]):
+        if dlam[i] < 0 and -lam[i] / dlam[i] < s0:
+            s0 = -lam[i] / dlam[i]
+    s = 0.99 * s0
+    alpha, beta = pars.alpha, pars.beta
+    r_t = pd_residual(pb, t, x, lam)
+    x_s = x + dx * s
+    lam_s = lam + dlam * s
+    norm_rt = float(np.linalg.norm(r_t))
+    norm_rts = float(np.linalg.norm(pd_residual(pb, t, x_s, lam_s)))
+    feas = all(is_satisfied_strictly(pb, i, x_s) for i in range(pb.m))
+    decreased = norm_rts < (1 - alpha * s) * norm_rt
+    it = 0
+    maxIter = -30 / math.log(beta)
+    while not (feas and decreased) and it <= maxIter:
+        s *= beta
+        x_s = x + dx * s
+        lam_s = lam + dlam * s
+        norm_rts = float(np.linalg.norm(pd_residual(pb, t, x_s, lam_s)))
+        feas = all(is_satisfied_strictly(pb, i, x_s) for i in range(pb.m))
+        decreased = norm_rts < (1 - alpha * s) * norm_rt
+        it += 1
+    if it >= maxIter:
+        raise LineSearchFailedException("Line search unsuccessful.")
+    if rec is not None:
+        rec.s0, rec.step, rec.backtracks = s0, s, it
+    return x_s, lam_s
+
+
+def pd_solve(pb: Problem, x0: np.ndarray, pars: SolverParams, record: bool = False) -> PDSolution:
+    """PrimalDualSolver.solve (:628-633) -> solve_noEQs (:381-460): lambda0 = -1/h(x0)
+    (ConstraintSet.lambda, ConstraintSet.scala:116-120), t = mu m / gap, stop when gap < tol and
+    |r_dual| < tol (the state of the previous iteration), at most 2000/mu iterations."""
+    if pb.Aeq is not None:
+        raise NotImplementedError("solve_withEQs: see pd_solve_with_eqs")
+    tol = pars.tolSolver
+    mu = 10.0
+    x = x0.copy()
+    lam = -1.0 / pd_constraint_function(pb, x)
+    gap = -float(np.dot(pd_constraint_function(pb, x), lam))
+    normDual = float("inf")
+    m = pb.m
+    t = mu * m / gap
+    maxIter = 2000 / mu
+    it = 0
+    records = []
+    while not (gap < tol and normDual < tol) and it < maxIter:
+        rec = PDStepRecord(t=t, x=x.copy(), lam=lam.copy())
+        dx, dlam = pd_direction(pb, t, x, lam, pars.tolEqSolve, rec)
+        rec.dx, rec.dlam = dx, dlam
+        x, lam = pd_line_search(pb, t, x, lam, dx, dlam, pars, rec)
+        gap = -float(np.dot(pd_constraint_function(pb, x), lam))
+        normDual = float(np.linalg.norm(pd_dual_residual(pb, x, lam)))
+        with np.errstate(divide="ignore"):
+            t = float(np.float64(mu * m) / np.float64(gap))  # JVM Double semantics: x/0.0 = Infinity
+        it += 1
+        if record:
+            records.append(rec)
+    return PDSolution(x=x, lam=lam, dualityGap=gap, normDualResidual=normDual, iter=it - 1,
+                      maxedOut=it == maxIter, records=records)
+
+
+def pd_solve_with_eqs(pb: Problem, x0: np.ndarray, pars: SolverParams, record: bool = False):
+    """PrimalDualSolver.solve_withEQs (:550-621) as written: KKTSystem(H, A, q = rhs1 + A'nu, b = -(Ax - b))
+    (:271-285, the reference's own 'FIX ME: check this!'); KKTSystem solves H dx + A' w = -q, the OPPOSITE sign
+    of the no-equality system H dx = rhs1.  lineSearch_withEQs (:478-543) on the full residual
+    (r_dual + A'nu, r_central, Ax - b); normDualResidual is the norm of that full residual; <= 1500/mu
+    iterations.  Returns (x, lambda, nu, gap, normResidual, iter, maxedOut) or raises like the reference."""
+    A, b = pb.Aeq, pb.beq
+    tol, mu, m = pars.tolSolver, 10.0, pb.m
+    x = x0.copy()
+    lam = -1.0 / pd_constraint_function(pb, x)
+    nu = np.zeros(A.shape[0])
+    gap = -float(np.dot(pd_constraint_function(pb, x), lam))
+    normRes = float("inf")
+    t = mu * m / gap
+
+    def residual(t_, x_, l_, n_):
+        return np.concatenate([pd_dual_residual(pb, x_, l_) + A.T @ n_, pd_central_residual(pb, t_, x_, l_),
+                               A @ x_ - b])
+
+    maxIter = 1500 / mu
+    it = 0
+    while not (gap < tol and normRes < tol) and it < maxIter:
+        H = pd_kkt_matrix(pb, x, lam)
+        q = pd_rhs1(pb, t, x) + A.T @ nu
+        dx, dnu = kkt_solve(H, A, q, -(A @ x - b), pars.tolEqSolve)
+        dlam = pd_delta_lambda(pb, t, x, dx, lam)
+        s0 = 1.0
+        for i in range(m):
+            if dlam[i] < 0 and -lam[i] / dlam[i] < s0:
+                s0 = -lam[i] / dlam[i]
+        s = 0.99 * s0
+        norm_rt = float(np.linalg.norm(residual(t, x, lam, nu)))
+
+        def trial(s_):
+            x_s, l_s, n_s = x + dx * s_, lam + dlam * s_, nu + dnu * s_
+            ok = all(is_satisfied_strictly(pb, i, x_s) for i in range(m))
+            dec = float(np.linalg.norm(residual(t, x_s, l_s, n_s))) < (1 - pars.alpha * s_) * norm_rt
+            return ok and dec, (x_s, l_s, n_s)
+
+        good, u = trial(s)
+        k = 0
+        maxLS = -30 / math.log(pars.beta)
+        while not good and k <= maxLS:
+            s *= pars.beta
+            good, u = trial(s)
+            k += 1
+        if k >= maxLS:
+            raise LineSearchFailedException("Line search unsuccessful.")
+        x, lam, nu = u
+        gap = -float(np.dot(pd_constraint_function(pb, x), lam))
+        normRes = float(np.linalg.norm(residual(t, x, lam, nu)))
+        t = mu * m / gap
+        it += 1
+    return x, lam, nu, gap, normRes, it - 1, it == maxIter

@@ -471,3 +471,85 @@ def test_kl2A_dual_solve_on_gpu(mods):
     sol = Dist_KL.apply("dist_KL_2A", n, None, None, A, r, "BR").solveDual("BR", SP.standardParams())
     assert np.max(np.abs(sol.x - O.kl1_analytic_solution(n))) < 1e-6
     assert sol.nu is not None and sol.nu.shape == (3,)
+
+
+# ---- PrimalDualSolver (solverType "PD") on the device -----------------------------------------------------------
+
+@pytest.mark.parametrize("kind,n,m", [("qp", 40, 96), ("qp", 300, 500), ("bounds", 60, 40)])
+def test_pd_direction_vs_oracle(mods, kind, n, m):
+    """One primal-dual KKT solve (kktMatrix_noEqs + SymmetricLinearSystem + deltaLambda) from identical
+    (t, x, lambda): dx and dlambda within 1e-8 of the oracle, the same s0, fallback and Ruiz sweep count."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp(n, m, instance=41) if kind == "qp" else Z.random_qp_bounds(n, m, instance=42)
+    pb = _opb(O, spec)
+    eng = _engine(Engine, spec)
+    pars = SP.standardParams()
+    x = spec["x0"]
+    lam = -1.0 / O.pd_constraint_function(pb, x)
+    for t in (10.0, 1e3, 1e5):
+        dx, dlam, info = eng.pd_direction(pars, t, x, lam)
+        rec = O.PDStepRecord(t=t, x=x, lam=lam)
+        dxr, dlr = O.pd_direction(pb, t, x, lam, pars.tolEqSolve, rec)
+        assert np.linalg.norm(dx - dxr) <= 1e-8 * np.linalg.norm(dxr), t
+        assert np.linalg.norm(dlam - dlr) <= 1e-8 * np.linalg.norm(dlr), t
+        s0 = 1.0
+        for i in range(pb.m):
+            if dlr[i] < 0 and -lam[i] / dlr[i] < s0:
+                s0 = -lam[i] / dlr[i]
+        assert info.s0 == pytest.approx(s0, rel=1e-10)
+        assert info.fallback == rec.fallback and info.ruiz_sweeps == rec.ruiz_sweeps
+        assert info.regularized == rec.regularized
+    eng.close()
+
+
+@pytest.mark.parametrize("kind,n,m", [("qp", 40, 96), ("bounds", 24, 16)])
+def test_pd_solve_vs_oracle(mods, kind, n, m):
+    """PrimalDualSolver.solve end to end: the oracle's x and lambda (1e-6), its iteration count (+-1), gap and
+    dual residual below tolSolver."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp(n, m, instance=43) if kind == "qp" else Z.random_qp_bounds(n, m, instance=6)
+    pb = _opb(O, spec)
+    pars = SP.standardParams()
+    eng = _engine(Engine, spec)
+    eng.set_x(spec["x0"])
+    sol = eng.pd_solve(pars)
+    x, lam = eng.get_x(), eng.get_lambda()
+    eng.close()
+    ref = O.pd_solve(pb, spec["x0"], pars)
+    assert np.linalg.norm(x - ref.x) <= 1e-6 * max(1.0, np.linalg.norm(ref.x))
+    assert np.linalg.norm(lam - ref.lam) <= 1e-6 * max(1.0, np.linalg.norm(ref.lam))
+    assert abs(sol.iter - ref.iter) <= 1
+    assert sol.duality_gap < pars.tolSolver and sol.norm_dual_residual < pars.tolSolver
+    assert not sol.maxed_out
+
+
+@pytest.mark.parametrize("spec_fn", ["probability_simplex_problem", "min_dot_product"])
+def test_pd_known_minimizers_on_gpu(mods, spec_fn):
+    """SimpleOptimizationProblems with solverType "PD" (the Runner's default, Runner.scala:31):
+    OptimizationProblem.withoutFeasiblePoint(..., "PD") -> phase I on the engine, then the device PD solver."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import OptimizationProblem, problem_from_spec
+    spec = (Z.probability_simplex_problem(10) if spec_fn == "probability_simplex_problem"
+            else Z.min_dot_product(np.array([1.0, -2.0, 0.5, 3.0, -1.5])))
+    objF, cs, eqs = problem_from_spec(dict(spec, x0=spec["x_where_defined"]))
+    pars = SP.standardParams()
+    prob = OptimizationProblem.withoutFeasiblePoint(spec["id"], objF, cs, eqs, "PD", pars)
+    sol = prob.solve()
+    fopt = Z.objective_value(spec, spec["x_opt"])
+    assert abs(Z.objective_value(spec, sol.x) - fopt) < 1e-2
+    if spec_fn == "min_dot_product":
+        assert np.linalg.norm(sol.x - spec["x_opt"]) < 1e-2
+    assert sol.dualityGap < pars.tolSolver and sol.normDualResidual < pars.tolSolver
+    assert np.all(sol.lambda_ > 0)
+    prob.solver.engine.close()
+
+
+def test_pd_with_equalities_is_unsupported(mods):
+    Z, SP, Engine, O = mods
+    spec = Z.joptP2()
+    eng = _engine(Engine, spec)
+    eng.set_x(np.array([0.5, 0.5]))
+    from cvx_amd.engine import CvxgError
+    with pytest.raises(CvxgError):
+        eng.pd_solve(SP.standardParams())
+    eng.close()

@@ -202,3 +202,49 @@ def test_kl_dual_oracles_are_consistent():
         dg = (O.objective_gradient(pb, z + e) - O.objective_gradient(pb, z - e)) / (2 * h)
         assert np.max(np.abs(dg - Hs[:, i])) < 1e-7
     assert O.KL_E != np.e  # the reference's constant (Dist_KL.scala:114) is kept, not exp(1)
+
+
+# ---- PrimalDualSolver (PrimalDualSolver.scala; Runner.scala:31 runs the known-answer problems with "PD") ------
+
+@pytest.mark.parametrize("spec", [s for s in Z.known_answer_zoo() if s["Aeq"] is None and
+                                  s["id"] != "normSquaredWithFreeVariables"], ids=lambda s: s["id"])
+def test_known_minimizers_primal_dual_with_phase_I(spec):
+    """OptimizationProblem.withoutFeasiblePoint(..., "PD"): phase I, then PrimalDualSolver.solve; the known
+    minimiser within the Runner tolerance 1e-2, gap and dual residual below tolSolver.  (normSquaredWithFreeVariables
+    is left out: its phase I is unbounded below in the slack and returns x_0 ~ -5e11, from which the primal-dual
+    iteration leaves the strictly feasible region — kktMatrix_noEqs asserts.)"""
+    pb = _problem(spec)
+    pars = O.standard_params()
+    x0 = O.with_feasible_point(pb, spec["x_where_defined"], pars)
+    sol = O.pd_solve(pb, x0, pars)
+    assert abs(O.objective_value(pb, sol.x) - O.objective_value(pb, spec["x_opt"])) < 1e-2
+    if spec["id"] != "Probability_simplex_problem":
+        assert np.linalg.norm(sol.x - spec["x_opt"]) < 1e-2
+    assert sol.dualityGap < pars.tolSolver and sol.normDualResidual < pars.tolSolver
+    assert np.all(sol.lam > 0)
+
+
+def test_primal_dual_agrees_with_barrier_on_random_qp():
+    """Both solvers of the reference reach the same minimiser of a random dense QP (strictly convex)."""
+    spec = Z.random_qp(30, 60, instance=3)
+    pb = _problem(spec)
+    pars = O.standard_params()
+    pd = O.pd_solve(pb, spec["x0"], pars, record=True)
+    br = O.barrier_solve(pb, spec["x0"], pars)
+    assert np.linalg.norm(pd.x - br.x) < 1e-7 * max(1.0, np.linalg.norm(br.x))
+    assert pd.iter + 1 == len(pd.records) and not pd.maxedOut
+    # KKT: lambda_i g_i(x) ~ -1/t at the end, and stationarity
+    assert np.linalg.norm(O.pd_dual_residual(pb, pd.x, pd.lam)) < pars.tolSolver
+
+
+@pytest.mark.parametrize("spec", [Z.joptP2(), Z.rank_one_problem_simplex(10)], ids=lambda s: s["id"])
+def test_primal_dual_with_equalities_fails_like_the_reference(spec):
+    """solve_withEQs as written passes q = rhs1 + A'nu to KKTSystem (H dx + A'dnu = -q): the opposite sign of the
+    no-equality system (the reference marks it 'FIX ME', PrimalDualSolver.scala:284).  On the reference's own
+    equality-constrained known-answer problems its line search fails; the engine does not build this path
+    (CVXG_E_UNSUPPORTED)."""
+    pb = _problem(spec)
+    pars = O.standard_params()
+    x0 = O.with_feasible_point(pb, spec["x_where_defined"], pars)
+    with pytest.raises(O.LineSearchFailedException):
+        O.pd_solve_with_eqs(pb, x0, pars)
