@@ -168,3 +168,26 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_newtonDirection(JNIEnv* env, jcla
   (*env)->ReleasePrimitiveArrayCritical(env, x, px, JNI_ABORT);
   return rc;
 }
+
+/* pdSolve(h, maxIter, params[6], out[6]) -> PrimalDualSolver.solve on the device (cvxg_pd_solve) */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_pdSolve(JNIEnv* env, jclass cls, jlong h, jint maxIter, jdoubleArray jp,
+                                                       jdoubleArray out) {
+  (void)cls;
+  cvxg_params p;
+  cvxg_pd_solution s;
+  fill_params(env, jp, maxIter, &p);
+  jint rc = cvxg_pd_solve(CTX(h), &p, &s);
+  double o[6] = {s.duality_gap, s.norm_dual_residual, s.objective, (double)s.iter, (double)s.maxed_out,
+                 (double)s.newton_steps};
+  (*env)->SetDoubleArrayRegion(env, out, 0, 6, o);
+  return rc;
+}
+
+/* getLambda(h, lambda[m]) */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_getLambda(JNIEnv* env, jclass cls, jlong h, jdoubleArray lam) {
+  (void)cls;
+  double* pl = (*env)->GetPrimitiveArrayCritical(env, lam, 0);
+  jint rc = cvxg_get_lambda(CTX(h), pl);
+  (*env)->ReleasePrimitiveArrayCritical(env, lam, pl, 0);
+  return rc;
+}
