@@ -81,6 +81,7 @@ SIGNATURES = {
     "cvxg_set_objective_kl": (C.c_int, [_P, _D, C.c_int, C.c_int, C.c_int, _D, C.c_double]),
     "cvxg_set_ineq": (C.c_int, [_P, _D, C.c_int, C.c_int, _D, _D]),
     "cvxg_set_eq": (C.c_int, [_P, _D, C.c_int, C.c_int, _D]),
+    "cvxg_set_quad": (C.c_int, [_P, C.c_int, _I, _D, C.c_int]),
     "cvxg_set_x": (C.c_int, [_P, _D]),
     "cvxg_get_x": (C.c_int, [_P, _D]),
     "cvxg_barrier_eval": (C.c_int, [_P, C.c_double, _D, _D, _D, _D]),

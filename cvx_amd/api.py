@@ -172,6 +172,49 @@ class LinearConstraint:
         return self.ub - self.valueAt(x)
 
 
+class QuadraticConstraint(LinearConstraint):
+    """r + a'x + x'Px/2 <= ub (QuadraticConstraint.scala:8-63); P symmetric (checkSymmetric(P, 1e-13))."""
+
+    def __init__(self, id: str, dim: int, ub: float, r: float, a, P):
+        super().__init__(id, dim, ub, r, a)
+        P = np.asarray(P, dtype=np.float64)
+        if P.shape != (dim, dim):
+            raise ValueError(f"Matrix P must be square of dimension {dim} but is {P.shape[0]}x{P.shape[1]}")
+        if not np.sqrt(np.sum((P - P.T) ** 2)) < 1e-13:
+            raise ValueError("QuadraticConstraint: P not symmetric")
+        self.P = P
+
+    def valueAt(self, x):
+        return self.r + float(self.a @ x) + float(x @ (self.P @ x)) / 2
+
+    def gradientAt(self, x):
+        return self.a + self.P @ x
+
+    def hessianAt(self, x):
+        return self.P
+
+
+class Constraints:
+    """The constraint factories of Constraints.scala used by the reference's test problems."""
+
+    @staticmethod
+    def singleCoordinatePositive(n: int, j: int) -> LinearConstraint:
+        """Constraints.scala:26-35: -x_j <= 0."""
+        a = np.zeros(n)
+        a[j] = -1.0
+        return LinearConstraint(f"x_{j}>0", n, 0.0, 0.0, a)
+
+    @staticmethod
+    def allCoordinatesPositive(n: int) -> List[LinearConstraint]:
+        return [Constraints.singleCoordinatePositive(n, j) for j in range(n)]
+
+    @staticmethod
+    def oneHalfNorm2BoundedBy(n: int, ub: float) -> QuadraticConstraint:
+        """Constraints.scala:299-309: (x dot x)/2 <= ub (gradient x, Hessian I) — the QuadraticConstraint
+        (r = 0, a = 0, P = I): (x dot (I x))/2 is the same number."""
+        return QuadraticConstraint(f"x dot x <= {ub}", n, ub, 0.0, np.zeros(n), np.eye(n))
+
+
 class EqualityConstraint:
     """Ax = b with A p x n, p < n (EqualityConstraint.scala:16-27)."""
 
@@ -221,6 +264,13 @@ class ConstraintSet:
             A[i], r[i], ub[i] = c.a, c.r, c.ub
         return A, r, ub
 
+    def quadratic(self):
+        """(rows, P stack) of the QuadraticConstraint members in list order, or (None, None)."""
+        rows = [i for i, c in enumerate(self.constraints) if isinstance(c, QuadraticConstraint)]
+        if not rows:
+            return None, None
+        return np.array(rows, dtype=np.int32), np.stack([self.constraints[i].P for i in rows])
+
     def isSatisfiedStrictlyBy(self, x) -> bool:
         return all(c.isSatisfiedStrictly(x) for c in self.constraints)
 
@@ -247,12 +297,17 @@ class ConstraintSet:
         A1 = np.hstack([A, -np.ones((m, 1))])                 # g_j(x) - s <= ub_j  (Constraint.scala:64-89)
         a0 = np.zeros(n + 1)
         a0[n] = 1.0                                            # f(x,s) = s        (:129-140)
-        y0 = max(float(r[j] + A[j] @ x0) - ub[j] for j in range(m))
+        y0 = max(cnts[j].valueAt(x0) - ub[j] for j in range(m))
         fp = np.concatenate([x0, [1 + y0]])                    # feasible point    (:161-164)
+        qrows, qP = ConstraintSet(self.dim, cnts).quadratic()
         eng = Engine(n + 1, m, 0)
         try:
             eng.set_objective(a0, 0.0, None)
             eng.set_ineq(A1, r, ub)
+            if qrows is not None:  # Constraint.phase_I: hessianAt pads P with a zero row/column for s (:82-88)
+                qP1 = np.zeros((len(qrows), n + 1, n + 1))
+                qP1[:, :n, :n] = qP
+                eng.set_quad(qrows, qP1)
             eng.set_x(fp)
             eng.barrier_solve(pars, termination=1)             # phase_I_TerminationCriterion
             w = eng.get_x()
@@ -295,6 +350,9 @@ class GpuBarrierSolver:
         else:
             self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
         self.engine.set_ineq(A, r, ub)
+        qrows, qP = cnts.quadratic()
+        if qrows is not None:
+            self.engine.set_quad(qrows, qP)
         if p:
             self.engine.set_eq(eqs.A, eqs.b)
 
@@ -340,6 +398,8 @@ class GpuPrimalDualSolver:
             raise TypeError("GPU primal-dual engine: objective must be Quadratic- or LinearObjectiveFunction")
         if eqs is not None:
             raise TypeError("GPU primal-dual engine: equality constraints are not supported (solve_withEQs)")
+        if cnts.quadratic()[0] is not None:
+            raise TypeError("GPU primal-dual engine: LinearConstraint only")
         if cnts.feasiblePoint is None:
             raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
         self.objF, self.cnts, self.eqs, self.pars = objF, cnts, eqs, pars
@@ -454,7 +514,14 @@ def problem_from_spec(spec: dict):
     n = spec["a0"].shape[0]
     objF = (QuadraticObjectiveFunction(n, spec["r0"], spec["a0"], spec["P"]) if spec.get("P") is not None
             else LinearObjectiveFunction(n, spec["r0"], spec["a0"]))
-    cnts = [LinearConstraint(f"LinCnt{i}", n, spec["ub"][i], spec["r"][i], spec["A"][i]) for i in range(spec["A"].shape[0])]
+    qrows = [] if spec.get("qrows") is None else [int(v) for v in spec["qrows"]]
+    cnts = []
+    for i in range(spec["A"].shape[0]):
+        if i in qrows:
+            cnts.append(QuadraticConstraint(f"QuadCnt{i}", n, spec["ub"][i], spec["r"][i], spec["A"][i],
+                                            spec["qP"][qrows.index(i)]))
+        else:
+            cnts.append(LinearConstraint(f"LinCnt{i}", n, spec["ub"][i], spec["r"][i], spec["A"][i]))
     cs = ConstraintSet(n, cnts, spec.get("x_where_defined", spec.get("x0")))
     eqs = EqualityConstraint(spec["Aeq"], spec["beq"]) if spec.get("Aeq") is not None else None
     return objF, cs, eqs
@@ -462,6 +529,6 @@ def problem_from_spec(spec: dict):
 
 __all__ = ["SolverParams", "Solution", "ObjectiveFunction", "QuadraticObjectiveFunction", "LinearObjectiveFunction",
            "DualKLObjectiveFunction", "Dist_KL",
-           "LinearConstraint", "EqualityConstraint", "ConstraintSet", "GpuBarrierSolver", "BarrierSolver",
+           "LinearConstraint", "QuadraticConstraint", "Constraints", "EqualityConstraint", "ConstraintSet", "GpuBarrierSolver", "BarrierSolver",
            "GpuPrimalDualSolver", "PrimalDualSolver",
            "OptimizationProblem", "problem_from_spec", "CvxgError", "NotStrictlyFeasible"]

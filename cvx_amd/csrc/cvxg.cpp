@@ -84,6 +84,12 @@ struct cvxg_ctx {
   double* sp_coef = nullptr;
   int kl_nsplit = 1;            // K split of the KL SYRK's tail tiles over the outcomes
   double* kl_spart = nullptr;   // its partials
+  // QuadraticConstraint rows (cvxg_set_quad): row qrows[k] of A holds a_k, P_k stacked in Pq ((nq np) x np)
+  int nq = 0;
+  std::vector<int> qrows_h;
+  std::vector<char> is_quad;     // per constraint row
+  int *qrows = nullptr, *qslot = nullptr;  // device: row of constraint k, its row in As
+  double *Pq = nullptr, *qPx = nullptr, *qPs = nullptr, *qextra = nullptr, *qf = nullptr;
   // primal-dual solver state (PrimalDualSolver.scala; allocated on first use)
   double *lam = nullptr, *dlam = nullptr, *pd_rc = nullptr, *pd_w = nullptr;  // mp
   double *pd_rhs = nullptr, *pd_d1 = nullptr, *pd_R0 = nullptr, *pd_R1 = nullptr, *pd_tmp = nullptr;  // np
@@ -377,14 +383,25 @@ static double objective_from_ctrl(const cvxg_ctx* ctx, const DevCtrl& h) {
   return ctx->r0 + h.sc[SC_A0X] + (ctx->hasP ? h.sc[SC_XPX] / 2 : 0.0);
 }
 
+// c = g(x), d, 1/d, 1/d^2, log d at ctx->x; QuadraticConstraint rows add x'P_k x / 2 (P_k x kept in qPx for the
+// gradient, the Hessian rows and the line search).
+static void constraint_eval_all(cvxg_ctx* ctx) {
+  const int np = ctx->np;
+  if (ctx->nq > 0) {
+    launch_rowdot(ctx->s, ctx->Pq, np, ctx->nq * np, np, ctx->x, ctx->qPx);
+    launch_quad_xpx(ctx->s, ctx->qPx, ctx->x, ctx->qrows, ctx->nq, np, ctx->qextra);
+  }
+  launch_constraint_eval(ctx->s, ctx->A, np, ctx->mp, np, ctx->x, ctx->r, ctx->ub, ctx->c, ctx->d, ctx->invd, ctx->w,
+                         ctx->logd, ctx->ctrl, ctx->nq > 0 ? ctx->qextra : nullptr);
+}
+
 // Barrier value / gradient pieces at the current x and ctrl->t (BarrierSolver.scala:280-301):
 // c, d, w, invd, logd, Px, y, eqDiff, and sc[A0X, XPX, SUMLOG, GG, EQ2].
 static int eval_at_x(cvxg_ctx* ctx) {
   hipStream_t s = ctx->s;
   const int np = ctx->np, mp = ctx->mp;
   launch_ctrl_reset_eval(s, ctx->ctrl);
-  launch_constraint_eval(s, ctx->A, np, mp, np, ctx->x, ctx->r, ctx->ub, ctx->c, ctx->d, ctx->invd, ctx->w,
-                         ctx->logd, ctx->ctrl);
+  constraint_eval_all(ctx);
   const bool quad = ctx->hasP && !ctx->kl;
   if (quad) launch_rowdot(s, ctx->P, np, np, np, ctx->x, ctx->Px);
   if (ctx->kl) {  // v = B'z, y = R exp(-v), -B y (the KL dual gradient is w - B y), sum_j y_j
@@ -398,6 +415,7 @@ static int eval_at_x(cvxg_ctx* ctx) {
   launch_coldot_partials(s, ctx->A, np, mp, np, ctx->invd, ctx->part);
   launch_gradient_finalize(s, ctx->a0, quad ? ctx->Px : (ctx->kl ? ctx->kl_negBy : nullptr), ctx->part,
                            coldot_chunks(mp), np, ctx->ctrl, ctx->y);
+  if (ctx->nq > 0) launch_quad_grad(s, ctx->qPx, ctx->invd, ctx->qrows, ctx->nq, np, ctx->y);  // + (P_k x)/d_k
   launch_dot(s, ctx->a0, ctx->x, np, ctx->ctrl, SC_A0X);
   if (quad) launch_dot(s, ctx->x, ctx->Px, np, ctx->ctrl, SC_XPX);
   launch_sum(s, ctx->logd, mp, ctx->ctrl, SC_SUMLOG);
@@ -444,6 +462,8 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr) {
   const double* w = wsrc;
   int rows = ctx->mp;
   if (ctx->have_sparse) {  // dense rows only; the sparse rows' entries are added below
+    if (ctx->nq > 0)  // gradient rows G_k = a_k + P_k x of the quadratic constraints
+      launch_quad_rows(ctx->s, ctx->A, ctx->qPx, ctx->qrows, ctx->qslot, ctx->nq, ctx->np, ctx->As);
     launch_gather_w(ctx->s, wsrc, ctx->didx, ctx->ndense, ctx->mdp, ctx->wd);
     A = ctx->As;
     w = ctx->wd;
@@ -458,6 +478,8 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr) {
                          ctx->part);
   if (ctx->have_sparse)
     launch_sparse_hess(ctx->s, ctx->sp_ptr, ctx->sp_pq, ctx->sp_row, ctx->sp_coef, wsrc, ctx->sp_T, ctx->H, ctx->np);
+  if (ctx->nq > 0)  // + hessianAt/d = P_k / d_k  (BarrierSolver.scala:314)
+    launch_quad_hess(ctx->s, ctx->Pq, ctx->invd, ctx->qrows, ctx->nq, ctx->np, ctx->H);
   tstop(ctx, 5);
   HIPC(ctx, hipGetLastError());
   return CVXG_OK;
@@ -819,7 +841,8 @@ static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch
     HIPC(ctx, hipMemcpyAsync(b->kl, ctx->kl_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
   }
   const int nb = ls_blocks(ctx->m);
-  launch_ls_trials(ctx->s, ctx->c, ctx->e, ctx->ub, ctx->m, tbase, beta, ctx->ls_plog, ctx->ls_pcnt);
+  launch_ls_trials(ctx->s, ctx->c, ctx->e, ctx->ub, ctx->m, tbase, beta, ctx->ls_plog, ctx->ls_pcnt,
+                   ctx->nq > 0 ? ctx->qf : nullptr);
   launch_ls_finalize(ctx->s, ctx->ls_plog, ctx->ls_pcnt, nb, ctx->ls_log, ctx->ls_cnt);
   HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipMemcpyAsync(ctx->hls, ctx->ls_log, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
@@ -844,6 +867,10 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
   const double beta = pars->beta, alpha = pars->alpha;
   // e = A s, and the quadratic pieces of f0(x + s t)
   if (ctx->m > 0) launch_rowdot(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e);
+  if (ctx->nq > 0) {  // e_k = G_k.s and f_k = s'P_k s: g_k(x + t s) = g_k + t e_k + t^2 f_k / 2
+    launch_rowdot(s, ctx->Pq, ctx->np, ctx->nq * ctx->np, ctx->np, ctx->sdir, ctx->qPs);
+    launch_quad_ls(s, ctx->qPx, ctx->qPs, ctx->sdir, ctx->qrows, ctx->nq, ctx->np, ctx->e, ctx->qf);
+  }
   launch_dot(s, ctx->a0, ctx->sdir, ctx->np, ctx->ctrl, SC_A0S);
   if (ctx->kl) launch_rowdot(s, ctx->KB, ctx->np, ctx->noutp, ctx->np, ctx->sdir, ctx->kl_u);  // u = B's
   const bool quad = ctx->hasP && !ctx->kl;
@@ -1057,7 +1084,8 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->kl_negBy, ctx->kl_part, ctx->kl_ls, ctx->As, ctx->wd, ctx->didx, ctx->sp_ptr,
                   ctx->sp_pq, ctx->sp_row, ctx->sp_coef, ctx->kl_spart, ctx->lam, ctx->dlam, ctx->pd_rc,
                   ctx->pd_w, ctx->pd_rhs, ctx->pd_d1, ctx->pd_R0, ctx->pd_R1, ctx->pd_tmp, ctx->pd_part_rows,
-                  ctx->pd_part_cols, ctx->pd_out};
+                  ctx->pd_part_cols, ctx->pd_out, ctx->qrows, ctx->qslot, ctx->Pq, ctx->qPx, ctx->qPs,
+                  ctx->qextra, ctx->qf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
@@ -1145,7 +1173,7 @@ static int plan_sparse_rows(cvxg_ctx* ctx, const double* A, int ldA, int row_maj
   ctx->have_sparse = 0;
   ctx->sp_T = 0;
   ctx->nsplit = syrk_nsplit(ctx, ctx->mp / KC);
-  if (!ctx->sparse_rows) return CVXG_OK;
+  if (!ctx->sparse_rows && ctx->nq == 0) return CVXG_OK;
   auto at = [&](int i, int j) { return row_major ? A[(size_t)i * ldA + j] : A[(size_t)j * ldA + i]; };
   struct Term {
     int p, q, row;
@@ -1165,14 +1193,14 @@ static int plan_sparse_rows(cvxg_ctx* ctx, const double* A, int ldA, int row_maj
         nzv.push_back(v);
       }
     }
-    if ((int)nzc.size() > SPARSE_NNZ) {
-      dense.push_back(i);
+    if (!ctx->sparse_rows || (int)nzc.size() > SPARSE_NNZ || (!ctx->is_quad.empty() && ctx->is_quad[i])) {
+      dense.push_back(i);  // QuadraticConstraint rows are always dense: their SYRK row G = a + P x changes with x
       continue;
     }
     for (size_t a = 0; a < nzc.size(); ++a)  // lower entries: p = nzc[a] >= q = nzc[b]
       for (size_t b = 0; b <= a; ++b) terms.push_back({nzc[a], nzc[b], i, nzv[a] * nzv[b]});
   }
-  if ((int)dense.size() == m) return CVXG_OK;  // no sparse rows: the SYRK keeps using A itself
+  if ((int)dense.size() == m && ctx->nq == 0) return CVXG_OK;  // no sparse rows: the SYRK keeps using A itself
   std::stable_sort(terms.begin(), terms.end(),
                    [](const Term& x, const Term& y) { return x.p != y.p ? x.p < y.p : x.q < y.q; });
   std::vector<int> ptr, pq, row;
@@ -1211,6 +1239,14 @@ static int plan_sparse_rows(cvxg_ctx* ctx, const double* A, int ldA, int row_maj
     CHK(copy_sync(ctx, ctx->sp_row, row.data(), row.size() * sizeof(int), hipMemcpyHostToDevice));
     CHK(copy_sync(ctx, ctx->sp_coef, coef.data(), coef.size() * sizeof(double), hipMemcpyHostToDevice));
   }
+  if (ctx->nq > 0) {  // As row of each quadratic constraint
+    std::vector<int> slot(ctx->nq);
+    for (int k = 0; k < ctx->nq; ++k)
+      slot[k] = (int)(std::lower_bound(dense.begin(), dense.end(), ctx->qrows_h[k]) - dense.begin());
+    if (ctx->qslot) (void)hipFree(ctx->qslot);
+    CHK(dalloc(ctx, &ctx->qslot, ctx->nq));
+    CHK(copy_sync(ctx, ctx->qslot, slot.data(), slot.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
   ctx->have_sparse = 1;
   ctx->nsplit = syrk_nsplit(ctx, ctx->mdp / KC);
   return CVXG_OK;
@@ -1228,9 +1264,49 @@ int cvxg_set_ineq(cvxg_ctx* ctx, const double* A, int ldA, int row_major, const 
     memcpy(uu.data(), ub, m * sizeof(double));
     CHK(copy_sync(ctx, ctx->r, rr.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
     CHK(copy_sync(ctx, ctx->ub, uu.data(), ctx->mp * sizeof(double), hipMemcpyHostToDevice));
+    ctx->nq = 0;  // a new constraint list: quadratic rows are declared again with cvxg_set_quad
+    ctx->is_quad.clear();
     CHK(plan_sparse_rows(ctx, A, ldA, row_major));
   }
   ctx->have_ineq = 1;
+  ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+int cvxg_set_quad(cvxg_ctx* ctx, int q, const int* rows, const double* P, int ldP) {
+  if (!ctx || q < 0 || (q > 0 && (!rows || !P))) return CVXG_E_ARG;
+  if (!ctx->have_ineq) return set_err(ctx, CVXG_E_ARG, "cvxg_set_quad: call cvxg_set_ineq first");
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  const int n = ctx->n, m = ctx->m;
+  const size_t np = ctx->np;
+  if (ldP < n) return set_err(ctx, CVXG_E_DIM, "ldP too small");
+  std::vector<int> rs(rows, rows + q);
+  for (int k = 0; k < q; ++k) {
+    if (rs[k] < 0 || rs[k] >= m) return set_err(ctx, CVXG_E_DIM, "quadratic constraint row %d out of range", rs[k]);
+    if (k > 0 && rs[k] <= rs[k - 1]) return set_err(ctx, CVXG_E_ARG, "quadratic constraint rows must ascend");
+  }
+  for (double** v : {&ctx->Pq, &ctx->qPx, &ctx->qPs, &ctx->qextra, &ctx->qf})
+    if (*v) (void)hipFree(*v), *v = nullptr;
+  if (ctx->qrows) (void)hipFree(ctx->qrows), ctx->qrows = nullptr;
+  ctx->nq = q;
+  ctx->qrows_h = rs;
+  ctx->is_quad.assign(m, 0);
+  for (int r : rs) ctx->is_quad[r] = 1;
+  if (q > 0) {
+    CHK(dalloc(ctx, &ctx->Pq, (size_t)q * np * np));
+    for (int k = 0; k < q; ++k)
+      CHK(upload_mat(ctx, ctx->Pq + (size_t)k * np * np, (int)np, (int)np, P + (size_t)k * n * ldP, n, n, ldP, 1));
+    CHK(dalloc(ctx, &ctx->qrows, q));
+    CHK(copy_sync(ctx, ctx->qrows, rs.data(), q * sizeof(int), hipMemcpyHostToDevice));
+    CHK(dalloc(ctx, &ctx->qPx, (size_t)q * np));
+    CHK(dalloc(ctx, &ctx->qPs, (size_t)q * np));
+    CHK(dalloc(ctx, &ctx->qextra, ctx->mp));  // zero on the linear rows
+    CHK(dalloc(ctx, &ctx->qf, ctx->mp));
+  }
+  // re-split the rows (quadratic rows are dense SYRK rows with a changing gradient): A back from the device
+  std::vector<double> hA((size_t)ctx->mp * np);
+  CHK(copy_sync(ctx, hA.data(), ctx->A, hA.size() * sizeof(double), hipMemcpyDeviceToHost));
+  CHK(plan_sparse_rows(ctx, hA.data(), (int)np, 1));
   ctx->x_eval_valid = 0;
   return CVXG_OK;
 }
@@ -1302,8 +1378,7 @@ int cvxg_constraint_values(cvxg_ctx* ctx, const double* x, double* gx) {
   HIPC(ctx, hipSetDevice(ctx->dev));
   CHK(cvxg_set_x(ctx, x));
   launch_ctrl_reset_eval(ctx->s, ctx->ctrl);
-  launch_constraint_eval(ctx->s, ctx->A, ctx->np, ctx->mp, ctx->np, ctx->x, ctx->r, ctx->ub, ctx->c, ctx->d,
-                         ctx->invd, ctx->w, ctx->logd, ctx->ctrl);
+  constraint_eval_all(ctx);
   HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipMemcpyAsync(gx, ctx->c, ctx->m * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
   HIPC(ctx, hipStreamSynchronize(ctx->s));
@@ -1525,6 +1600,7 @@ static int pd_check(cvxg_ctx* ctx) {
                    "PrimalDualSolver.solve_withEQs is not built (its KKT right-hand side has the opposite sign of "
                    "the no-equality system, PrimalDualSolver.scala:284)");
   if (ctx->kl) return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: quadratic or linear objective only");
+  if (ctx->nq > 0) return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: linear constraints only");
   if (ctx->m == 0) return set_err(ctx, CVXG_E_ARG, "primal-dual solver needs inequality constraints");
   if (ctx->lam) return CVXG_OK;
   const size_t np = ctx->np, mp = ctx->mp;

@@ -42,13 +42,14 @@ __global__ __launch_bounds__(256) void k_constraint_eval(const double* __restric
                                                          const double* __restrict__ ub, double* __restrict__ c,
                                                          double* __restrict__ d, double* __restrict__ invd,
                                                          double* __restrict__ w, double* __restrict__ logd,
-                                                         DevCtrl* ctrl) {
+                                                         DevCtrl* ctrl, const double* __restrict__ extra) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= mp) return;
   const double dot = row_dot_wave(A + (size_t)row * ld, x, cols, lane);
   if (lane == 0) {
-    const double ci = r[row] + dot;          // r + (a dot x)          LinearConstraint.scala:23
+    // r + (a dot x)  (LinearConstraint.scala:23), + (x dot P x)/2 for a QuadraticConstraint row (:31)
+    const double ci = extra ? (r[row] + dot) + extra[row] : r[row] + dot;
     const double di = ub[row] - ci;          // d = ub - valueAt(x)    BarrierSolver.scala:283
     c[row] = ci;
     d[row] = di;
@@ -62,8 +63,8 @@ __global__ __launch_bounds__(256) void k_constraint_eval(const double* __restric
 
 void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int n_cols, const double* x,
                             const double* r, const double* ub, double* c, double* d, double* invd,
-                            double* w, double* logd, DevCtrl* ctrl) {
-  k_constraint_eval<<<(mp + 3) / 4, 256, 0, s>>>(A, ld, mp, n_cols, x, r, ub, c, d, invd, w, logd, ctrl);
+                            double* w, double* logd, DevCtrl* ctrl, const double* extra) {
+  k_constraint_eval<<<(mp + 3) / 4, 256, 0, s>>>(A, ld, mp, n_cols, x, r, ub, c, d, invd, w, logd, ctrl, extra);
 }
 
 __global__ __launch_bounds__(256) void k_rowdot(const double* __restrict__ M, int ld, int rows, int cols,
@@ -452,7 +453,8 @@ int ls_blocks(int m) { return (m + 255) / 256; }
 
 __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c, const double* __restrict__ e,
                                                    const double* __restrict__ ub, int m, double tbase, double beta,
-                                                   double* __restrict__ part_log, int* __restrict__ part_cnt) {
+                                                   double* __restrict__ part_log, int* __restrict__ part_cnt,
+                                                   const double* __restrict__ f) {
   __shared__ double slog[4][LS_TRIALS];
   __shared__ int sviol[4][LS_TRIALS];
   __shared__ int snpos[4][LS_TRIALS];
@@ -460,9 +462,10 @@ __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c,
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool valid = i < m;
   const double ci = valid ? c[i] : 0.0, ei = valid ? e[i] : 0.0, ubi = valid ? ub[i] : 1.0;
+  const double fi = (valid && f) ? f[i] : 0.0;  // s'P s of a QuadraticConstraint row (0: linear)
   double t = tbase;
   for (int k = 0; k < LS_TRIALS; ++k) {
-    const double g = ci + t * ei;
+    const double g = f ? (ci + t * ei) + (t * t * fi) / 2 : ci + t * ei;
     const double dd = ubi - g;
     const bool viol = valid && !(g * (1 + 3e-16) < ubi);   // Constraint.scala:23
     const bool npos = valid && !(dd > 0.0);                 // BarrierSolver.scala:284
@@ -493,8 +496,8 @@ __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c,
 }
 
 void launch_ls_trials(hipStream_t s, const double* c, const double* e, const double* ub, int m, double tbase,
-                      double beta, double* part_log, int* part_cnt) {
-  k_ls_trials<<<ls_blocks(m), 256, 0, s>>>(c, e, ub, m, tbase, beta, part_log, part_cnt);
+                      double beta, double* part_log, int* part_cnt, const double* f) {
+  k_ls_trials<<<ls_blocks(m), 256, 0, s>>>(c, e, ub, m, tbase, beta, part_log, part_cnt, f);
 }
 
 // KL dual objective along the trial steps: per trial k, sum_j R exp(-(v_j + t_k u_j)) (v = B'z, u = B's),

@@ -17,7 +17,7 @@ struct TileList {
 // Constraint.scala:23).
 void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int n_cols, const double* x,
                             const double* r, const double* ub, double* c, double* d, double* invd,
-                            double* w, double* logd, DevCtrl* ctrl);
+                            double* w, double* logd, DevCtrl* ctrl, const double* extra = nullptr);
 // y = M v (row-major, one wave per row); rows, cols multiples of 128 / any.
 void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y);
 // part[chunk][j] = sum_{i in chunk} M[i][j] v[i]  (chunks of COLDOT_ROWS rows; rows % 64 == 0)
@@ -53,6 +53,18 @@ void launch_set_diag(hipStream_t s, double* H, int ld, int n, const double* diag
 void launch_sparse_hess(hipStream_t s, const int* ptr, const int* pq, const int* row, const double* coef,
                         const double* w, int T, double* H, int ld);
 void launch_gather_w(hipStream_t s, const double* w, const int* idx, int nd, int ndp, double* wd);
+
+// ---- QuadraticConstraint rows (k_quad.hip) ------------------------------------------------------------
+void launch_quad_xpx(hipStream_t s, const double* qPx, const double* x, const int* qrows, int nq, int np,
+                     double* extra);
+void launch_quad_grad(hipStream_t s, const double* qPx, const double* invd, const int* qrows, int nq, int np,
+                      double* y);
+void launch_quad_rows(hipStream_t s, const double* A, const double* qPx, const int* qrows, const int* qslot, int nq,
+                      int np, double* As);
+void launch_quad_hess(hipStream_t s, const double* Pq, const double* invd, const int* qrows, int nq, int np,
+                      double* H);
+void launch_quad_ls(hipStream_t s, const double* qPx, const double* qPs, const double* sdir, const int* qrows, int nq,
+                    int np, double* e, double* f);
 
 // ---- primal-dual iteration pieces (k_pd.hip) ---------------------------------------------------------
 void launch_pd_rhs(hipStream_t s, const double* y, double t, int n, int np, double* rhs);
@@ -103,7 +115,7 @@ void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* L
 // For trials k in [0, LS_TRIALS): t_k = tbase*beta^k; g_i = c_i + t_k e_i; per-block partials of
 // (#violations of g*(1+3e-16)<ub, #(ub-g<=0), sum log(ub-g)).
 void launch_ls_trials(hipStream_t s, const double* c, const double* e, const double* ub, int m, double tbase,
-                      double beta, double* part_log, int* part_cnt);
+                      double beta, double* part_log, int* part_cnt, const double* f = nullptr);
 void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_cnt, int nblocks,
                         double* out_log, int* out_cnt);
 int ls_blocks(int m);

@@ -105,6 +105,14 @@ class Engine:
         A, r, ub = _f64(A), _f64(r), _f64(ub)
         self._check(self.lib.cvxg_set_ineq(self.h, _dp(A), A.shape[1] if A.ndim == 2 else self.n, 1, _dp(r), _dp(ub)))
 
+    def set_quad(self, rows, P):
+        """QuadraticConstraint rows (cvxg_set_quad): rows ascending indices into the set_ineq list, P (q, n, n)."""
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        P = _f64(np.asarray(P).reshape(len(rows), self.n, self.n)) if len(rows) else np.zeros((0, self.n, self.n))
+        self._keep_quad = (rows, P)
+        self._check(self.lib.cvxg_set_quad(self.h, len(rows), rows.ctypes.data_as(C.POINTER(C.c_int)), _dp(P),
+                                           self.n))
+
     def set_eq(self, Aeq, beq):
         Aeq, beq = _f64(Aeq), _f64(beq)
         self._check(self.lib.cvxg_set_eq(self.h, _dp(Aeq), Aeq.shape[1], 1, _dp(beq)))
@@ -115,6 +123,8 @@ class Engine:
         else:
             self.set_objective(spec["a0"], spec.get("r0", 0.0), spec.get("P"))
         self.set_ineq(spec["A"], spec["r"], spec["ub"])
+        if spec.get("qrows") is not None and len(spec["qrows"]) > 0:
+            self.set_quad(spec["qrows"], spec["qP"])
         if self.p > 0:
             self.set_eq(spec["Aeq"], spec["beq"])
 

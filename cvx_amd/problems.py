@@ -149,6 +149,76 @@ def norm_squared_with_free_variables(dim: int) -> Dict:
                 ub=np.array([-1.0]), Aeq=None, beq=None, x_where_defined=np.ones(dim), x_opt=x_opt)
 
 
+# ---- problems with QuadraticConstraint rows (qrows index the (A, r, ub) rows; qP holds their P) -----------------
+
+def rank_one_problem_sphere(dim: int) -> Dict:
+    """SimpleOptimizationProblems.scala:266-300 — f = x'(aa')x/2, a = linspace(1,2,dim), constraints
+    oneHalfNorm2BoundedBy(dim, 1/2) :: allCoordinatesPositive(dim) (Constraints.scala:299-309, 26-69); x* = 0."""
+    a = np.linspace(1.0, 2.0, dim)
+    Ap, rp, ubp = _positivity(dim)
+    A = np.vstack([np.zeros((1, dim)), Ap])
+    return dict(id="Spherical rankOneProblem", a0=np.zeros(dim), r0=0.0, P=np.outer(a, a), A=A,
+                r=np.concatenate([[0.0], rp]), ub=np.concatenate([[0.5], ubp]), Aeq=None, beq=None,
+                qrows=np.array([0], dtype=np.int32), qP=np.eye(dim)[None], x_where_defined=np.full(dim, 1.0 / dim),
+                x_opt=np.zeros(dim))
+
+
+def jopt_p1(dim: int) -> Dict:
+    """SimpleOptimizationProblems.scala:347-377 — f = sum(x) s.t. (x.x)/2 <= 1/2; x* = -1/sqrt(dim)."""
+    return dict(id="f(x)=sum(x) with ||x||^2<=1", a0=np.ones(dim), r0=0.0, P=None, A=np.zeros((1, dim)),
+                r=np.zeros(1), ub=np.array([0.5]), Aeq=None, beq=None, qrows=np.array([0], dtype=np.int32),
+                qP=np.eye(dim)[None], x_where_defined=np.full(dim, 2.0), x_opt=-np.ones(dim) / np.sqrt(dim))
+
+
+def distance_from_origin(n: int, sliced: bool) -> Dict:
+    """SimpleOptimizationProblems.scala:464-561 — min ||x||^2/2 (ObjectiveFunctions.normSquared) over
+    x'x/2 - 2 x_n + 3/2 <= 0 (QuadraticConstraint(r = 1.5, a = -2 e_n, P = I)); distanceFromOrigin1 (sliced) adds
+    for every j the row -(e_j + e_n).x <= -1 twice (the reference builds lc2_j from -a again, not from b); x* = e_n."""
+    N = n + 1
+    e = np.zeros(N)
+    e[n] = 1.0
+    rows, r, ub = [-2.0 * e], [1.5], [0.0]
+    if sliced:
+        for j in range(n):
+            a = np.zeros(N)
+            a[j] = 1.0
+            a = a + e
+            rows += [-a, -a]
+            r += [0.0, 0.0]
+            ub += [-1.0, -1.0]
+    return dict(id="DistanceFromOrigin_1" if sliced else "DistanceFromOrigin_0", a0=np.zeros(N), r0=0.0,
+                P=np.eye(N), A=np.array(rows), r=np.array(r), ub=np.array(ub), Aeq=None, beq=None,
+                qrows=np.array([0], dtype=np.int32), qP=np.eye(N)[None], x_where_defined=np.zeros(N), x_opt=e.copy())
+
+
+def random_qp_quad(n: int, m: int, q: int, instance: int = 0) -> Dict:
+    """random_qp plus q random convex QuadraticConstraint rows x'P_k x/2 + a_k.x <= ub_k (P_k = R'R/n, a_k small),
+    interleaved with the linear rows; x0 = 0 stays strictly feasible (ub_k > 0)."""
+    spec = random_qp(n, m, instance)
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 31337 + instance))
+    qP = np.empty((q, n, n))
+    qa = np.empty((q, n))
+    for k in range(q):
+        R = rng.uniform(-1.0, 1.0, size=(n, n))
+        Pk = (R.T @ R) / n
+        qP[k] = 0.5 * (Pk + Pk.T)
+        qa[k] = 0.1 * rng.uniform(-1.0, 1.0, size=n)
+    qrows = np.sort(rng.choice(m + q, size=q, replace=False)).astype(np.int32)
+    A = np.zeros((m + q, n))
+    ub = np.zeros(m + q)
+    lin = [i for i in range(m + q) if i not in set(qrows.tolist())]
+    A[lin], ub[lin] = spec["A"], spec["ub"]
+    A[qrows], ub[qrows] = qa, rng.uniform(0.5, 1.0, size=q)
+    spec.update(id=f"random_qp_quad(n={n},m={m},q={q},instance={instance})", A=A, ub=ub, r=np.zeros(m + q),
+                qrows=qrows, qP=qP)
+    return spec
+
+
+def known_answer_zoo_quadratic():
+    """The SimpleOptimizationProblems.standardProblems members with a quadratic constraint."""
+    return [rank_one_problem_sphere(10), jopt_p1(5), distance_from_origin(4, False), distance_from_origin(4, True)]
+
+
 def known_answer_zoo():
     """The SimpleOptimizationProblems.standardProblems subset (:576-598) the linear engine covers."""
     return [joptP2(), rank_one_problem_simplex(10), probability_simplex_problem(10),

@@ -120,6 +120,13 @@ int cvxg_set_objective_kl(cvxg_ctx* ctx, const double* B, int ldB, int row_major
 int cvxg_set_ineq(cvxg_ctx* ctx, const double* A, int ldA, int row_major, const double* r,
                   const double* ub);
 
+/* QuadraticConstraint(id, dim, ub, r, a, P): r + a.x + x'P x / 2 <= ub (QuadraticConstraint.scala:8-40).  Row
+ * rows[k] (ascending) of the cvxg_set_ineq list holds its (a, r, ub); P_k is the n x n row-major block at
+ * P + k n ldP (symmetric).  Call after cvxg_set_ineq (which clears the quadratic rows).  The barrier path
+ * (value, gradient a + P x, Hessian terms G G'/d^2 + P/d, line search) handles them; the primal-dual solver
+ * returns CVXG_E_UNSUPPORTED. */
+int cvxg_set_quad(cvxg_ctx* ctx, int q, const int* rows, const double* P, int ldP);
+
 /* EqualityConstraint(A, b) (EqualityConstraint.scala:16). */
 int cvxg_set_eq(cvxg_ctx* ctx, const double* Aeq, int ldAeq, int row_major, const double* beq);
 

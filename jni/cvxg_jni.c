@@ -191,3 +191,15 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_getLambda(JNIEnv* env, jclass cls
   (*env)->ReleasePrimitiveArrayCritical(env, lam, pl, 0);
   return rc;
 }
+
+/* setQuad(h, q, rows[q], P[q n n] row-major, ldP) -> QuadraticConstraint rows (cvxg_set_quad) */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_setQuad(JNIEnv* env, jclass cls, jlong h, jint q, jintArray rows,
+                                                       jdoubleArray P, jint ldP) {
+  (void)cls;
+  jint* pr = (*env)->GetPrimitiveArrayCritical(env, rows, 0);
+  double* pp = (*env)->GetPrimitiveArrayCritical(env, P, 0);
+  jint rc = cvxg_set_quad(CTX(h), q, (const int*)pr, pp, ldP);
+  (*env)->ReleasePrimitiveArrayCritical(env, P, pp, JNI_ABORT);
+  (*env)->ReleasePrimitiveArrayCritical(env, rows, pr, JNI_ABORT);
+  return rc;
+}

@@ -115,6 +115,16 @@ class Problem:
     # w = a0 and R = kl_R:  f(z) = w.z + R.exp(-B'z),  grad = w - B(R o exp(-B'z)),  Hessian = B diag(y) B'.
     kl_B: Optional[np.ndarray] = None
     kl_R: Optional[np.ndarray] = None
+    # QuadraticConstraint rows (QuadraticConstraint.scala:8-40): row qrows[k] of (A, r, ub) holds (a, r, ub) of
+    # r + a'x + x'P_k x / 2 <= ub with P_k = qP[k]
+    qrows: Optional[np.ndarray] = None
+    qP: Optional[np.ndarray] = None
+
+    def quad_index(self, i: int) -> int:
+        if self.qrows is None:
+            return -1
+        hit = np.nonzero(self.qrows == i)[0]
+        return int(hit[0]) if hit.size else -1
 
     @property
     def n(self) -> int:
@@ -165,8 +175,23 @@ def objective_hessian(pb: Problem, x: Optional[np.ndarray] = None) -> np.ndarray
 
 
 def constraint_value(pb: Problem, i: int, x: np.ndarray) -> float:
-    """LinearConstraint.scala:22-24 — r + (a dot x)."""
+    """LinearConstraint.scala:22-24 — r + (a dot x); QuadraticConstraint.scala:30-32 — r + (a dot x) + (x dot (P*x))/2."""
+    k = pb.quad_index(i)
+    if k >= 0:
+        return pb.r[i] + float(np.dot(pb.A[i], x)) + float(np.dot(x, pb.qP[k] @ x)) / 2
     return pb.r[i] + float(np.dot(pb.A[i], x))
+
+
+def constraint_gradient(pb: Problem, i: int, x: np.ndarray) -> np.ndarray:
+    """LinearConstraint.gradientAt = a; QuadraticConstraint.gradientAt = a + P*x (QuadraticConstraint.scala:34-36)."""
+    k = pb.quad_index(i)
+    return pb.A[i] + pb.qP[k] @ x if k >= 0 else pb.A[i]
+
+
+def constraint_hessian(pb: Problem, i: int) -> Optional[np.ndarray]:
+    """QuadraticConstraint.hessianAt = P; None for a LinearConstraint (its zeros(n,n) adds exact zeros)."""
+    k = pb.quad_index(i)
+    return pb.qP[k] if k >= 0 else None
 
 
 def is_satisfied_strictly(pb: Problem, i: int, x: np.ndarray) -> bool:
@@ -184,7 +209,7 @@ def is_in_set(pb: Problem, x: np.ndarray) -> bool:
 
 def active_set(pb: Problem, x: np.ndarray, tol: float = 1e-12) -> np.ndarray:
     """Constraint.scala:26 isActive — |g_i(x) - ub_i| < tol (never called by the reference)."""
-    g = pb.r + pb.A @ x
+    g = np.array([constraint_value(pb, i, x) for i in range(pb.m)])
     return np.nonzero(np.abs(g - pb.ub) < tol)[0]
 
 
@@ -211,7 +236,7 @@ def barrier_gradient(pb: Problem, t: float, x: np.ndarray) -> np.ndarray:
         d = pb.ub[i] - constraint_value(pb, i, x)
         if d <= 0:
             raise NotStrictlyFeasible(f"gradientBarrierFunction: x not strictly feasible, d = {d}")
-        s = s + pb.A[i] / d
+        s = s + constraint_gradient(pb, i, x) / d
     return s
 
 
@@ -229,9 +254,12 @@ def barrier_hessian(pb: Problem, t: float, x: np.ndarray, literal: bool = True) 
         d = pb.ub[i] - constraint_value(pb, i, x)
         if d <= 0:
             raise NotStrictlyFeasible(f"hessianBarrierFunction: x not strictly feasible, d = {d}")
-        G = pb.A[i]
+        G = constraint_gradient(pb, i, x)
         GGt = np.outer(G, G)
-        if literal:
+        Hq = constraint_hessian(pb, i)
+        if Hq is not None:
+            s = s + GGt / (d * d) + Hq / d
+        elif literal:
             Hc = np.zeros((n, n))
             s = s + GGt / (d * d) + Hc / d
         else:
@@ -724,7 +752,11 @@ def phase_I_problem(pb: Problem, x_where_defined: np.ndarray) -> Tuple[Problem, 
     a0[n] = 1.0
     y0 = max(constraint_value(pb, j, x_where_defined) - pb.ub[j] for j in range(m))
     fp = np.concatenate([x_where_defined, [1 + y0]])
-    return Problem(a0=a0, r0=0.0, P=None, A=A1, r=pb.r.copy(), ub=pb.ub.copy()), fp
+    qP = None
+    if pb.qrows is not None:  # hessianAt of the phase-I constraint: P in the x block, zero row/column for s
+        qP = np.zeros((pb.qP.shape[0], n + 1, n + 1))
+        qP[:, :n, :n] = pb.qP
+    return Problem(a0=a0, r0=0.0, P=None, A=A1, r=pb.r.copy(), ub=pb.ub.copy(), qrows=pb.qrows, qP=qP), fp
 
 
 def phase_I_analysis(pb: Problem, x_where_defined: np.ndarray, pars: SolverParams):
@@ -737,9 +769,10 @@ def phase_I_analysis(pb: Problem, x_where_defined: np.ndarray, pars: SolverParam
         for i in range(pb.Aeq.shape[0]):
             rowsA.append(pb.Aeq[i:i + 1]); rowsr.append(np.zeros(1)); rowsub.append(np.array([pb.beq[i] + tolEqs]))
             rowsA.append(-pb.Aeq[i:i + 1]); rowsr.append(np.zeros(1)); rowsub.append(np.array([-pb.beq[i] + tolEqs]))
-        base = Problem(a0=pb.a0, A=np.vstack(rowsA), r=np.concatenate(rowsr), ub=np.concatenate(rowsub))
+        base = Problem(a0=pb.a0, A=np.vstack(rowsA), r=np.concatenate(rowsr), ub=np.concatenate(rowsub),
+                       qrows=pb.qrows, qP=pb.qP)
     else:
-        base = Problem(a0=pb.a0, A=pb.A, r=pb.r, ub=pb.ub)
+        base = Problem(a0=pb.a0, A=pb.A, r=pb.r, ub=pb.ub, qrows=pb.qrows, qP=pb.qP)
     p1, fp = phase_I_problem(base, x_where_defined)
     sol = barrier_solve(p1, fp, pars, tc=phase_I_termination)
     n = pb.n

@@ -553,3 +553,71 @@ def test_pd_with_equalities_is_unsupported(mods):
     with pytest.raises(CvxgError):
         eng.pd_solve(SP.standardParams())
     eng.close()
+
+
+# ---- QuadraticConstraint rows (QuadraticConstraint.scala) in the barrier path -------------------------------------
+
+def _qopb(O, spec):
+    return O.Problem(a0=spec["a0"], r0=float(spec["r0"]), P=spec.get("P"), A=spec["A"], r=spec["r"], ub=spec["ub"],
+                     qrows=spec["qrows"], qP=spec["qP"])
+
+
+@pytest.mark.parametrize("n,m,q", [(40, 60, 3), (300, 400, 2)])
+def test_quadratic_constraints_oracles_and_direction(mods, n, m, q):
+    """Barrier value / gradient / Hessian with quadratic rows (G = a + P x, + P/d) vs the oracle (1e-12), exact
+    symmetry, the constraint values, and the Newton direction within 1e-8."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp_quad(n, m, q, instance=7)
+    pb = _qopb(O, spec)
+    eng = _engine(Engine, spec)
+    pars = SP.standardParams()
+    rng = np.random.default_rng(9)
+    x = 1e-3 * rng.uniform(-1, 1, n) / np.sqrt(n)
+    g_ref = np.array([O.constraint_value(pb, i, x) for i in range(pb.m)])
+    np.testing.assert_allclose(eng.constraint_values(x), g_ref, rtol=1e-13, atol=1e-15)
+    for t in (1.0, 1e2, 1e4):
+        f, g, H = eng.barrier_eval(t, x, want_grad=True, want_hess=True)
+        assert abs(f - O.barrier_value(pb, t, x)) <= 1e-12 * max(1.0, abs(f))
+        gr = O.barrier_gradient(pb, t, x)
+        assert np.linalg.norm(g - gr) <= 1e-12 * np.linalg.norm(gr)
+        Hr = O.barrier_hessian(pb, t, x, literal=False)
+        assert np.linalg.norm(H - Hr) <= 1e-12 * np.linalg.norm(Hr)
+        assert np.array_equal(H, H.T)
+        dx, _, info = eng.newton_direction(pars, t, x, grad=gr)
+        rec = O.NewtonStepRecord(x=x, grad=gr, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
+        dref = O.newton_direction(pb, t, x, gr, pars.tolEqSolve, rec)
+        assert np.linalg.norm(dx - dref) <= 1e-8 * np.linalg.norm(dref), t
+    eng.close()
+
+
+def test_quadratic_constraints_barrier_solve(mods):
+    """A whole barrier solve with quadratic rows (one of them active at the optimum): the oracle's x, gap < tol."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp_quad(40, 80, 3, instance=1)
+    pars = SP.standardParams()
+    eng = _engine(Engine, spec)
+    eng.set_x(spec["x0"])
+    sol = eng.barrier_solve(pars, termination=0)
+    x = eng.get_x()
+    eng.close()
+    ref = O.barrier_solve(_qopb(O, spec), spec["x0"], pars)
+    assert np.linalg.norm(x - ref.x) <= 1e-6 * max(1.0, np.linalg.norm(ref.x))
+    assert sol.duality_gap < pars.tolSolver
+    assert abs(sol.newton_steps - ref.newton_steps) <= max(2, int(0.05 * ref.newton_steps))
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2, 3])
+def test_quadratic_known_minimizers_on_gpu(mods, idx):
+    """rankOneProblemSphere, joptP1, distanceFromOrigin0/1 through OptimizationProblem.withoutFeasiblePoint
+    (phase I with the quadratic rows, then BR) on the engine: the known minimiser within the Runner tolerance."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import OptimizationProblem, problem_from_spec
+    spec = Z.known_answer_zoo_quadratic()[idx]
+    objF, cs, eqs = problem_from_spec(dict(spec, x0=spec["x_where_defined"]))
+    pars = SP.standardParams()
+    prob = OptimizationProblem.withoutFeasiblePoint(spec["id"], objF, cs, eqs, "BR", pars)
+    sol = prob.solve()
+    assert abs(Z.objective_value(spec, sol.x) - Z.objective_value(spec, spec["x_opt"])) < 1e-2
+    assert np.linalg.norm(sol.x - spec["x_opt"]) < 1e-2
+    assert sol.dualityGap < pars.tolSolver
+    prob.solver.engine.close()

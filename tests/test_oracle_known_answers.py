@@ -248,3 +248,40 @@ def test_primal_dual_with_equalities_fails_like_the_reference(spec):
     x0 = O.with_feasible_point(pb, spec["x_where_defined"], pars)
     with pytest.raises(O.LineSearchFailedException):
         O.pd_solve_with_eqs(pb, x0, pars)
+
+
+# ---- QuadraticConstraint problems (SimpleOptimizationProblems.scala:266-300, 347-377, 464-561) ------------------
+
+def _qproblem(spec):
+    return O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"],
+                     qrows=spec["qrows"], qP=spec["qP"])
+
+
+@pytest.mark.parametrize("spec", Z.known_answer_zoo_quadratic(), ids=lambda s: s["id"])
+def test_known_minimizers_quadratic_constraints(spec):
+    """Phase I + BR on the reference's quadratic-constraint problems: the known minimiser within the Runner's
+    tolerance (1e-2), duality gap below tolSolver."""
+    pb = _qproblem(spec)
+    pars = O.standard_params()
+    x0 = O.with_feasible_point(pb, spec["x_where_defined"], pars)
+    sol = O.barrier_solve(pb, x0, pars)
+    assert abs(O.objective_value(pb, sol.x) - O.objective_value(pb, spec["x_opt"])) < 1e-2
+    assert np.linalg.norm(sol.x - spec["x_opt"]) < 1e-2
+    assert sol.dualityGap < pars.tolSolver
+
+
+def test_quadratic_constraint_oracles_are_consistent():
+    """The barrier gradient / Hessian with quadratic rows against central differences of the barrier value."""
+    spec = Z.random_qp_quad(12, 20, 3, instance=2)
+    pb = _qproblem(spec)
+    x = 1e-3 * np.linspace(-1, 1, 12)
+    t = 3.0
+    g = O.barrier_gradient(pb, t, x)
+    H = O.barrier_hessian(pb, t, x)
+    h = 1e-6
+    for i in range(12):
+        e = np.zeros(12)
+        e[i] = h
+        assert abs((O.barrier_value(pb, t, x + e) - O.barrier_value(pb, t, x - e)) / (2 * h) - g[i]) < 1e-6
+        dg = (O.barrier_gradient(pb, t, x + e) - O.barrier_gradient(pb, t, x - e)) / (2 * h)
+        assert np.max(np.abs(dg - H[:, i])) < 1e-5 * max(1.0, np.max(np.abs(H)))
