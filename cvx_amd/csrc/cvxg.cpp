@@ -265,7 +265,8 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
 // back by its group.  The critical chain tasks POTRF(k), TRSM(k+1,k), UPDATE(k+1,k+1,k) are simulated but
 // not emitted (workgroup 0 runs them in sequence); every transitive dependency of a chain task still precedes
 // that task's dependents in the emitted order, which keeps the launch deadlock-free.
-static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles) {
+static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles, int near = 0,
+                                                 double boost = 0.0, int band = 0) {
   struct Task {
     int type, i, j, k, cnt;
     double dur, bl, avail;
@@ -285,7 +286,12 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
       }
     upd_id.assign(tot, -1);
   }
-  const double d_potrf = 18.0, d_trsm = 6.0, d_upd = 5.5, d_upd4 = 10.0;  // us (scripts/df_trace.py)
+  // Estimated task times (us).  POTRF stands for the chain period minus the simulated TRSM + UPDATE of the chain
+  // (measured ~22 us per block), UPDATE4 for its measured ~14 us plus the contention of a full chip.  With the
+  // former 18 / 10 the simulated chain ran slower and the workers faster than on the device, so the emitted order
+  // put TRSM(k+2, k) -- which the chain needs next -- behind trailing updates: 1.77 -> 1.57 ms per factorization.
+  double d_potrf = 10.0, d_trsm = 6.0, d_upd = 5.5, d_upd4 = 16.0;
+  if (const char* e = getenv("CVXG_DF_DUR")) sscanf(e, "%lf,%lf,%lf,%lf", &d_potrf, &d_trsm, &d_upd, &d_upd4);
   for (int k = 0; k < nb; ++k) {  // (k, type) order is a topological order
     potrf_id[k] = (int)T.size();
     T.push_back({0, k, k, k, 1, d_potrf, 0, 0, k > 0 ? 1 : 0});
@@ -295,8 +301,9 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
     }
     for (int j = k + 1; j < nb; ++j)
       for (int i = j; i < nb; ++i) {
-        const bool grp = group && (k % 4 == 0) && (k + 4 <= j - singles);
-        const bool inside = group && (k % 4 != 0) && ((k & ~3) + 4 <= j - singles);
+        const bool band = i - j < near;  // near-diagonal tiles: single updates (each panel as soon as it is done)
+        const bool grp = group && !band && (k % 4 == 0) && (k + 4 <= j - singles);
+        const bool inside = group && !band && (k % 4 != 0) && ((k & ~3) + 4 <= j - singles);
         if (inside) continue;  // covered by the group starting at k & ~3
         const int cnt = grp ? 4 : 1;
         const int id = (int)T.size();
@@ -328,6 +335,10 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
     double m = 0.0;
     for (int s : sv) m = std::max(m, T[s].bl);
     T[t].bl = T[t].dur + m;
+    // priority bonus for the work the critical chain waits on: updates of near-diagonal tiles and the TRSMs
+    // of the next block rows (their results feed TRSM(k+1, k) and UPDATE(k+1, k+1, k))
+    const Task& x = T[t];
+    if (boost > 0.0 && ((x.type >= 2 && x.i - x.j < band) || (x.type == 1 && x.i - x.k <= band))) T[t].bl += boost;
   }
   // list scheduling
   typedef std::pair<double, int> DI;
@@ -1019,7 +1030,13 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
       int group = 1, singles = 2;
       if (const char* e = getenv("CVXG_DF_GROUP")) group = atoi(e) != 0;
       if (const char* e = getenv("CVXG_DF_SINGLES")) singles = std::max(1, atoi(e));
-      std::vector<unsigned> order = build_chol_schedule(ctx->nblk, ctx->ncu, group, singles);
+      int near = 0;
+      double boost = 0.0;
+      if (const char* e = getenv("CVXG_DF_NEAR")) near = std::max(0, atoi(e));
+      int band = 2;
+      if (const char* e = getenv("CVXG_DF_BOOST")) boost = atof(e);
+      if (const char* e = getenv("CVXG_DF_BAND")) band = atoi(e);
+      std::vector<unsigned> order = build_chol_schedule(ctx->nblk, ctx->ncu, group, singles, near, boost, band);
       ctx->df_ntasks = (int)order.size();
       CHK(dalloc(ctx, &ctx->df_tasks, order.size()));
       CHK(copy_sync(ctx, ctx->df_tasks, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
