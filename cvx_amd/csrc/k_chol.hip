@@ -249,6 +249,18 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
 #pragma unroll
   for (int rho = 0; rho < MAX_RHS; ++rho) acc[rho] = 0.0;
   double cur[16], nxt[16];
+  // off the critical path: this block's w_b and L_bb^-1 (final before the launch) into registers up front
+  double lin[16], wb[(MAX_RHS * NB + 255) / 256];
+  {
+    const double* li = Linv + (size_t)b * NB * NB;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) lin[r] = li[(16 * g + r) * NB + c];
+#pragma unroll
+    for (int q = 0; q < (MAX_RHS * NB + 255) / 256; ++q) {
+      const int t = threadIdx.x + 256 * q;
+      wb[q] = (t < nrhs * NB) ? rhs[(size_t)(b * NB + t % NB) * nrhs + t / NB] : 0.0;
+    }
+  }
   auto load_tile = [&](double (&t)[16], int i) {  // rows 16g.. of tile (i, b), column c
     const double* tp = L + (size_t)i * NB * ld + (size_t)b * NB + c;
 #pragma unroll
@@ -282,17 +294,20 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
   // y = w_b - s_b, then u_b = Linv_bb' y
   for (int rho = 0; rho < nrhs; ++rho) part[g][rho][c] = acc[rho];
   __syncthreads();
-  for (int t = threadIdx.x; t < nrhs * NB; t += 256) {
-    const int rho = t / NB, cc = t % NB;
-    const double sb = ((part[0][rho][cc] + part[1][rho][cc]) + part[2][rho][cc]) + part[3][rho][cc];
-    u[rho][cc] = rhs[(size_t)(b * NB + cc) * nrhs + rho] - sb;
+#pragma unroll
+  for (int q = 0; q < (MAX_RHS * NB + 255) / 256; ++q) {
+    const int t = threadIdx.x + 256 * q;
+    if (t < nrhs * NB) {
+      const int rho = t / NB, cc = t % NB;
+      const double sb = ((part[0][rho][cc] + part[1][rho][cc]) + part[2][rho][cc]) + part[3][rho][cc];
+      u[rho][cc] = wb[q] - sb;
+    }
   }
   __syncthreads();
-  const double* li = Linv + (size_t)b * NB * NB;
   for (int rho = 0; rho < nrhs; ++rho) {
     double s = 0.0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s = fma(li[(16 * g + r) * NB + c], u[rho][16 * g + r], s);
+    for (int r = 0; r < 16; ++r) s = fma(lin[r], u[rho][16 * g + r], s);
     part[g][rho][c] = s;
   }
   __syncthreads();
