@@ -455,16 +455,20 @@ __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c,
                                                    const double* __restrict__ ub, int m, double tbase, double beta,
                                                    double* __restrict__ part_log, int* __restrict__ part_cnt,
                                                    const double* __restrict__ f) {
-  __shared__ double slog[4][LS_TRIALS];
-  __shared__ int sviol[4][LS_TRIALS];
-  __shared__ int snpos[4][LS_TRIALS];
+  // blockIdx.y = group of LS_GROUP consecutive trials (more workgroups than ceil(m/256) alone)
+  constexpr int LS_GROUP = 8;
+  __shared__ double slog[4][LS_GROUP];
+  __shared__ int sviol[4][LS_GROUP];
+  __shared__ int snpos[4][LS_GROUP];
+  const int k0 = blockIdx.y * LS_GROUP;
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool valid = i < m;
   const double ci = valid ? c[i] : 0.0, ei = valid ? e[i] : 0.0, ubi = valid ? ub[i] : 1.0;
   const double fi = (valid && f) ? f[i] : 0.0;  // s'P s of a QuadraticConstraint row (0: linear)
   double t = tbase;
-  for (int k = 0; k < LS_TRIALS; ++k) {
+  for (int q = 0; q < k0; ++q) t *= beta;  // the same product chain as trial by trial
+  for (int kk = 0; kk < LS_GROUP; ++kk) {
     const double g = f ? (ci + t * ei) + (t * t * fi) / 2 : ci + t * ei;
     const double dd = ubi - g;
     const bool viol = valid && !(g * (1 + 3e-16) < ubi);   // Constraint.scala:23
@@ -473,21 +477,21 @@ __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c,
     const double sl = wave_sum(lg);
     const unsigned long long bv = __ballot(viol), bn = __ballot(npos);
     if (lane == 0) {
-      slog[wid][k] = sl;
-      sviol[wid][k] = __popcll(bv);
-      snpos[wid][k] = __popcll(bn);
+      slog[wid][kk] = sl;
+      sviol[wid][kk] = __popcll(bv);
+      snpos[wid][kk] = __popcll(bn);
     }
     t *= beta;  // t *= beta (repeated products, not pow)   UnconstrainedSolver.scala:93
   }
   __syncthreads();
-  if (threadIdx.x < LS_TRIALS) {
-    const int k = threadIdx.x;
+  if (threadIdx.x < LS_GROUP) {
+    const int kk = threadIdx.x, k = k0 + kk;
     double s = 0.0;
     int v = 0, np_ = 0;
     for (int w = 0; w < 4; ++w) {
-      s += slog[w][k];
-      v += sviol[w][k];
-      np_ += snpos[w][k];
+      s += slog[w][kk];
+      v += sviol[w][kk];
+      np_ += snpos[w][kk];
     }
     part_log[(size_t)blockIdx.x * LS_TRIALS + k] = s;
     part_cnt[((size_t)blockIdx.x * LS_TRIALS + k) * 2 + 0] = v;
@@ -497,7 +501,7 @@ __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c,
 
 void launch_ls_trials(hipStream_t s, const double* c, const double* e, const double* ub, int m, double tbase,
                       double beta, double* part_log, int* part_cnt, const double* f) {
-  k_ls_trials<<<ls_blocks(m), 256, 0, s>>>(c, e, ub, m, tbase, beta, part_log, part_cnt, f);
+  k_ls_trials<<<dim3(ls_blocks(m), LS_TRIALS / 8), 256, 0, s>>>(c, e, ub, m, tbase, beta, part_log, part_cnt, f);
 }
 
 // KL dual objective along the trial steps: per trial k, sum_j R exp(-(v_j + t_k u_j)) (v = B'z, u = B's),
