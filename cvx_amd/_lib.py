@@ -97,6 +97,10 @@ SIGNATURES = {
                                     C.POINTER(cvxg_pd_step_info)]),
     "cvxg_pd_solve": (C.c_int, [_P, C.POINTER(cvxg_params), C.POINTER(cvxg_pd_solution)]),
     "cvxg_get_lambda": (C.c_int, [_P, _D]),
+    "cvxg_solution_space": (C.c_int, [C.c_int, C.c_int, C.c_int, _D, C.c_int, C.c_int, _D, _D, _D, C.c_int]),
+    "cvxg_affine_from": (C.c_int, [_P, _P, _D, _D, C.c_int]),
+    "cvxg_affine_parameter": (C.c_int, [_P, _D, _D]),
+    "cvxg_affine_map": (C.c_int, [_P, _D, _D]),
     "cvxg_set_timing": (C.c_int, [_P, C.c_int]),
     "cvxg_get_phase_times": (C.c_int, [_P, _D, C.c_int]),
 }

@@ -25,7 +25,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from .engine import CvxgError, Engine, NotStrictlyFeasible
+from .engine import CvxgError, Engine, NotStrictlyFeasible, solution_space
 
 # ------------------------------------------------------------------------------------------------
 
@@ -341,6 +341,7 @@ class GpuBarrierSolver:
         if p > _lib.CVXG_MAX_EQ:
             raise TypeError(f"GPU barrier engine: at most {_lib.CVXG_MAX_EQ} equality rows")
         self.objF, self.cnts, self.eqs, self.pars = objF, cnts, eqs, pars
+        self.device = device
         self.dim = cnts.dim
         self.startingPoint = cnts.feasiblePoint
         A, r, ub = cnts.packed()
@@ -379,6 +380,62 @@ class GpuBarrierSolver:
     def solve(self, debugLevel: int = 0) -> Solution:
         return self.solveSpecial(0)
 
+    # --- affine re-parametrisation (BarrierSolver.scala:191-256) -------------------------------------
+    def affineTransformed(self, z0, F, u0=None) -> "AffineGpuBarrierSolver":
+        """This solver in the variable u with x = z0 + F u; results are reported in u (BarrierSolver.scala:209-232).
+        u0 None: u0 = F'(x0 - z0) on the device — svdSolve(F, x0 - z0) of :237-243 for an F with orthonormal
+        columns (SolutionSpace's F); the reference's assertion |x0 - (z0 + F u0)| < tolEqSolve catches any other."""
+        return AffineGpuBarrierSolver(self, z0, F, u0)
+
+    def reduced(self, sol: "SolutionSpace") -> "AffineGpuBarrierSolver":
+        """BarrierSolver.reduced (BarrierSolver.scala:249-256): affineTransformed(sol.z0, sol.F, sol.parameter(x0))."""
+        return AffineGpuBarrierSolver(self, sol.z0, sol.F, None)
+
+
+class AffineGpuBarrierSolver(GpuBarrierSolver):
+    """The BarrierSolver returned by affineTransformed: the source problem pulled back to u on its own device context
+    (cvxg_affine_from), so every Newton step runs in dimension F.cols on the engine's kernels."""
+
+    def __init__(self, parent: GpuBarrierSolver, z0, F, u0=None):
+        z0 = np.asarray(z0, dtype=np.float64)
+        F = np.asarray(F, dtype=np.float64)
+        if F.ndim != 2 or F.shape[0] != parent.dim or z0.shape != (parent.dim,):
+            raise ValueError(f"affineTransformed: F must be {parent.dim} x k and z0 of length {parent.dim}")
+        self.parent, self.z0, self.F = parent, z0, F
+        self.objF, self.eqs, self.pars = parent.objF, parent.eqs, parent.pars
+        self.cnts = parent.cnts
+        self.dim = F.shape[1]
+        p = 0 if parent.eqs is None else parent.eqs.A.shape[0]
+        self.engine = Engine(self.dim, parent.engine.m, p, parent.device)
+        self.engine.affine_from(parent.engine, z0, F)
+        x0 = parent.startingPoint
+        u0 = self.engine.affine_parameter(x0) if u0 is None else np.asarray(u0, dtype=np.float64)
+        if not np.linalg.norm(x0 - self.engine.affine_map(u0)) < self.pars.tolEqSolve:  # BarrierSolver.scala:217-219
+            raise AssertionError("u0 does not map to x0 under the variable transform.")
+        self.startingPoint = u0
+
+    def x_of(self, u) -> np.ndarray:
+        """x = z0 + F u on the device (cvxg_affine_map)."""
+        return self.engine.affine_map(u)
+
+
+class SolutionSpace:
+    """SolutionSpace(A, b) (SolutionSpace.scala:20-37): {x : Ax = b} = {z0 + F u}, F with orthonormal columns spanning
+    ker A, z0 the minimum-norm solution — MatrixUtils.solveUnderdetermined's QR of A' on the device
+    (cvxg_solution_space)."""
+
+    def __init__(self, A, b, device: int = 0):
+        A = np.asarray(A, dtype=np.float64)
+        b = np.asarray(b, dtype=np.float64)
+        assert A.shape[0] == b.shape[0]
+        assert A.shape[0] < A.shape[1]
+        self.A, self.b = A, b
+        self.z0, self.F = solution_space(A, b, device)
+
+    @staticmethod
+    def apply(A, b, device: int = 0) -> "SolutionSpace":
+        return SolutionSpace(A, b, device)
+
 
 class BarrierSolver:
     @staticmethod
@@ -403,6 +460,7 @@ class GpuPrimalDualSolver:
         if cnts.feasiblePoint is None:
             raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
         self.objF, self.cnts, self.eqs, self.pars = objF, cnts, eqs, pars
+        self.device = device
         self.dim = cnts.dim
         self.startingPoint = cnts.feasiblePoint
         A, r, ub = cnts.packed()

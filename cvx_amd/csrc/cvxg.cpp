@@ -123,6 +123,9 @@ struct cvxg_ctx {
   double eqGap = 0.0;
   double f_at_x = 0.0;    // barrier value at x
   int x_eval_valid = 0;   // c/d/w/y/scalars correspond to the current x and t
+  // affine re-parametrisation (cvxg_affine_from): x = z0 + F u with F (aff_n x n, column-major, ld aff_n)
+  double *aff_F = nullptr, *aff_z0 = nullptr;
+  int aff_n = 0;
   Timer tm;
   std::string err;
 };
@@ -967,7 +970,8 @@ extern "C" {
 
 const char* cvxg_version(void) { return "cvxg 0.1 (gfx950, FP64 MFMA SYRK, blocked Cholesky NB=64)"; }
 
-const char* cvxg_last_error(const cvxg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+static thread_local std::string g_err;  // errors of the context-free entry points (cvxg_solution_space)
+const char* cvxg_last_error(const cvxg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
 // K split of the SYRK tail tiles: the leftover tiles share one wave of slots.
 static int syrk_nsplit(const cvxg_ctx* ctx, int kchunks) {
@@ -1102,7 +1106,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->sp_pq, ctx->sp_row, ctx->sp_coef, ctx->kl_spart, ctx->lam, ctx->dlam, ctx->pd_rc,
                   ctx->pd_w, ctx->pd_rhs, ctx->pd_d1, ctx->pd_R0, ctx->pd_R1, ctx->pd_tmp, ctx->pd_part_rows,
                   ctx->pd_part_cols, ctx->pd_out, ctx->qrows, ctx->qslot, ctx->Pq, ctx->qPx, ctx->qPs,
-                  ctx->qextra, ctx->qf};
+                  ctx->qextra, ctx->qf, ctx->aff_F, ctx->aff_z0};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
@@ -1817,3 +1821,244 @@ int cvxg_get_lambda(cvxg_ctx* ctx, double* lambda) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Affine re-parametrisation x = z0 + F u (BarrierSolver.affineTransformed / reduced, BarrierSolver.scala:209-256)
+// ------------------------------------------------------------------------------------------------
+namespace {
+// Device scratch freed on every exit path of the setup calls below.
+struct DevBufs {
+  std::vector<void*> p;
+  template <class T>
+  T* get(size_t count) {
+    void* q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    p.push_back(q);
+    return (T*)q;
+  }
+  ~DevBufs() {
+    for (void* q : p) (void)hipFree(q);
+  }
+};
+}  // namespace
+
+static int gerr(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int cvxg_solution_space(int device, int p, int n, const double* A, int ldA, int row_major, const double* b,
+                        double* z0, double* F, int ldF) {
+  if (!A || !b || !z0 || !F) return gerr(CVXG_E_ARG, "cvxg_solution_space: null argument");
+  if (p <= 0 || p >= n) return gerr(CVXG_E_DIM, "SolutionSpace: need 0 < rows(A) = %d < cols(A) = %d", p, n);
+  if (ldA < (row_major ? n : p) || ldF < n) return gerr(CVXG_E_DIM, "cvxg_solution_space: leading dimension too small");
+  if (hipSetDevice(device) != hipSuccess) return gerr(CVXG_E_HIP, "hipSetDevice(%d) failed", device);
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return gerr(CVXG_E_HIP, "stream create failed");
+  int rc = CVXG_OK;
+  {
+    DevBufs B;
+    const size_t nn = (size_t)n * n;
+    double* M = B.get<double>(nn);
+    double* Rc = B.get<double>((size_t)n * p);
+    double* tau = B.get<double>(p);
+    double* y = B.get<double>(p);
+    double* z = B.get<double>(n);
+    std::vector<double> h(nn, 0.0);
+    for (int i = 0; i < p; ++i)  // column i of M = row i of A (M = A', column-major, ld n)
+      for (int j = 0; j < n; ++j) h[(size_t)i * n + j] = row_major ? A[(size_t)i * ldA + j] : A[(size_t)j * ldA + i];
+    std::vector<double> hR((size_t)n * p), hy(p);
+    if (!M || !Rc || !tau || !y || !z) {
+      rc = gerr(CVXG_E_HIP, "cvxg_solution_space: device allocation failed");
+    } else if (hipMemcpyAsync(M, h.data(), nn * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
+               lib_qr_full(s, M, n, p, tau, Rc) != 0 ||
+               hipMemcpyAsync(hR.data(), Rc, hR.size() * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+               hipStreamSynchronize(s) != hipSuccess) {
+      rc = gerr(CVXG_E_HIP, "cvxg_solution_space: QR of A' failed");
+    } else {
+      // forwardSolve(R.t, b) (MatrixUtils.scala:383-403): L = R' is read on and below its diagonal, j ascending
+      auto Lij = [&](int i, int j) { return hR[(size_t)i * n + j]; };  // L(i,j) = R(j,i) = column i, row j
+      for (int i = 0; i < p && rc == CVXG_OK; ++i) {
+        if (!(fabs(Lij(i, i)) > 0)) rc = gerr(CVXG_E_UNSOLVABLE, "Singular lower trianguar matrix L: zero on the diagonal");
+        double acc = 0.0;
+        for (int j = 0; j < i; ++j) acc += Lij(i, j) * hy[j];
+        hy[i] = (b[i] - acc) / Lij(i, i);
+      }
+      std::vector<double> hz(n);
+      if (rc == CVXG_OK &&
+          (hipMemcpyAsync(y, hy.data(), p * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
+           lib_gemv(s, false, n, p, 1.0, M, n, y, 0.0, z) != 0 ||  // z0 = Q(:, 0 until p) y
+           hipMemcpyAsync(hz.data(), z, n * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+           hipMemcpyAsync(h.data(), M, nn * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+           hipStreamSynchronize(s) != hipSuccess))
+        rc = gerr(CVXG_E_HIP, "cvxg_solution_space: z0 / Q download failed");
+      if (rc == CVXG_OK) {
+        memcpy(z0, hz.data(), n * sizeof(double));
+        for (int c = 0; c < n - p; ++c) memcpy(F + (size_t)c * ldF, h.data() + (size_t)(p + c) * n, n * sizeof(double));
+      }
+    }
+  }
+  (void)hipStreamDestroy(s);
+  return rc;
+}
+
+#define LIBC(ctx, call)                                                                    \
+  do {                                                                                     \
+    if ((call) != 0) return set_err(ctx, CVXG_E_HIP, "%s failed (%s:%d)", #call, __FILE__, __LINE__); \
+  } while (0)
+
+int cvxg_affine_from(cvxg_ctx* dst, cvxg_ctx* src, const double* z0, const double* F, int ldF) {
+  if (!dst || !src || !z0 || !F || dst == src) return dst ? set_err(dst, CVXG_E_ARG, "cvxg_affine_from: bad argument") : CVXG_E_ARG;
+  if (dst->dev != src->dev) return set_err(dst, CVXG_E_ARG, "cvxg_affine_from: contexts on different devices");
+  if (dst->m != src->m || dst->p != src->p)
+    return set_err(dst, CVXG_E_DIM, "cvxg_affine_from: dst must have the m and p of src");
+  if (ldF < src->n) return set_err(dst, CVXG_E_DIM, "cvxg_affine_from: ldF < n");
+  if (!src->have_obj || !src->have_ineq || (src->p > 0 && !src->have_eq))
+    return set_err(dst, CVXG_E_ARG, "cvxg_affine_from: the source problem is not complete");
+  if (src->kl) return set_err(dst, CVXG_E_UNSUPPORTED, "cvxg_affine_from: KL dual objective");
+  HIPC(dst, hipSetDevice(src->dev));
+  HIPC(dst, hipStreamSynchronize(src->s));
+  const int n = src->n, k = dst->n, m = src->m, p = src->p, nq = src->nq;
+  const int lds = src->np;
+  hipStream_t s = dst->s;
+  DevBufs B;
+  double* dF = B.get<double>((size_t)n * k);
+  double* dz = B.get<double>(n);
+  double* dT = B.get<double>((size_t)n * k);
+  double* dQ = B.get<double>((size_t)k * k);
+  double* dv = B.get<double>(n);
+  double* du = B.get<double>(k);
+  double* dAu = B.get<double>((size_t)std::max(m, 1) * k);
+  double* dr = B.get<double>(std::max(m, 1));
+  double* dAe = B.get<double>((size_t)std::max(p, 1) * k);
+  double* dbe = B.get<double>(std::max(p, 1));
+  if (!dF || !dz || !dT || !dQ || !dv || !du || !dAu || !dr || !dAe || !dbe)
+    return set_err(dst, CVXG_E_HIP, "cvxg_affine_from: device allocation failed");
+  {
+    std::vector<double> h((size_t)n * k);
+    for (int c = 0; c < k; ++c) memcpy(h.data() + (size_t)c * n, F + (size_t)c * ldF, n * sizeof(double));
+    CHK(copy_sync(dst, dF, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    CHK(copy_sync(dst, dz, z0, n * sizeof(double), hipMemcpyHostToDevice));
+  }
+  // F' X F for a symmetric row-major X (ld lds): T = X F, Q = F' T; lower triangle mirrored (the engine reads H's
+  // lower triangle, as dpotrf('L') reads the reference's (F'H)F)
+  auto pullback = [&](const double* X, std::vector<double>& out) -> int {
+    LIBC(dst, lib_gemm(s, false, false, n, k, n, X, lds, dF, n, dT, n));
+    LIBC(dst, lib_gemm(s, true, false, k, k, n, dF, n, dT, n, dQ, k));
+    out.resize((size_t)k * k);
+    CHK(copy_sync(dst, out.data(), dQ, out.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int j = 0; j < k; ++j)
+      for (int i = j + 1; i < k; ++i) out[(size_t)i * k + j] = out[(size_t)j * k + i];  // column-major: (i,j) -> (j,i)
+    return CVXG_OK;
+  };
+  // objective: QuadraticObjectiveFunction / LinearObjectiveFunction under x = z0 + F u
+  std::vector<double> Pu, au(k);
+  double r0u = src->r0, dot = 0.0;
+  CHK(copy_sync(dst, dv, src->a0, n * sizeof(double), hipMemcpyDeviceToDevice));
+  LIBC(dst, lib_dot(s, n, src->a0, dz, &dot));
+  r0u = r0u + dot;  // r + (a dot z)
+  if (src->hasP) {
+    CHK(pullback(src->P, Pu));
+    LIBC(dst, lib_gemv(s, false, n, n, 1.0, src->P, lds, dz, 1.0, dv));  // v = a + P z0
+    LIBC(dst, lib_gemv(s, false, n, n, 1.0, src->P, lds, dz, 0.0, dT));  // P z0
+    LIBC(dst, lib_dot(s, n, dz, dT, &dot));
+    r0u = r0u + dot / 2;  // + (z dot (P*z))/2
+  }
+  LIBC(dst, lib_gemv(s, true, n, k, 1.0, dF, n, dv, 0.0, du));  // a_u = F'(a + P z0)
+  CHK(copy_sync(dst, au.data(), du, k * sizeof(double), hipMemcpyDeviceToHost));
+  CHK(cvxg_set_objective(dst, src->hasP ? Pu.data() : nullptr, k, au.data(), r0u));
+  // inequalities: rows a_i -> F'a_i, r_i -> r_i + a_i.z0 (the row-major A is the column-major A', ld lds)
+  if (m > 0) {
+    std::vector<double> Au((size_t)m * k), ru(m), ubh(m);
+    LIBC(dst, lib_gemm(s, true, false, k, m, n, dF, n, src->A, lds, dAu, k));  // (A F)' = F' A'
+    CHK(copy_sync(dst, dr, src->r, m * sizeof(double), hipMemcpyDeviceToDevice));
+    LIBC(dst, lib_gemv(s, true, n, m, 1.0, src->A, lds, dz, 1.0, dr));
+    std::vector<double> Pqu;
+    if (nq > 0) {  // QuadraticConstraint.affineTransformed: F'(a + P z), F'PF, valueAt(z)
+      Pqu.resize((size_t)nq * k * k);
+      for (int q = 0; q < nq; ++q) {
+        const double* Pk = src->Pq + (size_t)q * lds * lds;
+        const int row = src->qrows_h[q];
+        std::vector<double> Q;
+        CHK(pullback(Pk, Q));
+        memcpy(Pqu.data() + (size_t)q * k * k, Q.data(), Q.size() * sizeof(double));
+        CHK(copy_sync(dst, dv, src->A + (size_t)row * lds, n * sizeof(double), hipMemcpyDeviceToDevice));
+        LIBC(dst, lib_gemv(s, false, n, n, 1.0, Pk, lds, dz, 1.0, dv));        // a + P z
+        LIBC(dst, lib_gemv(s, true, n, k, 1.0, dF, n, dv, 0.0, dAu + (size_t)row * k));
+        LIBC(dst, lib_gemv(s, false, n, n, 1.0, Pk, lds, dz, 0.0, dT));        // P z
+        LIBC(dst, lib_dot(s, n, dz, dT, &dot));
+        double rq = 0.0;
+        CHK(copy_sync(dst, &rq, dr + row, sizeof(double), hipMemcpyDeviceToHost));
+        rq = rq + dot / 2;
+        CHK(copy_sync(dst, dr + row, &rq, sizeof(double), hipMemcpyHostToDevice));
+      }
+    }
+    CHK(copy_sync(dst, Au.data(), dAu, Au.size() * sizeof(double), hipMemcpyDeviceToHost));
+    CHK(copy_sync(dst, ru.data(), dr, m * sizeof(double), hipMemcpyDeviceToHost));
+    CHK(copy_sync(dst, ubh.data(), src->ub, m * sizeof(double), hipMemcpyDeviceToHost));
+    CHK(cvxg_set_ineq(dst, Au.data(), k, 1, ru.data(), ubh.data()));
+    if (nq > 0) CHK(cvxg_set_quad(dst, nq, src->qrows_h.data(), Pqu.data(), k));
+  } else {
+    CHK(cvxg_set_ineq(dst, nullptr, k, 1, nullptr, nullptr));
+  }
+  // equalities: (A F) u = b - A z0
+  if (p > 0) {
+    std::vector<double> Ae((size_t)p * k), be(p);
+    LIBC(dst, lib_gemm(s, true, false, k, p, n, dF, n, src->Aeq, lds, dAe, k));
+    CHK(copy_sync(dst, dbe, src->beq, p * sizeof(double), hipMemcpyDeviceToDevice));
+    LIBC(dst, lib_gemv(s, true, n, p, -1.0, src->Aeq, lds, dz, 1.0, dbe));
+    CHK(copy_sync(dst, Ae.data(), dAe, Ae.size() * sizeof(double), hipMemcpyDeviceToHost));
+    CHK(copy_sync(dst, be.data(), dbe, p * sizeof(double), hipMemcpyDeviceToHost));
+    CHK(cvxg_set_eq(dst, Ae.data(), k, 1, be.data()));
+  }
+  // keep z0 and F for cvxg_affine_parameter / cvxg_affine_map
+  for (double** v : {&dst->aff_F, &dst->aff_z0})
+    if (*v) (void)hipFree(*v), *v = nullptr;
+  CHK(dalloc(dst, &dst->aff_F, (size_t)n * k));
+  CHK(dalloc(dst, &dst->aff_z0, n));
+  CHK(copy_sync(dst, dst->aff_F, dF, (size_t)n * k * sizeof(double), hipMemcpyDeviceToDevice));
+  CHK(copy_sync(dst, dst->aff_z0, dz, n * sizeof(double), hipMemcpyDeviceToDevice));
+  dst->aff_n = n;
+  return CVXG_OK;
+}
+
+int cvxg_affine_parameter(cvxg_ctx* dst, const double* x0, double* u0) {
+  if (!dst || !x0 || !u0) return CVXG_E_ARG;
+  if (!dst->aff_F) return set_err(dst, CVXG_E_ARG, "cvxg_affine_parameter: no affine transform loaded");
+  HIPC(dst, hipSetDevice(dst->dev));
+  const int n = dst->aff_n, k = dst->n;
+  DevBufs B;
+  double* dx = B.get<double>(n);
+  double* du = B.get<double>(k);
+  if (!dx || !du) return set_err(dst, CVXG_E_HIP, "device allocation failed");
+  CHK(copy_sync(dst, dx, x0, n * sizeof(double), hipMemcpyHostToDevice));
+  launch_axpy(dst->s, dx, dst->aff_z0, -1.0, n, dx);  // x0 - z0
+  HIPC(dst, hipGetLastError());
+  LIBC(dst, lib_gemv(dst->s, true, n, k, 1.0, dst->aff_F, n, dx, 0.0, du));
+  CHK(copy_sync(dst, u0, du, k * sizeof(double), hipMemcpyDeviceToHost));
+  return CVXG_OK;
+}
+
+int cvxg_affine_map(cvxg_ctx* dst, const double* u, double* x) {
+  if (!dst || !x) return CVXG_E_ARG;
+  if (!dst->aff_F) return set_err(dst, CVXG_E_ARG, "cvxg_affine_map: no affine transform loaded");
+  HIPC(dst, hipSetDevice(dst->dev));
+  const int n = dst->aff_n, k = dst->n;
+  DevBufs B;
+  double* du = B.get<double>(k);
+  double* dx = B.get<double>(n);
+  if (!du || !dx) return set_err(dst, CVXG_E_HIP, "device allocation failed");
+  if (u)
+    CHK(copy_sync(dst, du, u, k * sizeof(double), hipMemcpyHostToDevice));
+  else
+    CHK(copy_sync(dst, du, dst->x, k * sizeof(double), hipMemcpyDeviceToDevice));
+  CHK(copy_sync(dst, dx, dst->aff_z0, n * sizeof(double), hipMemcpyDeviceToDevice));
+  LIBC(dst, lib_gemv(dst->s, false, n, k, 1.0, dst->aff_F, n, du, 1.0, dx));  // z0 + F u
+  CHK(copy_sync(dst, x, dx, n * sizeof(double), hipMemcpyDeviceToHost));
+  return CVXG_OK;
+}

@@ -130,6 +130,13 @@ void launch_kkt_schur(hipStream_t s, const double* X, int nrhs, const double* B,
 
 // ---- symSolve / kktSymSolve fallback (symsolve.cpp, k_vec.hip) ----------------------------------------
 int sym_eig(hipStream_t s, double* M, int n2, int ldm, double* d, double* e_work, int* dinfo);
+// affine.cpp: rocSOLVER / rocBLAS calls of the affine re-parametrisation (setup only)
+int lib_qr_full(hipStream_t s, double* M, int n, int p, double* tau, double* Rcols);
+int lib_gemm(hipStream_t s, bool ta, bool tb, int m, int n, int k, const double* A, int lda, const double* B, int ldb,
+             double* C, int ldc);
+int lib_gemv(hipStream_t s, bool ta, int rows, int cols, double alpha, const double* A, int lda, const double* x,
+             double beta, double* y);
+int lib_dot(hipStream_t s, int n, const double* u, const double* v, double* out);
 void launch_eig_coeffs(hipStream_t s, const double* dots, const double* d, int n2, int npad, double* a, double* z);
 void launch_sum_chunks(hipStream_t s, const double* part, int nchunks, int cols, double* out);
 void launch_kkt_matrix(hipStream_t s, const double* H, int ldh, const double* Aeq, int lda, int n, int p, int ld,

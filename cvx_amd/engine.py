@@ -137,6 +137,28 @@ class Engine:
         self._check(self.lib.cvxg_get_x(self.h, _dp(x)))
         return x
 
+    # --- affine re-parametrisation x = z0 + F u -------------------------------------------------------
+    def affine_from(self, src: "Engine", z0, F):
+        """Load src's problem pulled back to u (cvxg_affine_from; BarrierSolver.affineTransformed). F: n x k."""
+        z0 = _f64(z0)
+        Fc = np.ascontiguousarray(np.asarray(F, dtype=np.float64).T)  # column-major n x k = row-major k x n
+        assert Fc.shape == (self.n, src.n) and z0.shape == (src.n,)
+        self._check(self.lib.cvxg_affine_from(self.h, src.h, _dp(z0), _dp(Fc), src.n))
+        self.n_x = src.n
+
+    def affine_parameter(self, x0) -> np.ndarray:
+        """SolutionSpace.parameter: u0 = F'(x0 - z0) (cvxg_affine_parameter)."""
+        x0 = _f64(x0)
+        u0 = np.zeros(self.n)
+        self._check(self.lib.cvxg_affine_parameter(self.h, _dp(x0), _dp(u0)))
+        return u0
+
+    def affine_map(self, u=None) -> np.ndarray:
+        """x = z0 + F u (cvxg_affine_map); u None = the current iterate."""
+        x = np.zeros(self.n_x)
+        self._check(self.lib.cvxg_affine_map(self.h, None if u is None else _dp(_f64(u)), _dp(x)))
+        return x
+
     # --- oracles ---------------------------------------------------------------------------------
     def barrier_eval(self, t: float, x, want_grad=True, want_hess=False):
         x = _f64(x)
@@ -222,3 +244,17 @@ class Engine:
         ms = np.zeros(8)
         self._check(self.lib.cvxg_get_phase_times(self.h, _dp(ms), 8))
         return ms
+
+
+def solution_space(A, b, device: int = 0):
+    """SolutionSpace(A, b) on the device (cvxg_solution_space; MatrixUtils.solveUnderdetermined): returns (z0, F)
+    with F n x (n-p) column-orthonormal, A F = 0 and A z0 = b."""
+    lib = L.lib()
+    A, b = _f64(A), _f64(b)
+    p, n = A.shape
+    z0 = np.zeros(n)
+    Fc = np.zeros((max(n - p, 0), n))  # column-major n x (n-p)
+    rc = lib.cvxg_solution_space(device, p, n, _dp(A), n, 1, _dp(b), _dp(z0), _dp(Fc), n)
+    if rc != 0:
+        raise _EXC.get(rc, CvxgError)(rc, lib.cvxg_last_error(None).decode())
+    return z0, Fc.T.copy()

@@ -32,6 +32,21 @@ def random_qp(n: int, m: int, instance: int = 0, dtype=np.float64) -> Dict[str, 
                 r=np.zeros(m), ub=ub, Aeq=None, beq=None, x0=np.zeros(n))
 
 
+def random_qp_eq(n: int, m: int, p: int, instance: int = 0) -> Dict[str, np.ndarray]:
+    """random_qp plus p dense equality rows Aeq x = beq (entries U[-1,1]) with beq = Aeq x0 at a small x0 that is
+    strictly inside the inequalities: the workload of the affine reduction x = z0 + F u
+    (BarrierSolver.reduced over SolutionSpace(Aeq, beq)), including p > CVXG_MAX_EQ."""
+    spec = random_qp(n, m, instance)
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 104729 + instance))
+    x0 = 0.01 * rng.uniform(-1.0, 1.0, size=n)
+    A = spec["A"]
+    ub = A @ x0 + rng.uniform(0.1, 0.2, size=m)
+    Aeq = rng.uniform(-1.0, 1.0, size=(p, n))
+    beq = Aeq @ x0
+    spec.update(id=f"random_qp_eq(n={n},m={m},p={p},instance={instance})", ub=ub, Aeq=Aeq, beq=beq, x0=x0)
+    return spec
+
+
 def random_qp_bounds(n: int, m: int, instance: int = 0) -> Dict[str, np.ndarray]:
     """random_qp plus sparse constraint rows interleaved with the dense ones, x0 = 0 strictly feasible:
     lower bounds -x_j <= 1 (the Constraints.singleCoordinatePositive shape, Constraints.scala:26-35, shifted),

@@ -97,7 +97,7 @@ typedef struct cvxg_solution {
 /* Allocate a context on HIP device `device` for n variables, m linear inequalities, p equalities. */
 int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out);
 void cvxg_destroy(cvxg_ctx* ctx);
-const char* cvxg_last_error(const cvxg_ctx* ctx);
+const char* cvxg_last_error(const cvxg_ctx* ctx);  /* NULL: the last error of a context-free call (this thread) */
 /* Library version / build string (for logs). */
 const char* cvxg_version(void);
 
@@ -216,6 +216,34 @@ int cvxg_pd_solve(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_pd_solution* sol)
 
 /* The dual iterate lambda (m entries) after cvxg_pd_solve. */
 int cvxg_get_lambda(cvxg_ctx* ctx, double* lambda);
+
+/* ---- affine re-parametrisation x = z0 + F u (BarrierSolver.affineTransformed / reduced) ----------- */
+
+/* SolutionSpace(A, b) (SolutionSpace.scala:20-27 -> MatrixUtils.solveUnderdetermined, MatrixUtils.scala:536-550):
+ * for A (p x n, p < n, full rank) the QR of A' (rocSOLVER dgeqrf + dorgqr with the full n x n Q, the LAPACK routines
+ * Breeze's qr calls) gives F = Q(:, p..n-1) (column-major n x (n-p), leading dimension ldF >= n, orthonormal columns
+ * spanning ker A) and z0 = Q(:, 0..p-1) y with R'y = b by forwardSolve (the minimum-norm solution).  No context:
+ * errors are reported through cvxg_last_error(NULL). */
+int cvxg_solution_space(int device, int p, int n, const double* A, int ldA, int row_major, const double* b,
+                        double* z0, double* F, int ldF);
+
+/* BarrierSolver.affineTransformed(z0, F, u0) (BarrierSolver.scala:209-232): load into `dst` (created with n = F.cols,
+ * the same m and p as `src`, on the same device) the problem of `src` pulled back to u with x = z0 + F u.  The
+ * reference composes its barrier functions (value at z0 + F u, F' gradient, (F' H) F); this engine transforms the
+ * problem data once on the device instead — P_u = F'PF, a_u = F'(a + P z0), r0_u = f0(z0), constraint rows A F with
+ * r + A z0 (LinearConstraint.affineTransformed, LinearConstraint.scala:46-52), quadratic rows F'(a + P_k z0) and
+ * F'P_kF with r + a.z0 + z0'P_k z0/2 (QuadraticConstraint.scala:54-61), equalities (A_eq F) u = b - A_eq z0
+ * (EqualityConstraint.scala:72-73) — so each Newton step runs in dimension F.cols at the cost of that dimension.
+ * Equal to the reference's composition in exact arithmetic.  F is column-major (ldF >= src n).  The KL dual
+ * objective is not transformable (CVXG_E_UNSUPPORTED).  dst keeps z0 and F for the two calls below. */
+int cvxg_affine_from(cvxg_ctx* dst, cvxg_ctx* src, const double* z0, const double* F, int ldF);
+
+/* SolutionSpace.parameter (SolutionSpace.scala:29-33): u0 = F'(x0 - z0) (x0 has src n entries, u0 dst n). */
+int cvxg_affine_parameter(cvxg_ctx* dst, const double* x0, double* u0);
+
+/* x = z0 + F u (the reporting map of the reduced solvers, UnconstrainedSolver.scala:199-200); u NULL = the current
+ * iterate of dst. */
+int cvxg_affine_map(cvxg_ctx* dst, const double* u, double* x);
 
 /* ---- instrumentation ----------------------------------------------------------------------------- */
 

@@ -203,3 +203,55 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_setQuad(JNIEnv* env, jclass cls, 
   (*env)->ReleasePrimitiveArrayCritical(env, rows, pr, JNI_ABORT);
   return rc;
 }
+
+/* solutionSpace(dev, p, n, A[p n] column-major, b[p], z0[n], F[n (n-p)] column-major) -> SolutionSpace(A, b) */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_solutionSpace(JNIEnv* env, jclass cls, jint dev, jint p, jint n,
+                                                            jdoubleArray A, jdoubleArray b, jdoubleArray z0,
+                                                            jdoubleArray F) {
+  (void)cls;
+  double* pA = (*env)->GetPrimitiveArrayCritical(env, A, 0);
+  double* pb = (*env)->GetPrimitiveArrayCritical(env, b, 0);
+  double* pz = (*env)->GetPrimitiveArrayCritical(env, z0, 0);
+  double* pF = (*env)->GetPrimitiveArrayCritical(env, F, 0);
+  jint rc = cvxg_solution_space(dev, p, n, pA, p, 0, pb, pz, pF, n);
+  (*env)->ReleasePrimitiveArrayCritical(env, F, pF, 0);
+  (*env)->ReleasePrimitiveArrayCritical(env, z0, pz, 0);
+  (*env)->ReleasePrimitiveArrayCritical(env, b, pb, JNI_ABORT);
+  (*env)->ReleasePrimitiveArrayCritical(env, A, pA, JNI_ABORT);
+  return rc;
+}
+
+/* affineFrom(dst, src, z0[n], F[n k] column-major, ldF) -> BarrierSolver.affineTransformed (cvxg_affine_from) */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_affineFrom(JNIEnv* env, jclass cls, jlong dst, jlong src,
+                                                         jdoubleArray z0, jdoubleArray F, jint ldF) {
+  (void)cls;
+  double* pz = (*env)->GetPrimitiveArrayCritical(env, z0, 0);
+  double* pF = (*env)->GetPrimitiveArrayCritical(env, F, 0);
+  jint rc = cvxg_affine_from(CTX(dst), CTX(src), pz, pF, ldF);
+  (*env)->ReleasePrimitiveArrayCritical(env, F, pF, JNI_ABORT);
+  (*env)->ReleasePrimitiveArrayCritical(env, z0, pz, JNI_ABORT);
+  return rc;
+}
+
+/* affineParameter(h, x0[n], u0[k]) -> SolutionSpace.parameter;  affineMap(h, u[k] (nullable), x[n]) -> z0 + F u */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_affineParameter(JNIEnv* env, jclass cls, jlong h, jdoubleArray x0,
+                                                              jdoubleArray u0) {
+  (void)cls;
+  double* px = (*env)->GetPrimitiveArrayCritical(env, x0, 0);
+  double* pu = (*env)->GetPrimitiveArrayCritical(env, u0, 0);
+  jint rc = cvxg_affine_parameter(CTX(h), px, pu);
+  (*env)->ReleasePrimitiveArrayCritical(env, u0, pu, 0);
+  (*env)->ReleasePrimitiveArrayCritical(env, x0, px, JNI_ABORT);
+  return rc;
+}
+
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_affineMap(JNIEnv* env, jclass cls, jlong h, jdoubleArray u,
+                                                        jdoubleArray x) {
+  (void)cls;
+  double* pu = u ? (*env)->GetPrimitiveArrayCritical(env, u, 0) : NULL;
+  double* px = (*env)->GetPrimitiveArrayCritical(env, x, 0);
+  jint rc = cvxg_affine_map(CTX(h), pu, px);
+  (*env)->ReleasePrimitiveArrayCritical(env, x, px, 0);
+  if (u) (*env)->ReleasePrimitiveArrayCritical(env, u, pu, JNI_ABORT);
+  return rc;
+}

@@ -144,6 +144,8 @@ def objective_value(pb: Problem, x: np.ndarray) -> float:
     """QuadraticObjectiveFunction.scala:31 — r + (a dot x) + (x dot (P*x))/2;
     LinearObjectiveFunction.scala:19 — r + (a dot x);
     KL dual: -dualObjFAt(z) = (vec_w dot z) + (vec_R dot exp(-B'z)) (Dist_KL.scala:146-147, Duality.scala:76)."""
+    if isinstance(pb, AffineView):
+        return objective_value(pb.pb, pb.x_of(x))
     if pb.kl_B is not None:
         return float(np.dot(pb.a0, x)) + float(np.dot(pb.kl_R, np.exp(-(pb.kl_B.T @ x))))
     v = pb.r0 + float(np.dot(pb.a0, x))
@@ -201,6 +203,8 @@ def is_satisfied_strictly(pb: Problem, i: int, x: np.ndarray) -> bool:
 
 def is_in_set(pb: Problem, x: np.ndarray) -> bool:
     """ConstraintSet.scala:34-38 via ConvexSet.scala:69 — short-circuit forall in list order."""
+    if isinstance(pb, AffineView):  # ConvexSet.affineTransformed: isInSet(u) = C.isInSet(z0 + F u) (ConvexSet.scala:47-58)
+        return is_in_set(pb.pb, pb.x_of(x))
     for i in range(pb.m):
         if not is_satisfied_strictly(pb, i, x):
             return False
@@ -220,6 +224,8 @@ def active_set(pb: Problem, x: np.ndarray, tol: float = 1e-12) -> np.ndarray:
 
 def barrier_value(pb: Problem, t: float, x: np.ndarray) -> float:
     """BarrierSolver.scala:280-289."""
+    if isinstance(pb, AffineView):  # BarrierSolver.scala:226 — self.barrierFunction(t, z0 + F u)
+        return barrier_value(pb.pb, t, pb.x_of(x))
     s = t * objective_value(pb, x)
     for i in range(pb.m):
         d = pb.ub[i] - constraint_value(pb, i, x)
@@ -231,6 +237,8 @@ def barrier_value(pb: Problem, t: float, x: np.ndarray) -> float:
 
 def barrier_gradient(pb: Problem, t: float, x: np.ndarray) -> np.ndarray:
     """BarrierSolver.scala:291-301 — fold starts at objF.gradientAt(x)*t, adds G/d."""
+    if isinstance(pb, AffineView):  # BarrierSolver.scala:227-228 — F.t * self.gradientBarrierFunction(t, z0 + F u)
+        return pb.F.T @ barrier_gradient(pb.pb, t, pb.x_of(x))
     s = objective_gradient(pb, x) * t
     for i in range(pb.m):
         d = pb.ub[i] - constraint_value(pb, i, x)
@@ -248,6 +256,8 @@ def barrier_hessian(pb: Problem, t: float, x: np.ndarray, literal: bool = True) 
     that is the CPU-baseline cost model.  ``literal=False`` drops only the +zeros/d term, which adds
     exact zeros (bit-identical result for d > 0).
     """
+    if isinstance(pb, AffineView):  # BarrierSolver.scala:229-230 — (F.t * self.hessianBarrierFunction(t, z0 + F u)) * F
+        return (pb.F.T @ barrier_hessian(pb.pb, t, pb.x_of(x), literal)) @ pb.F
     n = pb.n
     s = objective_hessian(pb, x) * t
     for i in range(pb.m):
@@ -265,6 +275,56 @@ def barrier_hessian(pb: Problem, t: float, x: np.ndarray, literal: bool = True) 
         else:
             s = s + GGt / (d * d)
     return s
+
+
+# ----------------------------------------------------------------------------------------------
+# Affine re-parametrisation x = z0 + F u (BarrierSolver.affineTransformed / reduced)
+# ----------------------------------------------------------------------------------------------
+
+
+def solve_underdetermined(A: np.ndarray, b: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """MatrixUtils.solveUnderdetermined (MatrixUtils.scala:536-550), used by SolutionSpace (SolutionSpace.scala:20-27).
+
+    Breeze ``qr(A.t)`` is LAPACK dgeqrf + dorgqr with the full n x n Q (restated by scipy's qr, the same routines):
+    F = Q(::, p until n); y = forwardSolve(R.t, b) (only the leading p x p block of R.t is read); z0 = Q(::, 0 until p) y.
+    """
+    import scipy.linalg
+    p, n = A.shape
+    assert p == b.shape[0] and p < n
+    Q, R = scipy.linalg.qr(A.T)
+    F = Q[:, p:]
+    y = forward_solve(np.ascontiguousarray(R.T[:, :p]), b)
+    z0 = Q[:, :p] @ y
+    return z0, F
+
+
+def solution_space_parameter(z0: np.ndarray, F: np.ndarray, x0: np.ndarray) -> np.ndarray:
+    """SolutionSpace.parameter (SolutionSpace.scala:29-33) — u0 = F.t * (x0 - z0)."""
+    return F.T @ (x0 - z0)
+
+
+class AffineView:
+    """The solver returned by BarrierSolver.affineTransformed(z0, F, u0) (BarrierSolver.scala:209-232): a
+    BarrierSolver in the variable u whose barrier value, gradient and Hessian are the original ones at
+    x = z0 + F u (value; F.t * gradient; (F.t * H) * F), whose feasible set is the preimage of C
+    (ConvexSet.scala:47-58) and whose equality constraint is (A F) u = b - A z0 (EqualityConstraint.scala:72-73).
+    The oracle functions dispatch on this type, so the inner solvers run unchanged on it."""
+
+    def __init__(self, pb: Problem, z0: np.ndarray, F: np.ndarray):
+        self.pb, self.z0, self.F = pb, np.asarray(z0, dtype=np.float64), np.asarray(F, dtype=np.float64)
+        self.Aeq = None if pb.Aeq is None else pb.Aeq @ self.F
+        self.beq = None if pb.Aeq is None else pb.beq - pb.Aeq @ self.z0
+
+    def x_of(self, u: np.ndarray) -> np.ndarray:
+        return self.z0 + self.F @ u
+
+    @property
+    def n(self) -> int:
+        return self.F.shape[1]
+
+    @property
+    def m(self) -> int:
+        return self.pb.m
 
 
 # ----------------------------------------------------------------------------------------------

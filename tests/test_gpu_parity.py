@@ -621,3 +621,115 @@ def test_quadratic_known_minimizers_on_gpu(mods, idx):
     assert np.linalg.norm(sol.x - spec["x_opt"]) < 1e-2
     assert sol.dualityGap < pars.tolSolver
     prob.solver.engine.close()
+
+
+# ---- affine re-parametrisation x = z0 + F u (BarrierSolver.affineTransformed / reduced, SolutionSpace) -----------
+
+@pytest.mark.parametrize("p,n", [(1, 10), (12, 40), (200, 700)])
+def test_solution_space_vs_oracle(mods, p, n):
+    """cvxg_solution_space (rocSOLVER dgeqrf + dorgqr) against MatrixUtils.solveUnderdetermined's restatement (LAPACK
+    through scipy): the same Householder convention gives the same F and z0."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.engine import solution_space
+    rng = np.random.default_rng(900 + p)
+    A = rng.uniform(-1, 1, size=(p, n))
+    b = rng.uniform(-1, 1, size=p)
+    z0, F = solution_space(A, b)
+    z0r, Fr = O.solve_underdetermined(A, b)
+    assert np.abs(F - Fr).max() < 1e-12
+    assert np.abs(z0 - z0r).max() < 1e-12 * max(1.0, np.abs(z0r).max())
+    assert np.abs(A @ F).max() < 1e-12 and np.abs(A @ z0 - b).max() < 1e-11
+
+
+def _eq_quad_spec(Z, n, m, q, p, instance):
+    spec = Z.random_qp_quad(n, m, q, instance=instance) if q else Z.random_qp(n, m, instance=instance)
+    rng = np.random.default_rng(77 + instance)
+    Aeq = rng.uniform(-1, 1, size=(p, n))
+    x0 = 1e-4 * rng.uniform(-1, 1, size=n)  # strictly feasible (|a_i.x0| << ub_i), not in ker Aeq: z0 != 0
+    spec.update(Aeq=Aeq, beq=Aeq @ x0, x0=x0)
+    return spec
+
+
+@pytest.mark.parametrize("n,m,q,p", [(40, 96, 0, 12), (40, 60, 3, 5), (300, 500, 2, 20)])
+def test_affine_oracles_and_direction_vs_oracle(mods, n, m, q, p):
+    """cvxg_affine_from: the problem pulled back to u (data transformed once on the device) against the reference's
+    composition (value at z0 + F u, F' gradient, (F' H) F; BarrierSolver.scala:224-231): oracles 1e-10, Newton
+    direction du 1e-8 relative."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.engine import solution_space
+    spec = _eq_quad_spec(Z, n, m, q, p, instance=5)
+    base = dict(spec, Aeq=None, beq=None)
+    pb = _qopb(O, base) if q else _opb(O, base)
+    src = _engine(Engine, base)
+    z0, F = solution_space(spec["Aeq"], spec["beq"])
+    k = F.shape[1]
+    eng = Engine(k, src.m, 0)
+    eng.affine_from(src, z0, F)
+    view = O.AffineView(pb, z0, F)
+    u = eng.affine_parameter(spec["x0"])
+    np.testing.assert_allclose(u, O.solution_space_parameter(z0, F, spec["x0"]), atol=1e-14)
+    assert np.linalg.norm(eng.affine_map(u) - spec["x0"]) < 1e-13
+    rng = np.random.default_rng(4)
+    u = u + 1e-3 * rng.standard_normal(k) / np.sqrt(k)
+    pars = SP.standardParams()
+    for t in (1.0, 37.5, 1e4):
+        f, g, H = eng.barrier_eval(t, u, want_grad=True, want_hess=True)
+        fr = O.barrier_value(view, t, u)
+        gr = O.barrier_gradient(view, t, u)
+        Hr = O.barrier_hessian(view, t, u, literal=False)
+        assert abs(f - fr) <= 1e-10 * max(1.0, abs(fr))
+        assert np.linalg.norm(g - gr) <= 1e-10 * np.linalg.norm(gr)
+        assert np.linalg.norm(H - Hr) <= 1e-10 * np.linalg.norm(Hr)
+        du, _, info = eng.newton_direction(pars, t, u, gr)
+        du_ref = O.newton_direction(view, t, u, gr, pars.tolEqSolve)
+        assert np.linalg.norm(du - du_ref) <= 1e-8 * np.linalg.norm(du_ref)
+    eng.close()
+    src.close()
+
+
+@pytest.mark.parametrize("n,m,q,p,inst", [(40, 96, 0, 12, 8), (60, 80, 2, 9, 9)])
+def test_reduced_barrier_solve_vs_oracle(mods, n, m, q, p, inst):
+    """BarrierSolver.reduced(SolutionSpace(Aeq, beq)) through the API mirror, with more equality rows than the on-device
+    KKT path takes (p > CVXG_MAX_EQ): the final x = z0 + F u matches the oracle's reduced solve and satisfies Aeq x = b."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import BarrierSolver, SolutionSpace, problem_from_spec
+    spec = _eq_quad_spec(Z, n, m, q, p, instance=inst)
+    base = dict(spec, Aeq=None, beq=None)
+    objF, cs, _ = problem_from_spec(base)
+    pars = SP.standardParams()
+    solver = BarrierSolver.apply(objF, cs.addFeasiblePoint(spec["x0"]), None, pars)
+    red = solver.reduced(SolutionSpace.apply(spec["Aeq"], spec["beq"]))
+    sol = red.solve()
+    x = red.x_of(sol.x)
+    pb = _qopb(O, base) if q else _opb(O, base)
+    z0, F = O.solve_underdetermined(spec["Aeq"], spec["beq"])
+    view = O.AffineView(pb, z0, F)
+    ref = O.barrier_solve(view, O.solution_space_parameter(z0, F, spec["x0"]), pars)
+    xr = view.x_of(ref.x)
+    assert np.linalg.norm(x - xr) <= 1e-6 * max(1.0, np.linalg.norm(xr))
+    assert np.abs(spec["Aeq"] @ x - spec["beq"]).max() < 1e-10
+    assert sol.dualityGap < pars.tolSolver
+    # (instances whose last centering stalls in rounding noise until maxIter — the reference's loop does that on
+    # e.g. instance 8 of the quadratic case — are not used here: their step count is noise)
+    assert not ref.maxedOut
+    assert abs(sol.newtonSteps - ref.newton_steps) <= max(2, int(0.05 * ref.newton_steps))
+    red.engine.close()
+    solver.engine.close()
+
+
+def test_reduced_known_minimizer_rank_one_simplex(mods):
+    """rankOneProblemSimplex(10) (SimpleOptimizationProblems.scala:221-255) by dimension reduction over sumToOne on the
+    engine: the known minimiser e_1 within the Runner tolerance."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import BarrierSolver, SolutionSpace, problem_from_spec
+    spec = Z.rank_one_problem_simplex(10)
+    objF, cs, eqs = problem_from_spec(dict(spec, x0=np.full(10, 0.1)))
+    pars = SP.standardParams()
+    solver = BarrierSolver.apply(objF, cs.addFeasiblePoint(np.full(10, 0.1)), None, pars)
+    red = solver.reduced(SolutionSpace.apply(eqs.A, eqs.b))
+    sol = red.solve()
+    x = red.x_of(sol.x)
+    assert np.linalg.norm(x - spec["x_opt"]) < 1e-2
+    assert abs(x.sum() - 1.0) < 1e-12
+    red.engine.close()
+    solver.engine.close()

@@ -285,3 +285,62 @@ def test_quadratic_constraint_oracles_are_consistent():
         assert abs((O.barrier_value(pb, t, x + e) - O.barrier_value(pb, t, x - e)) / (2 * h) - g[i]) < 1e-6
         dg = (O.barrier_gradient(pb, t, x + e) - O.barrier_gradient(pb, t, x - e)) / (2 * h)
         assert np.max(np.abs(dg - H[:, i])) < 1e-5 * max(1.0, np.max(np.abs(H)))
+
+
+# ---- affine re-parametrisation x = z0 + F u (BarrierSolver.affineTransformed / reduced) -----------------------
+
+@pytest.mark.parametrize("p,n", [(1, 10), (12, 30), (40, 64)])
+def test_solution_space_properties(p, n):
+    """SolutionSpace.scala:8-18 contract: A F = 0, F'F = I (orthonormal columns spanning ker A), A z0 = b, and z0 is
+    the minimum-norm solution (orthogonal to ker A); parameter(x0) recovers u0 from x0 = z0 + F u0."""
+    rng = RNG(500 + p)
+    A = rng.uniform(-1, 1, size=(p, n))
+    b = rng.uniform(-1, 1, size=p)
+    z0, F = O.solve_underdetermined(A, b)
+    assert F.shape == (n, n - p)
+    assert np.abs(A @ F).max() < 1e-13
+    assert np.abs(F.T @ F - np.eye(n - p)).max() < 1e-13
+    assert np.abs(A @ z0 - b).max() < 1e-12
+    assert np.abs(F.T @ z0).max() < 1e-12
+    u0 = rng.uniform(-1, 1, size=n - p)
+    np.testing.assert_allclose(O.solution_space_parameter(z0, F, z0 + F @ u0), u0, atol=1e-13)
+
+
+@pytest.mark.parametrize("spec", [Z.rank_one_problem_simplex(10), Z.joptP2()], ids=lambda s: s["id"])
+def test_reduced_barrier_known_minimizers(spec):
+    """The known-answer simplex problems of SimpleOptimizationProblems.scala solved by dimension reduction
+    (BarrierSolver.reduced over the sumToOne SolutionSpace, no equality constraint left): the reference's
+    isMinimizer tolerance 1e-2 (Runner.scala:30), and the same optimum as the KKT (EqualityConstrainedSolver) path."""
+    pb = O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"])
+    z0, F = O.solve_underdetermined(spec["Aeq"], spec["beq"])
+    n = spec["a0"].shape[0]
+    x0 = np.full(n, 1.0 / n)  # strictly feasible point of the simplex
+    view = O.AffineView(pb, z0, F)
+    pars = O.standard_params()
+    sol = O.barrier_solve(view, O.solution_space_parameter(z0, F, x0), pars)
+    x = view.x_of(sol.x)
+    assert abs(O.objective_value(pb, x) - O.objective_value(pb, spec["x_opt"])) < 1e-2
+    assert np.linalg.norm(x - spec["x_opt"]) < 1e-2
+    sol_kkt = O.barrier_solve(_problem(spec), x0, pars)
+    assert np.linalg.norm(x - sol_kkt.x) < 1e-6
+
+
+def test_reduced_barrier_matches_kkt_path_many_equalities():
+    """p = 12 equality rows (more than the engine's on-device KKT Schur path takes): the reduced barrier solve
+    reaches the optimum of the EqualityConstrainedSolver path, and the composed oracles are the transforms of the
+    original ones (gradient F'g, Hessian (F'H)F)."""
+    spec = Z.random_qp_eq(30, 60, 12, instance=1)
+    pb = O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"])
+    z0, F = O.solve_underdetermined(spec["Aeq"], spec["beq"])
+    view = O.AffineView(pb, z0, F)
+    u0 = O.solution_space_parameter(z0, F, spec["x0"])
+    assert np.linalg.norm(view.x_of(u0) - spec["x0"]) < 1e-12
+    x = spec["x0"]
+    np.testing.assert_allclose(O.barrier_gradient(view, 3.0, u0), F.T @ O.barrier_gradient(pb, 3.0, x), rtol=1e-12)
+    pars = O.standard_params()
+    sol = O.barrier_solve(view, u0, pars)
+    sol_kkt = O.barrier_solve(_problem(spec), spec["x0"], pars)
+    assert sol.dualityGap < pars.tolSolver
+    xr = view.x_of(sol.x)
+    assert np.linalg.norm(xr - sol_kkt.x) / np.linalg.norm(sol_kkt.x) < 1e-8
+    assert np.abs(spec["Aeq"] @ xr - spec["beq"]).max() < 1e-12
