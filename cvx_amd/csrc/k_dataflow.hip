@@ -249,6 +249,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   __shared__ __attribute__((aligned(16))) double smem[DF_SMEM];
   __shared__ unsigned s_task;
   __shared__ int s_ok;
+  __shared__ int s_next;
   int* counter = work;
   int* abortw = work + 1;
   int* state = work + 64;  // own cache lines
@@ -330,33 +331,33 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
 #pragma unroll 1
         for (int cb = 0; cb < 4; ++cb) {
           double* E = cs.E2[cb & 1];
+          if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
           if (cb > 0 && !have_next) {
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
           }
           if (cb == 3) mark(k, 1, 3);  // trace: last row-block of L_kk^-1 in hand
+          // non-blocking look at the next row-block: the sc1 poll is issued here and its value consumed only after
+          // this slice's MFMAs, so its round trip stays off the chain
+          int pollv = 0;
+          if (cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q;
             *reinterpret_cast<f64x2*>(E + (e >> 5) * DF_SP + 2 * (e & 31)) = er[q];
           }
-          have_next = false;
-          if (cb < 3) {  // non-blocking look at the next row-block
-            if (tid == 0) s_ok = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cb + 2;
-          }
           __syncthreads();
-          if (cb < 3 && s_ok) {
-            have_next = true;
-            eload(cb + 1);
-          }
-          {  // L'[16 wv.., 16 cb..] = A[16 wv.., :] L^-1[16 cb.., :]^T, K = 16 (cb + 1)
-            d4f acc = {0.0, 0.0, 0.0, 0.0};
+          {  // L'[16 wv.., 16 cb..] = A[16 wv.., :] L^-1[16 cb.., :]^T, K = 16 (cb + 1), two MFMA chains
+            d4f acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
             const double* Ar = cs.Sa + 16 * wv * DF_SP;
-            for (int s2 = 0; s2 < 4 * (cb + 1); ++s2) {
+            for (int s2 = 0; s2 < 4 * (cb + 1); s2 += 2) {
               const int kk = 4 * s2 + (lane >> 4);
-              acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ar[(lane & 15) * DF_SP + kk], E[(lane & 15) * DF_SP + kk], acc,
-                                                         0, 0, 0);
+              acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Ar[(lane & 15) * DF_SP + kk], E[(lane & 15) * DF_SP + kk], acc0,
+                                                          0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Ar[(lane & 15) * DF_SP + kk + 4], E[(lane & 15) * DF_SP + kk + 4],
+                                                          acc1, 0, 0, 0);
             }
+            const d4f acc = acc0 + acc1;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
@@ -364,7 +365,10 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               mA.st(row * ld + col, acc[r]);
             }
           }
+          if (tid == 0) s_next = (cb < 3) && pollv >= cb + 2;  // own word: read between this barrier and the next
           __syncthreads();
+          have_next = s_next;
+          if (have_next) eload(cb + 1);  // lands behind the diagonal update below
 #pragma unroll
           for (int q = 0; q < NBLK16; ++q) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
             const int ib = blk_ib[wv][q], jb = blk_jb[wv][q];
@@ -389,7 +393,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       // POTRF(b): tile and rhs block staged in LDS; L_bb^-1 row-blocks published progressively; before the
       // forward solve, the rhs block gets its last correction  - L_b,b-1 w_b-1  (w_b-1: POTRF(b-1) done)
       mark(b, 0, 0);
-      mark(b, 0, 1);
       auto fix = [&]() -> bool {
         if (b == 0) return true;
         const int k = b - 1;

@@ -1,0 +1,28 @@
+"""Per-block critical-chain stamps of a CVXG_DF_TRACE file (k_dataflow.hip): POTRF(k) start / last L^-1
+row-block published / done, and for block k+1 on the other chain workgroup: operands staged, slice 2 done,
+last row-block in hand, TRSM + diagonal update done (us from the first POTRF)."""
+import sys
+
+import numpy as np
+
+
+def main(path, blocks=(2, 3, 10, 30, 50, 61)):
+    raw = open(path, "rb").read()
+    nq, nb = (int(v) for v in np.frombuffer(raw[:8], dtype=np.int32))
+    n = nq + 3 * nb
+    tr = np.frombuffer(raw[8 + 4 * nq:8 + 4 * nq + 32 * n], dtype=np.uint64).reshape(n, 4).astype(np.int64)
+    ch = tr[nq:].reshape(nb, 3, 4)
+    t0 = ch[0, 0, 0]
+    us = lambda v: (v - t0) / 100.0
+    per = (ch[nb - 1, 0, 0] - ch[1, 0, 0]) / 100.0 / (nb - 2)
+    print(f"chain period {per:.2f} us per block")
+    for k in blocks:
+        if k + 1 >= nb:
+            continue
+        p, pn = ch[k], ch[k + 1]
+        print(f"{k:3d} potrf {us(p[0, 0]):8.1f} pub3 {us(p[0, 3]):8.1f} done {us(p[0, 2]):8.1f} | k+1: staged "
+              f"{us(p[1, 1]):8.1f} slice2 {us(pn[0, 1]):8.1f} lastrow {us(p[1, 3]):8.1f} done {us(p[1, 2]):8.1f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
