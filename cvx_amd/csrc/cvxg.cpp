@@ -70,7 +70,6 @@ struct cvxg_ctx {
   int* tiles = nullptr;
   int ntiles = 0, nsplit = 1;
   int ntiles_main = 0;  // tiles assembled without K split (whole waves of slots); the rest use nsplit
-  int chol_outer = 4;  // 64-blocks per outer Cholesky panel (trailing update width 256)
   int slots = 512;     // SYRK workgroup slots (2 per CU)
   // Sparse constraint rows (<= SPARSE_NNZ nonzeros: bounds, phase-I bound rows, box rows).  Their Hessian
   // terms are per-entry sums (k_sparse_hess); only the dense rows, packed into As, go through the SYRK.
@@ -99,11 +98,8 @@ struct cvxg_ctx {
   double *eig_M = nullptr, *eig_K = nullptr, *eig_d = nullptr, *eig_e = nullptr, *eig_dots = nullptr;
   double *eig_a = nullptr, *eig_z = nullptr, *eig_b = nullptr, *eig_x = nullptr, *eig_part = nullptr;
   int* eig_info = nullptr;
-  int bwd_dataflow = 1;  // 1: one-launch backward substitution (k_bwd_dataflow); 0: one launch per block
   int* bwd_flags = nullptr;
   int bwd_gen = 0;
-  int ruiz_full_rows = 0;  // 1: Ruiz sweeps over full rows of H (A/B reference for the lower-triangle sweep)
-  int chol_dataflow = 1;  // 1: persistent tile-DAG factorization (k_dataflow.hip); 0: kernel per step
   int ncu = 256;
   unsigned* df_tasks = nullptr;
   int df_ntasks = 0;
@@ -293,8 +289,7 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   // (measured ~22 us per block), UPDATE4 for its measured ~14 us plus the contention of a full chip.  With the
   // former 18 / 10 the simulated chain ran slower and the workers faster than on the device, so the emitted order
   // put TRSM(k+2, k) -- which the chain needs next -- behind trailing updates: 1.77 -> 1.57 ms per factorization.
-  double d_potrf = 10.0, d_trsm = 6.0, d_upd = 5.5, d_upd4 = 16.0;
-  if (const char* e = getenv("CVXG_DF_DUR")) sscanf(e, "%lf,%lf,%lf,%lf", &d_potrf, &d_trsm, &d_upd, &d_upd4);
+  const double d_potrf = 10.0, d_trsm = 6.0, d_upd = 5.5, d_upd4 = 16.0;
   for (int k = 0; k < nb; ++k) {  // (k, type) order is a topological order
     potrf_id[k] = (int)T.size();
     T.push_back({0, k, k, k, 1, d_potrf, 0, 0, k > 0 ? 1 : 0});
@@ -506,10 +501,7 @@ static void ruiz(cvxg_ctx* ctx) {
   for (int k = 0; k < RUIZ_MAX; ++k) {
     const double* dc = (k & 1) ? ctx->ruiz1 : ctx->ruiz0;
     double* dn = (k & 1) ? ctx->ruiz0 : ctx->ruiz1;
-    if (ctx->ruiz_full_rows)
-      launch_ruiz_sweep(s, ctx->H, ctx->np, ctx->n, dc, dn, ctx->ctrl, k);
-    else
-      launch_ruiz_sweep_tri(s, ctx->H, ctx->np, ctx->n, ctx->np, dc, dn, ctx->part, ctx->ctrl, k);
+    launch_ruiz_sweep_tri(s, ctx->H, ctx->np, ctx->n, ctx->np, dc, dn, ctx->part, ctx->ctrl, k);
   }
   launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl);
 }
@@ -523,27 +515,9 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs) {
   launch_ctrl_reset_chol(s, ctx->ctrl);
   launch_form_q(s, ctx->H, ctx->L, ctx->np, ctx->n, ctx->np, ctx->dfin, ctx->ctrl);
   fill_rhs();
-  // Two-level right-looking blocked Cholesky: outer panels of `chol_outer` 64-blocks.  Inside a panel each
-  // block is factored (potrf + fused forward solve), its column below is solved by MFMA TRSM and only the
-  // remaining panel columns are updated (K = 64); the trailing matrix is then updated once with K = the
-  // whole panel width, so it is read-modify-written nblk/chol_outer times instead of nblk times.
-  const int np = ctx->np, ow = ctx->chol_outer;
-  if (ctx->chol_dataflow) {
-    launch_chol_dataflow(s, ctx->L, np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
-                         ctx->df_ntasks, ctx->ncu, ctx->df_trace);
-  } else {
-    for (int K0 = 0; K0 < ctx->nblk; K0 += ow) {
-      const int K1 = std::min(K0 + ow, ctx->nblk);
-      for (int k = K0; k < K1; ++k) {
-        launch_potrf_diag(s, ctx->L, np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
-        launch_trsm_mfma(s, ctx->L, np, np, k, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl);
-        if (k + 1 < K1)
-          launch_chol_update(s, ctx->L, np, np, k * NB, NB, (k + 1) * NB, (k + 1) * NB, K1 * NB, ctx->ctrl);
-      }
-      if (K1 < ctx->nblk)
-        launch_chol_update(s, ctx->L, np, np, K0 * NB, (K1 - K0) * NB, K1 * NB, K1 * NB, np, ctx->ctrl);
-    }
-  }
+  // the whole factorization as one persistent launch over the 64 x 64 tile DAG (k_dataflow.hip)
+  launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
+                       ctx->df_ntasks, ctx->ncu, ctx->df_trace);
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
   if (ctx->hctrl->df_status != 0)
@@ -589,13 +563,8 @@ static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regula
 }
 
 static void backward_solve(cvxg_ctx* ctx, int nrhs) {
-  if (ctx->bwd_dataflow) {
-    launch_bwd_dataflow(ctx->s, ctx->L, ctx->np, ctx->Linv, ctx->rhs, ctx->sol, nrhs, ctx->nblk, ctx->bwd_flags,
-                        ++ctx->bwd_gen, ctx->ctrl);
-    return;
-  }
-  for (int k = ctx->nblk - 1; k >= 0; --k)
-    launch_bwd_step(ctx->s, ctx->L, ctx->np, ctx->Linv, k, ctx->rhs, ctx->sol, nrhs, ctx->ctrl);
+  launch_bwd_dataflow(ctx->s, ctx->L, ctx->np, ctx->Linv, ctx->rhs, ctx->sol, nrhs, ctx->nblk, ctx->bwd_flags,
+                      ++ctx->bwd_gen, ctx->ctrl);
 }
 
 // MatrixUtils.choleskySolve(H, b = -grad, tol) (MatrixUtils.scala:468-516); result in ctx->dx.
@@ -984,7 +953,8 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   *out = nullptr;
   if (n <= 0 || m < 0 || p < 0) return CVXG_E_DIM;
   if (p > CVXG_MAX_EQ) return CVXG_E_UNSUPPORTED;
-  if (n > 32767 * TILE) return CVXG_E_UNSUPPORTED;
+  // the dataflow Cholesky encodes tile indices in 10 bits (nblk <= 1023, n <= 65472; H alone is 34 GB there)
+  if (n > 1023 * NB) return CVXG_E_UNSUPPORTED;
   cvxg_ctx* ctx = new cvxg_ctx();
   *out = ctx;
   ctx->dev = device;
@@ -994,8 +964,6 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   ctx->np = round_up(n, TILE);
   ctx->mp = round_up(std::max(m, 1), MPAD);
   ctx->nblk = ctx->np / NB;
-  if (const char* e = getenv("CVXG_CHOL_OUTER")) ctx->chol_outer = std::max(1, atoi(e));
-  if (const char* e = getenv("CVXG_RUIZ_FULL")) ctx->ruiz_full_rows = atoi(e) != 0;  // A/B: full-row sweeps
   HIPC(ctx, hipSetDevice(device));
   HIPC(ctx, hipStreamCreateWithFlags(&ctx->s, hipStreamNonBlocking));
   const size_t np = ctx->np, mp = ctx->mp;
@@ -1028,32 +996,19 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   {  // dataflow Cholesky: task order for this tile count, work words
     (void)hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device);
     ctx->ncu = std::max(ctx->ncu, 1);
-    if (const char* e = getenv("CVXG_CHOL")) ctx->chol_dataflow = strcmp(e, "blocked") != 0;
-    if (ctx->nblk > 1023) ctx->chol_dataflow = 0;  // task encoding holds 10-bit tile indices
-    if (ctx->chol_dataflow) {
-      int group = 1, singles = 2;
-      if (const char* e = getenv("CVXG_DF_GROUP")) group = atoi(e) != 0;
-      if (const char* e = getenv("CVXG_DF_SINGLES")) singles = std::max(1, atoi(e));
-      // priority boost for the near-diagonal updates and next-row TRSMs the chain waits on: A/B at C3 (boost
-      // 0 / band 2 -> 100 / 3): Cholesky 1.553, 1.552, 1.556 -> 1.498, 1.529, 1.502 ms
-      int near = 0;
-      double boost = 100.0;
-      if (const char* e = getenv("CVXG_DF_NEAR")) near = std::max(0, atoi(e));
-      int band = 3;
-      if (const char* e = getenv("CVXG_DF_BOOST")) boost = atof(e);
-      if (const char* e = getenv("CVXG_DF_BAND")) band = atoi(e);
-      std::vector<unsigned> order = build_chol_schedule(ctx->nblk, ctx->ncu, group, singles, near, boost, band);
-      ctx->df_ntasks = (int)order.size();
-      CHK(dalloc(ctx, &ctx->df_tasks, order.size()));
-      CHK(copy_sync(ctx, ctx->df_tasks, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
-      CHK(dalloc(ctx, &ctx->df_work, chol_dataflow_work_ints(ctx->nblk)));
-      if (const char* e = getenv("CVXG_DF_TRACE")) {
-        ctx->df_trace_path = e;
-        CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk)));
-      }
+    // list schedule with four-panel update groups (the last two panels of a tile single) and a priority boost of
+    // 100 us for the near-diagonal updates and next-row TRSMs the chain waits on (band 3).  A/B at C3 (boost 0 /
+    // band 2 -> 100 / 3): Cholesky 1.553, 1.552, 1.556 -> 1.498, 1.529, 1.502 ms
+    std::vector<unsigned> order = build_chol_schedule(ctx->nblk, ctx->ncu, 1, 2, 0, 100.0, 3);
+    ctx->df_ntasks = (int)order.size();
+    CHK(dalloc(ctx, &ctx->df_tasks, order.size()));
+    CHK(copy_sync(ctx, ctx->df_tasks, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+    CHK(dalloc(ctx, &ctx->df_work, chol_dataflow_work_ints(ctx->nblk)));
+    if (const char* e = getenv("CVXG_DF_TRACE")) {  // instrumentation only: the task timeline of the last factorization
+      ctx->df_trace_path = e;
+      CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk)));
     }
   }
-  if (const char* e = getenv("CVXG_BWD")) ctx->bwd_dataflow = strcmp(e, "steps") != 0;
   CHK(dalloc(ctx, &ctx->bwd_flags, ctx->nblk));
   CHK(dalloc(ctx, &ctx->rhs, np * MAX_RHS));
   CHK(dalloc(ctx, &ctx->sol, np * MAX_RHS));
@@ -1068,7 +1023,6 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   const int kchunks = (int)(mp / KC);
   std::vector<int> tl = syrk_tile_plan(nt, slots, &ctx->ntiles_main);
   ctx->ntiles = (int)tl.size();
-  if (const char* e = getenv("CVXG_SYRK_NOTAIL")) ctx->ntiles_main = atoi(e) ? ctx->ntiles : ctx->ntiles_main;
   ctx->nsplit = syrk_nsplit(ctx, kchunks);
   CHK(dalloc(ctx, &ctx->tiles, tl.size()));
   CHK(copy_sync(ctx, ctx->tiles, tl.data(), tl.size() * sizeof(int), hipMemcpyHostToDevice));

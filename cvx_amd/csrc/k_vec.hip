@@ -227,48 +227,6 @@ void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl) {
   k_ruiz_init<<<(np + 255) / 256, 256, 0, s>>>(d0, np, ctrl);
 }
 
-__global__ __launch_bounds__(256) void k_ruiz_sweep(const double* __restrict__ H, int ld, int n,
-                                                    const double* __restrict__ dcur, double* __restrict__ dnext,
-                                                    DevCtrl* ctrl, int k) {
-  const double rho = __longlong_as_double((long long)ctrl->ruiz_rho[k]);
-  if (!(rho > 1e-6)) return;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n) return;
-  const double* hr = H + (size_t)row * ld;
-  // H and d are zero / one beyond n in the padded layout, so sweep whole 128-column groups (ld % 128 == 0)
-  const int ncol = (n + 127) & ~127;
-  vd2 a0 = {0.0, 0.0}, a1 = {0.0, 0.0};
-  int j = 2 * lane;
-  for (; j + 384 < ncol; j += 512) {
-    const vd2 h0 = *reinterpret_cast<const vd2*>(hr + j), h1 = *reinterpret_cast<const vd2*>(hr + j + 128);
-    const vd2 h2 = *reinterpret_cast<const vd2*>(hr + j + 256), h3 = *reinterpret_cast<const vd2*>(hr + j + 384);
-    const vd2 q0 = *reinterpret_cast<const vd2*>(dcur + j) * h0, q1 = *reinterpret_cast<const vd2*>(dcur + j + 128) * h1;
-    const vd2 q2 = *reinterpret_cast<const vd2*>(dcur + j + 256) * h2;
-    const vd2 q3 = *reinterpret_cast<const vd2*>(dcur + j + 384) * h3;
-    a0 = __builtin_elementwise_fma(q0, q0, a0);
-    a1 = __builtin_elementwise_fma(q1, q1, a1);
-    a0 = __builtin_elementwise_fma(q2, q2, a0);
-    a1 = __builtin_elementwise_fma(q3, q3, a1);
-  }
-  for (; j < ncol; j += 128) {
-    const vd2 q0 = *reinterpret_cast<const vd2*>(dcur + j) * *reinterpret_cast<const vd2*>(hr + j);
-    a0 = __builtin_elementwise_fma(q0, q0, a0);
-  }
-  const double ssum = wave_sum((a0[0] + a0[1]) + (a1[0] + a1[1]));
-  if (lane == 0) {
-    const double di = dcur[row];
-    const double u = sqrt(di * sqrt(ssum));        // sqrt(norm(Q(i,::)))   MatrixUtils.scala:258
-    const double v = (u > 0) ? 1.0 / u : 1.0;      // :259
-    dnext[row] = di * v;                           // :260
-    atomic_max_pos(&ctrl->ruiz_rho[k + 1], fabs(1.0 - u));  // :261-262
-  }
-}
-void launch_ruiz_sweep(hipStream_t s, const double* H, int ld, int n, const double* dcur, double* dnext,
-                       DevCtrl* ctrl, int k) {
-  k_ruiz_sweep<<<(n + 3) / 4, 256, 0, s>>>(H, ld, n, dcur, dnext, ctrl, k);
-}
-
 // Lower-triangle form of the sweep: H is exactly symmetric (the assembly mirrors its lower triangle), so
 // sum_j (d_j H_ij)^2 over a full row is assembled from the 64 x 64 tiles (I, J), J <= I, of the lower
 // triangle alone -- half the bytes per sweep.  Tile (I, J) writes

@@ -36,8 +36,6 @@ void launch_scale_vec(hipStream_t s, const double* u, const double* d, int n, do
 
 // ---- Ruiz equilibration + Q formation ------------------------------------------------------------
 void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl);
-void launch_ruiz_sweep(hipStream_t s, const double* H, int ld, int n, const double* dcur, double* dnext,
-                       DevCtrl* ctrl, int k);
 // The same sweep from the lower triangle only (64 x 64 tiles -> partials S[nbn][nbn*64] -> fixed-order row sums).
 void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np, const double* dcur, double* dnext,
                            double* S, DevCtrl* ctrl, int k);
@@ -86,27 +84,14 @@ void launch_pd_trials(hipStream_t s, const double* c, const double* e, const dou
 // H = t*P + A' diag(w) A over the lower tile list; split-K when nsplit > 1 (partials + ordered reduce).
 void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double* w, int mp, const double* P,
                           const DevCtrl* ctrl, double* H, int ldh, TileList tiles, int nsplit, double* partials);
-// Cholesky trailing update: C[r0:, r0:] (lower tiles) -= Pn Pn', Pn = C[r0:, k0:k0+64]
-void launch_syrk_update(hipStream_t s, double* C, int ld, int np, int k0, const DevCtrl* ctrl);
 
 // ---- Cholesky (k_chol.hip) ------------------------------------------------------------------------
-// diagonal block k: L_kk, L_kk^-1 (into Linv[k]) and the fused forward solve of the nrhs rhs columns
-void launch_potrf_diag(hipStream_t s, double* L, int ld, int k, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl);
-void launch_trsm_panel(hipStream_t s, double* L, int ld, int np, int k, double* rhs, int nrhs, const double* Linv,
-                       const DevCtrl* ctrl);
-// k_update.hip: MFMA panel TRSM (rows below block k) and the region update of the two-level Cholesky
-void launch_trsm_mfma(hipStream_t s, double* L, int ld, int np, int k, double* rhs, int nrhs, const double* Linv,
-                      const DevCtrl* ctrl);
-void launch_chol_update(hipStream_t s, double* C, int ld, int np, int k0, int kw, int r0, int c0, int c1,
-                        const DevCtrl* ctrl);
 // k_dataflow.hip: the whole factorization (potrf + trsm + updates + fused forward solve) as one persistent
 // launch over the 64x64 tile DAG in the host-built task order (build_chol_schedule in cvxg.cpp)
 size_t chol_dataflow_work_ints(int nblk);
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */);
-void launch_bwd_step(hipStream_t s, const double* L, int ld, const double* Linv, int k, double* rhs,
-                     double* out, int nrhs, const DevCtrl* ctrl);
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
 void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,
                          int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl);

@@ -251,13 +251,8 @@ __device__ bool potrf64_factor(double* __restrict__ L, int ld, int k, double* __
       double rinv = rcp_nr(piv);
       double mypiv = 1.0;  // lane j keeps p_j: the column scales p_j^-1/2 are formed once, after the sweep
       double pmin = piv;   // min_j L_jj = sqrt(min_j p_j)
-#ifdef P64_NO_SWEEP  // timing experiment only: the glue without the 16-column elimination (wrong results)
-#pragma unroll 1
-      for (int j = 0; j < 0; ++j) {
-#else
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-#endif
         double lc[16];
 #pragma unroll
         for (int c = j + 1; c < 16; ++c) lc[c] = readlane_d(a[j], c);  // D_cj, c > j (lower: lane c, column j)

@@ -94,7 +94,8 @@ typedef struct cvxg_solution {
 
 /* ---- context ------------------------------------------------------------------------------------ */
 
-/* Allocate a context on HIP device `device` for n variables, m linear inequalities, p equalities. */
+/* Allocate a context on HIP device `device` for n variables, m linear inequalities, p equalities.
+ * n <= 65472 (1023 Cholesky blocks of 64; CVXG_E_UNSUPPORTED above). */
 int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out);
 void cvxg_destroy(cvxg_ctx* ctx);
 const char* cvxg_last_error(const cvxg_ctx* ctx);  /* NULL: the last error of a context-free call (this thread) */
