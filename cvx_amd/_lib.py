@@ -42,7 +42,7 @@ class cvxg_step_info(C.Structure):
                 ("norm_grad_new", C.c_double), ("equality_gap", C.c_double),
                 ("backtracks_c", C.c_int), ("backtracks_armijo", C.c_int), ("fallback", C.c_int),
                 ("ruiz_sweeps", C.c_int), ("regularized", C.c_int), ("took_step", C.c_int), ("done", C.c_int),
-                ("iter", C.c_int)]
+                ("iter", C.c_int), ("ls_fresh", C.c_int), ("ls_ties", C.c_int)]
 
 
 class cvxg_centering_info(C.Structure):
@@ -90,6 +90,7 @@ SIGNATURES = {
     "cvxg_newton_direction": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, _D, _D, _D, _D,
                                         C.POINTER(cvxg_step_info)]),
     "cvxg_centering_begin": (C.c_int, [_P, C.c_double]),
+    "cvxg_centering_resume": (C.c_int, [_P, C.c_double, C.c_int, C.c_double, _D]),
     "cvxg_newton_step": (C.c_int, [_P, C.POINTER(cvxg_params), C.POINTER(cvxg_step_info)]),
     "cvxg_centering": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, C.POINTER(cvxg_centering_info)]),
     "cvxg_barrier_solve": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_int, C.POINTER(cvxg_solution)]),

@@ -23,7 +23,10 @@ def needs_build() -> bool:
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and not needs_build():
         return OUT
-    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+    # -ffp-contract=off: every a*b+c is rounded twice unless the source says fma(), so the elementwise steps the
+    # reference evaluates as separate Breeze operations (x + s*t, d*d, t*(a + Px) + ...) keep its roundings;
+    # the dot products and MFMA accumulations use explicit fma / MFMA builtins.
+    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall",
            "-Wno-pass-failed", "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + [
         "-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:

@@ -44,6 +44,18 @@ enum {
   SC_RES2B,     // second KKT residual |A x - b|^2
   SC_B2,        // |b|^2 (KKT)
   SC_KLSUM,     // KL dual: sum_j R exp(-(B'z)_j)
+  // magnitudes for the certified line-search decisions (cvxg.cpp: line_search)
+  SC_A0XA,      // |a0| . |x|
+  SC_XPXA,      // |x| . |P| |x|
+  SC_A0SA,      // |a0| . |s|
+  SC_SPXA,      // |s| . |P| |x|
+  SC_SPSA,      // |s| . |P| |s|
+  SC_CAINV,     // sum_i cabs_i / d_i at x
+  SC_LOGABS,    // sum_i |log d_i| at x
+  // a fresh evaluation of one trial point (line_search: ambiguous trials)
+  SC_TR_A0X,    // a0 . xt
+  SC_TR_XPX,    // xt . P xt
+  SC_TR_SUMLOG, // sum_i log d_i(xt)
   SC_COUNT
 };
 

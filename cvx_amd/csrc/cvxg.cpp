@@ -65,8 +65,13 @@ struct cvxg_ctx {
   double* part = nullptr;
   size_t part_bytes = 0;
   double *kB = nullptr, *kw = nullptr, *kx = nullptr, *kz = nullptr;
-  double *ls_plog = nullptr, *ls_log = nullptr;
+  double *ls_plog = nullptr, *ls_log = nullptr, *ls_paux = nullptr;
   int *ls_pcnt = nullptr, *ls_cnt = nullptr;
+  // certified line-search decisions: |r| + |a|.|x| per row, |a|.|s| per row, |P||x|, |P||s|; the fresh evaluation of
+  // an ambiguous trial point xt = x + s t goes to its own buffers (the batch keeps reading c and e)
+  double *cabs = nullptr, *eabs = nullptr, *Pxa = nullptr, *Psa = nullptr;
+  double *xtr = nullptr, *Pxtr = nullptr, *c_tr = nullptr, *d_tr = nullptr, *invd_tr = nullptr, *w_tr = nullptr,
+         *logd_tr = nullptr;
   int* tiles = nullptr;
   int ntiles = 0, nsplit = 1;
   int ntiles_main = 0;  // tiles assembled without K split (whole waves of slots); the rest use nsplit
@@ -108,7 +113,7 @@ struct cvxg_ctx {
   std::string df_trace_path;
   DevCtrl* ctrl = nullptr;
   DevCtrl* hctrl = nullptr;
-  double* hls = nullptr;  // pinned: [LS_TRIALS] logs then [2*LS_TRIALS] counts as ints
+  double* hls = nullptr;  // pinned: [3*LS_TRIALS] {log sum, its error bound, sum |log|} then [4*LS_TRIALS] counts as ints
   // centering state
   double t = 1.0;
   int iter = 0;
@@ -394,6 +399,10 @@ static double objective_from_ctrl(const cvxg_ctx* ctx, const DevCtrl& h) {
 
 // c = g(x), d, 1/d, 1/d^2, log d at ctx->x; QuadraticConstraint rows add x'P_k x / 2 (P_k x kept in qPx for the
 // gradient, the Hessian rows and the line search).
+// Certified line-search decisions cover linear constraints with a linear / quadratic objective (the configs of
+// BASELINE.json); QuadraticConstraint rows and the KL dual keep the plain trial arithmetic.
+static bool ls_certified(const cvxg_ctx* ctx) { return ctx->m > 0 && ctx->nq == 0 && !ctx->kl; }
+
 static void constraint_eval_all(cvxg_ctx* ctx) {
   const int np = ctx->np;
   if (ctx->nq > 0) {
@@ -401,7 +410,8 @@ static void constraint_eval_all(cvxg_ctx* ctx) {
     launch_quad_xpx(ctx->s, ctx->qPx, ctx->x, ctx->qrows, ctx->nq, np, ctx->qextra);
   }
   launch_constraint_eval(ctx->s, ctx->A, np, ctx->mp, np, ctx->x, ctx->r, ctx->ub, ctx->c, ctx->d, ctx->invd, ctx->w,
-                         ctx->logd, ctx->ctrl, ctx->nq > 0 ? ctx->qextra : nullptr);
+                         ctx->logd, ctx->ctrl, ctx->nq > 0 ? ctx->qextra : nullptr,
+                         ls_certified(ctx) ? ctx->cabs : nullptr);
 }
 
 // Barrier value / gradient pieces at the current x and ctrl->t (BarrierSolver.scala:280-301):
@@ -412,7 +422,11 @@ static int eval_at_x(cvxg_ctx* ctx) {
   launch_ctrl_reset_eval(s, ctx->ctrl);
   constraint_eval_all(ctx);
   const bool quad = ctx->hasP && !ctx->kl;
-  if (quad) launch_rowdot(s, ctx->P, np, np, np, ctx->x, ctx->Px);
+  const bool cert = ls_certified(ctx);
+  if (quad) {
+    if (cert) launch_rowdot_abs(s, ctx->P, np, np, np, ctx->x, ctx->Px, ctx->Pxa);
+    else launch_rowdot(s, ctx->P, np, np, np, ctx->x, ctx->Px);
+  }
   if (ctx->kl) {  // v = B'z, y = R exp(-v), -B y (the KL dual gradient is w - B y), sum_j y_j
     launch_rowdot(s, ctx->KB, np, ctx->noutp, np, ctx->x, ctx->kl_v);
     launch_kl_eval(s, ctx->kl_v, ctx->nout, ctx->noutp, ctx->kl_R, ctx->kl_y);
@@ -429,6 +443,17 @@ static int eval_at_x(cvxg_ctx* ctx) {
   if (quad) launch_dot(s, ctx->x, ctx->Px, np, ctx->ctrl, SC_XPX);
   launch_sum(s, ctx->logd, mp, ctx->ctrl, SC_SUMLOG);
   launch_dot(s, ctx->y, nullptr, np, ctx->ctrl, SC_GG);
+  if (cert) {  // error scales of f(x): |a0|.|x|, |x|.|P||x|, sum cabs/d, sum |log d|
+    AbsDots ad{};
+    auto add = [&](const double* u, const double* v, int len, int slot) {
+      ad.u[ad.count] = u, ad.v[ad.count] = v, ad.n[ad.count] = len, ad.slot[ad.count] = slot, ++ad.count;
+    };
+    add(ctx->a0, ctx->x, np, SC_A0XA);
+    if (quad) add(ctx->x, ctx->Pxa, np, SC_XPXA);
+    add(ctx->cabs, ctx->invd, mp, SC_CAINV);
+    add(ctx->logd, nullptr, mp, SC_LOGABS);
+    launch_dots_abs(s, ad, ctx->ctrl);
+  }
   if (ctx->p > 0) {
     launch_rowdot(s, ctx->Aeq, np, ctx->p, np, ctx->x, ctx->eqtmp);
     launch_axpy(s, ctx->beq, ctx->eqtmp, -1.0, ctx->p, ctx->eqd);  // b - A*x
@@ -804,9 +829,16 @@ static int newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_in
 struct TrialBatch {
   int k0 = -1;
   double logs[LS_TRIALS];
-  double kl[LS_TRIALS];  // KL dual: sum_j R exp(-(B'(x + t_k s))_j)
-  int viol[LS_TRIALS], npos[LS_TRIALS];
+  double lerr[LS_TRIALS];  // certified mode: bound of the log-sum error (inf: not certifiable)
+  double labs[LS_TRIALS];  // certified mode: sum |log d_i|
+  double kl[LS_TRIALS];    // KL dual: sum_j R exp(-(B'(x + t_k s))_j)
+  int viol[LS_TRIALS], npos[LS_TRIALS], sure[LS_TRIALS], amb[LS_TRIALS];
 };
+
+static constexpr double U53 = 1.1102230246251565e-16;  // unit roundoff 2^-53
+// gamma of the certified trial decisions: |fl(a.v) - a.v| <= (cols + 2) u |a|.|v| for any summation order, with a 4x
+// margin and room for the few roundings around the dot (r +, x + s t, ub -)
+static double ls_gamma(const cvxg_ctx* ctx) { return 4.0 * (ctx->np + 16) * U53; }
 
 static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch* b) {
   if (ctx->m == 0) {  // no inequality constraints: every trial is in C and contributes no log terms
@@ -816,7 +848,10 @@ static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch
       HIPC(ctx, hipStreamSynchronize(ctx->s));
     }
     b->k0 = k0;
-    for (int k = 0; k < LS_TRIALS; ++k) b->logs[k] = 0.0, b->viol[k] = 0, b->npos[k] = 0;
+    for (int k = 0; k < LS_TRIALS; ++k) {
+      b->logs[k] = b->lerr[k] = b->labs[k] = 0.0;
+      b->viol[k] = b->npos[k] = b->sure[k] = b->amb[k] = 0;
+    }
     return CVXG_OK;
   }
   if (ctx->kl) {
@@ -824,43 +859,110 @@ static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch
     HIPC(ctx, hipMemcpyAsync(b->kl, ctx->kl_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
   }
   const int nb = ls_blocks(ctx->m);
+  const bool cert = ls_certified(ctx);
   launch_ls_trials(ctx->s, ctx->c, ctx->e, ctx->ub, ctx->m, tbase, beta, ctx->ls_plog, ctx->ls_pcnt,
-                   ctx->nq > 0 ? ctx->qf : nullptr);
-  launch_ls_finalize(ctx->s, ctx->ls_plog, ctx->ls_pcnt, nb, ctx->ls_log, ctx->ls_cnt);
+                   ctx->nq > 0 ? ctx->qf : nullptr, cert ? ctx->cabs : nullptr, ctx->eabs, ls_gamma(ctx),
+                   ctx->ls_paux);
+  launch_ls_finalize(ctx->s, ctx->ls_plog, ctx->ls_pcnt, ctx->ls_paux, nb, ctx->ls_log, ctx->ls_cnt);
   HIPC(ctx, hipGetLastError());
-  HIPC(ctx, hipMemcpyAsync(ctx->hls, ctx->ls_log, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
-  HIPC(ctx, hipMemcpyAsync((int*)(ctx->hls + LS_TRIALS), ctx->ls_cnt, 2 * LS_TRIALS * sizeof(int),
+  HIPC(ctx, hipMemcpyAsync(ctx->hls, ctx->ls_log, 3 * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
+  HIPC(ctx, hipMemcpyAsync((int*)(ctx->hls + 3 * LS_TRIALS), ctx->ls_cnt, 4 * LS_TRIALS * sizeof(int),
                            hipMemcpyDeviceToHost, ctx->s));
   HIPC(ctx, hipStreamSynchronize(ctx->s));
   b->k0 = k0;
-  memcpy(b->logs, ctx->hls, sizeof(b->logs));
-  const int* cnt = (const int*)(ctx->hls + LS_TRIALS);
+  const int* cnt = (const int*)(ctx->hls + 3 * LS_TRIALS);
   for (int k = 0; k < LS_TRIALS; ++k) {
-    b->viol[k] = cnt[2 * k];
-    b->npos[k] = cnt[2 * k + 1];
+    b->logs[k] = ctx->hls[3 * k];
+    b->lerr[k] = ctx->hls[3 * k + 1];
+    b->labs[k] = ctx->hls[3 * k + 2];
+    b->viol[k] = cnt[4 * k];
+    b->npos[k] = cnt[4 * k + 1];
+    b->sure[k] = cnt[4 * k + 2];
+    b->amb[k] = cnt[4 * k + 3];
   }
+  return CVXG_OK;
+}
+
+// The reference's own evaluation of one trial point (UnconstrainedSolver.scala:93,102,107): xt = x + s*t, then
+// isInSet(xt) (Constraint.scala:23 for every row) and barrierFunction(t, xt) (BarrierSolver.scala:280-289), through the
+// same kernels and summation order as the barrier value at x.  Used for the trials whose batch margin is inside the
+// rounding band (line_search).
+struct FreshTrial {
+  int viol = 0, npos = 0;
+  double fv = 0.0;
+};
+static int trial_fresh(cvxg_ctx* ctx, double tt, FreshTrial* out) {
+  hipStream_t s = ctx->s;
+  const int np = ctx->np, mp = ctx->mp;
+  launch_axpy(s, ctx->x, ctx->sdir, tt, np, ctx->xtr);  // x + s*t (contraction off: two roundings, as Breeze)
+  launch_ctrl_reset_eval(s, ctx->ctrl);
+  launch_constraint_eval(s, ctx->A, np, mp, np, ctx->xtr, ctx->r, ctx->ub, ctx->c_tr, ctx->d_tr, ctx->invd_tr, ctx->w_tr,
+                         ctx->logd_tr, ctx->ctrl, nullptr, nullptr);
+  launch_sum(s, ctx->logd_tr, mp, ctx->ctrl, SC_TR_SUMLOG);
+  launch_dot(s, ctx->a0, ctx->xtr, np, ctx->ctrl, SC_TR_A0X);
+  const bool quad = ctx->hasP && !ctx->kl;
+  if (quad) {
+    launch_rowdot(s, ctx->P, np, np, np, ctx->xtr, ctx->Pxtr);
+    launch_dot(s, ctx->xtr, ctx->Pxtr, np, ctx->ctrl, SC_TR_XPX);
+  }
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  const DevCtrl& h = *ctx->hctrl;
+  const double f0 = ctx->r0 + h.sc[SC_TR_A0X] + (quad ? h.sc[SC_TR_XPX] / 2 : 0.0);
+  out->fv = ctx->t * f0 - h.sc[SC_TR_SUMLOG];
+  out->viol = h.not_strict;
+  out->npos = h.infeasible;
   return CVXG_OK;
 }
 
 // Backtracking from x along s (device ctx->sdir).  limit = 200 / throw_at = 100 (Unconstrained) or
 // 100 / 100 (EqualityConstrained).  Returns the accepted t and the two counters.
+//
+// Trials are scored in batches of LS_TRIALS from c = g(x) and e = A s (g(x + t s) = c + t e, O(m) per trial).  With
+// linear constraints (ls_certified) the batch also bounds how far its arithmetic and the reference's fresh evaluation
+// valueAt(x + s*t) can each lie from the exact value (any FP64 summation order), so every decision whose margin
+// exceeds that band is the one any evaluation order makes.  Inside the band:
+//  * feasibility (isInSet, Constraint.scala:23): the trial is evaluated fresh on the device (trial_fresh), exactly as
+//    the reference forms it, and decided from that (*fresh counts these) -- a wrong "in C" would leave the domain;
+//  * Armijo (UnconstrainedSolver.scala:107): |f(x + s t) - f - alpha t q| is below the rounding error of f itself, so
+//    the decision is rounding noise in every implementation (numpy, Breeze and a fresh device evaluation disagree
+//    among themselves).  It is taken from the batch value and counted in *ties.  (Deciding these from a fresh
+//    evaluation was measured: late in the path -- t = 1e10 -- the noise then rejected trial after trial and a
+//    centering ran into maxIter.)
 static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int limit, double* t_out, int* k_c,
-                       int* k_a) {
+                       int* k_a, int* fresh, int* ties) {
   hipStream_t s = ctx->s;
   const double beta = pars->beta, alpha = pars->alpha;
-  // e = A s, and the quadratic pieces of f0(x + s t)
-  if (ctx->m > 0) launch_rowdot(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e);
+  const bool cert = ls_certified(ctx);
+  const bool quad = ctx->hasP && !ctx->kl;
+  // e = A s (and |A||s|), and the quadratic pieces of f0(x + s t)
+  if (ctx->m > 0) {
+    if (cert) launch_rowdot_abs(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e, ctx->eabs);
+    else launch_rowdot(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e);
+  }
   if (ctx->nq > 0) {  // e_k = G_k.s and f_k = s'P_k s: g_k(x + t s) = g_k + t e_k + t^2 f_k / 2
     launch_rowdot(s, ctx->Pq, ctx->np, ctx->nq * ctx->np, ctx->np, ctx->sdir, ctx->qPs);
     launch_quad_ls(s, ctx->qPx, ctx->qPs, ctx->sdir, ctx->qrows, ctx->nq, ctx->np, ctx->e, ctx->qf);
   }
   launch_dot(s, ctx->a0, ctx->sdir, ctx->np, ctx->ctrl, SC_A0S);
   if (ctx->kl) launch_rowdot(s, ctx->KB, ctx->np, ctx->noutp, ctx->np, ctx->sdir, ctx->kl_u);  // u = B's
-  const bool quad = ctx->hasP && !ctx->kl;
   if (quad) {
-    launch_rowdot(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps);
+    if (cert) launch_rowdot_abs(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps, ctx->Psa);
+    else launch_rowdot(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps);
     launch_dot(s, ctx->sdir, ctx->Px, ctx->np, ctx->ctrl, SC_SPX);
     launch_dot(s, ctx->sdir, ctx->Ps, ctx->np, ctx->ctrl, SC_SPS);
+  }
+  if (cert) {
+    AbsDots ad{};
+    auto add = [&](const double* u, const double* v, int slot) {
+      ad.u[ad.count] = u, ad.v[ad.count] = v, ad.n[ad.count] = ctx->np, ad.slot[ad.count] = slot, ++ad.count;
+    };
+    add(ctx->a0, ctx->sdir, SC_A0SA);
+    if (quad) {
+      add(ctx->sdir, ctx->Pxa, SC_SPXA);
+      add(ctx->sdir, ctx->Psa, SC_SPSA);
+    }
+    launch_dots_abs(s, ad, ctx->ctrl);
   }
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
@@ -872,6 +974,15 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
     if (quad) v += (h.sc[SC_XPX] + 2 * tt * h.sc[SC_SPX] + tt * tt * h.sc[SC_SPS]) / 2;
     return v;
   };
+  // error bounds (certified mode) of the objective part at x + s tt and of the barrier value f at x
+  const double gam = ls_gamma(ctx);
+  auto ef0_at = [&](double tt) {
+    double v = fabs(ctx->r0) + h.sc[SC_A0XA] + tt * h.sc[SC_A0SA];
+    if (quad) v += (h.sc[SC_XPXA] + 2 * tt * h.sc[SC_SPXA] + tt * tt * h.sc[SC_SPSA]) / 2;
+    return gam * v;
+  };
+  const double ef_x = tb * ef0_at(0.0) + 2.0 * gam * h.sc[SC_CAINV] + (ctx->mp + 8) * U53 * h.sc[SC_LOGABS] +
+                      8 * U53 * fabs(f);
   TrialBatch b;
   double tcur = 1.0;
   double tbatch = 1.0;  // t at the start of the next batch (products of beta, UnconstrainedSolver.scala:93)
@@ -884,12 +995,30 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
     }
     return CVXG_OK;
   };
+  int fresh_it = -1;  // trial index of the cached fresh evaluation
+  FreshTrial fr;
+  auto fresh_at = [&](int it) -> int {
+    if (fresh_it != it) {
+      CHK(trial_fresh(ctx, tcur, &fr));
+      fresh_it = it;
+      ++*fresh;
+    }
+    return CVXG_OK;
+  };
   int it = 0;
   // while (!C.isInSet(x + s*t) && it < limit) { t *= beta; it += 1 }
   while (true) {
     if (it >= limit) break;
     CHK(ensure(it));
-    if (b.viol[it - b.k0] == 0) break;
+    const int j = it - b.k0;
+    bool in_set;
+    if (!cert || b.sure[j] > 0 || b.amb[j] == 0) {
+      in_set = b.viol[j] == 0;
+    } else {
+      CHK(fresh_at(it));
+      in_set = fr.viol == 0;
+    }
+    if (in_set) break;
     tcur *= beta;
     ++it;
   }
@@ -899,10 +1028,18 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
   while (it < limit) {
     CHK(ensure(it));
     const int j = it - b.k0;
-    if (b.npos[j] > 0)
+    int npos = b.npos[j];
+    double fv = tb * f0_at(tcur, b.kl[j]) - b.logs[j];
+    const double thr = f + alpha * tcur * q;
+    if (cert) {
+      if (fresh_it == it) npos = fr.npos;  // this trial's feasibility was decided fresh: its d > 0 test too
+      const double efv = tb * ef0_at(tcur) + b.lerr[j] + (ctx->mp + 8) * U53 * b.labs[j] + 8 * U53 * fabs(fv);
+      const double ethr = ef_x + 8 * U53 * (fabs(f) + fabs(alpha * tcur * q));
+      if (!(fabs(fv - thr) > efv + ethr)) ++*ties;  // a tie: decided by the batch value (see above)
+    }
+    if (npos > 0)
       return set_err(ctx, CVXG_E_INFEASIBLE_X, "barrierFunction: x not strictly feasible in line search");
-    const double fv = tb * f0_at(tcur, b.kl[j]) - b.logs[j];
-    if (!(fv > f + alpha * tcur * q)) break;
+    if (!(fv > thr)) break;
     tcur *= beta;
     ++it;
   }
@@ -1032,12 +1169,16 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   CHK(dalloc(ctx, &ctx->part, part));
   const int lsb = ls_blocks(std::max(m, 1));
   CHK(dalloc(ctx, &ctx->ls_plog, (size_t)lsb * LS_TRIALS));
-  CHK(dalloc(ctx, &ctx->ls_pcnt, (size_t)lsb * LS_TRIALS * 2));
-  CHK(dalloc(ctx, &ctx->ls_log, LS_TRIALS));
-  CHK(dalloc(ctx, &ctx->ls_cnt, 2 * LS_TRIALS));
+  CHK(dalloc(ctx, &ctx->ls_paux, (size_t)lsb * LS_TRIALS * 2));
+  CHK(dalloc(ctx, &ctx->ls_pcnt, (size_t)lsb * LS_TRIALS * 4));
+  CHK(dalloc(ctx, &ctx->ls_log, 3 * LS_TRIALS));
+  CHK(dalloc(ctx, &ctx->ls_cnt, 4 * LS_TRIALS));
+  for (double** v : {&ctx->Pxa, &ctx->Psa, &ctx->xtr, &ctx->Pxtr}) CHK(dalloc(ctx, v, np));
+  for (double** v : {&ctx->cabs, &ctx->eabs, &ctx->c_tr, &ctx->d_tr, &ctx->invd_tr, &ctx->w_tr, &ctx->logd_tr})
+    CHK(dalloc(ctx, v, mp));
   CHK(dalloc(ctx, &ctx->ctrl, 1));
   HIPC(ctx, hipHostMalloc((void**)&ctx->hctrl, sizeof(DevCtrl), hipHostMallocDefault));
-  HIPC(ctx, hipHostMalloc((void**)&ctx->hls, 3 * LS_TRIALS * sizeof(double), hipHostMallocDefault));
+  HIPC(ctx, hipHostMalloc((void**)&ctx->hls, 5 * LS_TRIALS * sizeof(double), hipHostMallocDefault));
   memset(ctx->hctrl, 0, sizeof(DevCtrl));
   for (int i = 0; i < NT; ++i) {
     HIPC(ctx, hipEventCreate(&ctx->tm.ev[i][0]));
@@ -1062,7 +1203,8 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->sp_pq, ctx->sp_row, ctx->sp_coef, ctx->kl_spart, ctx->lam, ctx->dlam, ctx->pd_rc,
                   ctx->pd_w, ctx->pd_rhs, ctx->pd_d1, ctx->pd_R0, ctx->pd_R1, ctx->pd_tmp, ctx->pd_part_rows,
                   ctx->pd_part_cols, ctx->pd_out, ctx->qrows, ctx->qslot, ctx->Pq, ctx->qPx, ctx->qPs,
-                  ctx->qextra, ctx->qf, ctx->aff_F, ctx->aff_z0};
+                  ctx->qextra, ctx->qf, ctx->aff_F, ctx->aff_z0, ctx->ls_paux, ctx->cabs, ctx->eabs, ctx->Pxa,
+                  ctx->Psa, ctx->xtr, ctx->Pxtr, ctx->c_tr, ctx->d_tr, ctx->invd_tr, ctx->w_tr, ctx->logd_tr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
@@ -1422,6 +1564,25 @@ int cvxg_centering_begin(cvxg_ctx* ctx, double t) {
   return CVXG_OK;
 }
 
+int cvxg_centering_resume(cvxg_ctx* ctx, double t, int iter, double trust_radius, const double* grad) {
+  if (!ctx || iter < 0) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  CHK(check_ready(ctx));
+  CHK(set_t(ctx, t));
+  ctx->iter = iter;
+  ctx->trust = iter == 0 ? NAN : trust_radius;
+  ctx->began = 1;
+  CHK(eval_at_x(ctx));
+  if (grad) {  // the host's y (UnconstrainedSolver.scala:44,131): replaces the engine's gradient for this iteration
+    double gg = 0.0;
+    for (int i = 0; i < ctx->n; ++i) gg += grad[i] * grad[i];
+    CHK(upload_vec(ctx, ctx->y, grad, ctx->n, ctx->np));
+    ctx->normGrad = sqrt(gg);
+  }
+  ctx->nd = std::numeric_limits<double>::infinity();  // tol + 1 at the next cvxg_newton_step
+  return CVXG_OK;
+}
+
 int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
   if (!ctx || !pars) return CVXG_E_ARG;
   HIPC(ctx, hipSetDevice(ctx->dev));
@@ -1467,8 +1628,10 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
       launch_axpy_strided(ctx->s, nullptr, ctx->dx, 1, 0, scale, ctx->np, ctx->sdir);  // d * (radius/hNorm)
     }
     double tacc = 1.0;
-    int kc = 0, ka = 0;
-    rc = line_search(ctx, pars, q, limit, &tacc, &kc, &ka);
+    int kc = 0, ka = 0, fresh = 0, ties = 0;
+    rc = line_search(ctx, pars, q, limit, &tacc, &kc, &ka, &fresh, &ties);
+    info->ls_fresh = fresh;
+    info->ls_ties = ties;
     tstop(ctx, 4);
     if (rc != CVXG_OK) return rc;
     launch_axpy(ctx->s, ctx->x, ctx->sdir, tacc, ctx->np, ctx->x);  // x = x + s*t

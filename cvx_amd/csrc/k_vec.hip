@@ -36,18 +36,36 @@ __device__ __forceinline__ double row_dot_wave(const double* __restrict__ row, c
   return wave_sum((acc0[0] + acc0[1]) + (acc1[0] + acc1[1]));
 }
 
+// a.v and |a|.|v| in one sweep (the abs dot bounds the rounding error of every evaluation order of a.v: the
+// line search's certified trial decisions, cvxg.cpp: line_search).
+__device__ __forceinline__ double row_dot_wave_abs(const double* __restrict__ row, const double* __restrict__ v,
+                                                   int cols, int lane, double* absdot) {
+  vd2 acc = {0.0, 0.0}, aab = {0.0, 0.0};
+  for (int j = 2 * lane; j < cols; j += 128) {
+    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), b0 = *reinterpret_cast<const vd2*>(v + j);
+    acc = __builtin_elementwise_fma(a0, b0, acc);
+    aab = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(b0), aab);
+  }
+  *absdot = wave_sum(aab[0] + aab[1]);
+  return wave_sum(acc[0] + acc[1]);
+}
+
 __global__ __launch_bounds__(256) void k_constraint_eval(const double* __restrict__ A, int ld, int mp, int cols,
                                                          const double* __restrict__ x,
                                                          const double* __restrict__ r,
                                                          const double* __restrict__ ub, double* __restrict__ c,
                                                          double* __restrict__ d, double* __restrict__ invd,
                                                          double* __restrict__ w, double* __restrict__ logd,
-                                                         DevCtrl* ctrl, const double* __restrict__ extra) {
+                                                         DevCtrl* ctrl, const double* __restrict__ extra,
+                                                         double* __restrict__ cabs) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= mp) return;
-  const double dot = row_dot_wave(A + (size_t)row * ld, x, cols, lane);
+  double adot = 0.0;
+  const double dot = cabs ? row_dot_wave_abs(A + (size_t)row * ld, x, cols, lane, &adot)
+                          : row_dot_wave(A + (size_t)row * ld, x, cols, lane);
   if (lane == 0) {
+    if (cabs) cabs[row] = fabs(r[row]) + adot;  // |r| + |a|.|x|: scale of the rounding error of r + a.x
     // r + (a dot x)  (LinearConstraint.scala:23), + (x dot P x)/2 for a QuadraticConstraint row (:31)
     const double ci = extra ? (r[row] + dot) + extra[row] : r[row] + dot;
     const double di = ub[row] - ci;          // d = ub - valueAt(x)    BarrierSolver.scala:283
@@ -63,8 +81,8 @@ __global__ __launch_bounds__(256) void k_constraint_eval(const double* __restric
 
 void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int n_cols, const double* x,
                             const double* r, const double* ub, double* c, double* d, double* invd,
-                            double* w, double* logd, DevCtrl* ctrl, const double* extra) {
-  k_constraint_eval<<<(mp + 3) / 4, 256, 0, s>>>(A, ld, mp, n_cols, x, r, ub, c, d, invd, w, logd, ctrl, extra);
+                            double* w, double* logd, DevCtrl* ctrl, const double* extra, double* cabs) {
+  k_constraint_eval<<<(mp + 3) / 4, 256, 0, s>>>(A, ld, mp, n_cols, x, r, ub, c, d, invd, w, logd, ctrl, extra, cabs);
 }
 
 __global__ __launch_bounds__(256) void k_rowdot(const double* __restrict__ M, int ld, int rows, int cols,
@@ -78,6 +96,24 @@ __global__ __launch_bounds__(256) void k_rowdot(const double* __restrict__ M, in
 
 void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y) {
   k_rowdot<<<(rows + 3) / 4, 256, 0, s>>>(M, ld, rows, cols, v, y);
+}
+
+__global__ __launch_bounds__(256) void k_rowdot_abs(const double* __restrict__ M, int ld, int rows, int cols,
+                                                    const double* __restrict__ v, double* __restrict__ y,
+                                                    double* __restrict__ yabs) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  double adot;
+  const double dot = row_dot_wave_abs(M + (size_t)row * ld, v, cols, lane, &adot);
+  if (lane == 0) {
+    y[row] = dot;
+    yabs[row] = adot;
+  }
+}
+void launch_rowdot_abs(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y,
+                       double* yabs) {
+  k_rowdot_abs<<<(rows + 3) / 4, 256, 0, s>>>(M, ld, rows, cols, v, y, yabs);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -150,6 +186,31 @@ __global__ __launch_bounds__(1024) void k_sum(const double* __restrict__ u, int 
   if (threadIdx.x == 0) ctrl->sc[slot] = acc;
 }
 
+__global__ __launch_bounds__(1024) void k_dot_abs(const double* __restrict__ u, const double* __restrict__ v, int n,
+                                                  DevCtrl* ctrl, int slot) {
+  __shared__ double red[16];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc = fma(fabs(u[i]), v ? fabs(v[i]) : 1.0, acc);
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) ctrl->sc[slot] = acc;
+}
+void launch_dot_abs(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot) {
+  k_dot_abs<<<1, 1024, 0, s>>>(u, v, n, ctrl, slot);
+}
+// up to 4 independent |u|.|v| sums in one launch (one block each)
+__global__ __launch_bounds__(1024) void k_dots_abs(AbsDots a, DevCtrl* ctrl) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  const double* u = a.u[b];
+  const double* v = a.v[b];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < a.n[b]; i += blockDim.x) acc = fma(fabs(u[i]), v ? fabs(v[i]) : 1.0, acc);
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) ctrl->sc[a.slot[b]] = acc;
+}
+void launch_dots_abs(hipStream_t s, const AbsDots& a, DevCtrl* ctrl) {
+  if (a.count > 0) k_dots_abs<<<a.count, 1024, 0, s>>>(a, ctrl);
+}
 void launch_dot(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot) {
   k_dot<<<1, 1024, 0, s>>>(u, v, n, ctrl, slot);
 }
@@ -409,57 +470,97 @@ void launch_set_diag(hipStream_t s, double* H, int ld, int n, const double* diag
 // ------------------------------------------------------------------------------------------------
 int ls_blocks(int m) { return (m + 255) / 256; }
 
+// Certified decisions (cabs != nullptr): the trial value c_i + t e_i and the reference's fresh evaluation
+// r_i + a_i.(x + s t) both lie within B_i(t) = gamma (cabs_i + t eabs_i) of the exact g_i(x + s t), with cabs_i = |r_i|
+// + |a_i|.|x|, eabs_i = |a_i|.|s| and gamma = 4 (n + 16) u.  A constraint whose feasibility margin is inside that
+// band counts as ambiguous (the host then evaluates that trial fresh); per trial the kernel also sums the first-
+// order bound of the log-sum error, sum_i (B_i + 4u(|g_i| + |ub_i|)) / d_i, and sum_i |log d_i| (+inf when some
+// B_i is not small against d_i).
 __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c, const double* __restrict__ e,
                                                    const double* __restrict__ ub, int m, double tbase, double beta,
                                                    double* __restrict__ part_log, int* __restrict__ part_cnt,
-                                                   const double* __restrict__ f) {
+                                                   const double* __restrict__ f, const double* __restrict__ cabs,
+                                                   const double* __restrict__ eabs, double gamma,
+                                                   double* __restrict__ part_aux) {
   // blockIdx.y = group of LS_GROUP consecutive trials (more workgroups than ceil(m/256) alone)
   constexpr int LS_GROUP = 8;
-  __shared__ double slog[4][LS_GROUP];
-  __shared__ int sviol[4][LS_GROUP];
-  __shared__ int snpos[4][LS_GROUP];
+  constexpr double U = 1.1102230246251565e-16;  // 2^-53
+  __shared__ double slog[4][LS_GROUP], serr[4][LS_GROUP], sabs[4][LS_GROUP];
+  __shared__ int sviol[4][LS_GROUP], snpos[4][LS_GROUP], ssure[4][LS_GROUP], samb[4][LS_GROUP];
   const int k0 = blockIdx.y * LS_GROUP;
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool valid = i < m;
   const double ci = valid ? c[i] : 0.0, ei = valid ? e[i] : 0.0, ubi = valid ? ub[i] : 1.0;
   const double fi = (valid && f) ? f[i] : 0.0;  // s'P s of a QuadraticConstraint row (0: linear)
+  const bool cert = cabs != nullptr;
+  const double ca = (valid && cert) ? cabs[i] : 0.0, ea = (valid && cert) ? eabs[i] : 0.0;
   double t = tbase;
   for (int q = 0; q < k0; ++q) t *= beta;  // the same product chain as trial by trial
   for (int kk = 0; kk < LS_GROUP; ++kk) {
     const double g = f ? (ci + t * ei) + (t * t * fi) / 2 : ci + t * ei;
     const double dd = ubi - g;
-    const bool viol = valid && !(g * (1 + 3e-16) < ubi);   // Constraint.scala:23
-    const bool npos = valid && !(dd > 0.0);                 // BarrierSolver.scala:284
+    const double gs = g * (1 + 3e-16);
+    const bool viol = valid && !(gs < ubi);   // Constraint.scala:23
+    const bool npos = valid && !(dd > 0.0);   // BarrierSolver.scala:284
     const double lg = (valid && dd > 0.0) ? log(dd) : 0.0;
-    const double sl = wave_sum(lg);
-    const unsigned long long bv = __ballot(viol), bn = __ballot(npos);
+    bool sure = false, amb = false;
+    double lerr = 0.0, labs = 0.0;
+    if (valid && cert) {
+      const double band = gamma * (ca + t * ea);
+      const double bt = band * (1 + 3e-16) + 4 * U * (fabs(g) + fabs(ubi));
+      const double margin = gs - ubi;  // >= 0: violated
+      sure = margin > bt;
+      amb = !sure && !(margin < -bt);
+      if (dd > 0.0) {
+        const double bd = band + 4 * U * (fabs(g) + fabs(ubi));
+        lerr = (bd < 0.25 * dd) ? 2.0 * bd / dd : __builtin_inf();
+        labs = fabs(lg);
+      }
+    }
+    const double sl = wave_sum(lg), se = wave_sum(lerr), sa = wave_sum(labs);
+    const unsigned long long bv = __ballot(viol), bn = __ballot(npos), bs = __ballot(sure), ba = __ballot(amb);
     if (lane == 0) {
       slog[wid][kk] = sl;
+      serr[wid][kk] = se;
+      sabs[wid][kk] = sa;
       sviol[wid][kk] = __popcll(bv);
       snpos[wid][kk] = __popcll(bn);
+      ssure[wid][kk] = __popcll(bs);
+      samb[wid][kk] = __popcll(ba);
     }
     t *= beta;  // t *= beta (repeated products, not pow)   UnconstrainedSolver.scala:93
   }
   __syncthreads();
   if (threadIdx.x < LS_GROUP) {
     const int kk = threadIdx.x, k = k0 + kk;
-    double s = 0.0;
-    int v = 0, np_ = 0;
+    double s = 0.0, se = 0.0, sa = 0.0;
+    int v = 0, np_ = 0, su = 0, am = 0;
     for (int w = 0; w < 4; ++w) {
       s += slog[w][kk];
+      se += serr[w][kk];
+      sa += sabs[w][kk];
       v += sviol[w][kk];
       np_ += snpos[w][kk];
+      su += ssure[w][kk];
+      am += samb[w][kk];
     }
-    part_log[(size_t)blockIdx.x * LS_TRIALS + k] = s;
-    part_cnt[((size_t)blockIdx.x * LS_TRIALS + k) * 2 + 0] = v;
-    part_cnt[((size_t)blockIdx.x * LS_TRIALS + k) * 2 + 1] = np_;
+    const size_t o = (size_t)blockIdx.x * LS_TRIALS + k;
+    part_log[o] = s;
+    part_aux[2 * o] = se;
+    part_aux[2 * o + 1] = sa;
+    part_cnt[4 * o + 0] = v;
+    part_cnt[4 * o + 1] = np_;
+    part_cnt[4 * o + 2] = su;
+    part_cnt[4 * o + 3] = am;
   }
 }
 
 void launch_ls_trials(hipStream_t s, const double* c, const double* e, const double* ub, int m, double tbase,
-                      double beta, double* part_log, int* part_cnt, const double* f) {
-  k_ls_trials<<<dim3(ls_blocks(m), LS_TRIALS / 8), 256, 0, s>>>(c, e, ub, m, tbase, beta, part_log, part_cnt, f);
+                      double beta, double* part_log, int* part_cnt, const double* f, const double* cabs,
+                      const double* eabs, double gamma, double* part_aux) {
+  k_ls_trials<<<dim3(ls_blocks(m), LS_TRIALS / 8), 256, 0, s>>>(c, e, ub, m, tbase, beta, part_log, part_cnt, f, cabs,
+                                                                eabs, gamma, part_aux);
 }
 
 // KL dual objective along the trial steps: per trial k, sum_j R exp(-(v_j + t_k u_j)) (v = B'z, u = B's),
@@ -500,24 +601,30 @@ void launch_kl_eval(hipStream_t s, const double* v, int nout, int noutp, double 
   k_kl_eval<<<(noutp + 255) / 256, 256, 0, s>>>(v, nout, noutp, R, y);
 }
 
-__global__ void k_ls_finalize(const double* __restrict__ part_log, const int* __restrict__ part_cnt, int nblocks,
-                              double* __restrict__ out_log, int* __restrict__ out_cnt) {
+// out: per trial k, out_log[3k..3k+2] = {sum log d, log-sum error bound, sum |log d|} and out_cnt[4k..4k+3] =
+// {violations, d <= 0, sure violations, ambiguous}; blocks summed in a fixed order.
+__global__ void k_ls_finalize(const double* __restrict__ part_log, const int* __restrict__ part_cnt,
+                              const double* __restrict__ part_aux, int nblocks, double* __restrict__ out_log,
+                              int* __restrict__ out_cnt) {
   const int k = threadIdx.x;
   if (k >= LS_TRIALS) return;
-  double s = 0.0;
-  int v = 0, np_ = 0;
+  double s = 0.0, se = 0.0, sa = 0.0;
+  int c4[4] = {0, 0, 0, 0};
   for (int b = 0; b < nblocks; ++b) {
-    s += part_log[(size_t)b * LS_TRIALS + k];
-    v += part_cnt[((size_t)b * LS_TRIALS + k) * 2 + 0];
-    np_ += part_cnt[((size_t)b * LS_TRIALS + k) * 2 + 1];
+    const size_t o = (size_t)b * LS_TRIALS + k;
+    s += part_log[o];
+    se += part_aux[2 * o];
+    sa += part_aux[2 * o + 1];
+    for (int q = 0; q < 4; ++q) c4[q] += part_cnt[4 * o + q];
   }
-  out_log[k] = s;
-  out_cnt[2 * k] = v;
-  out_cnt[2 * k + 1] = np_;
+  out_log[3 * k] = s;
+  out_log[3 * k + 1] = se;
+  out_log[3 * k + 2] = sa;
+  for (int q = 0; q < 4; ++q) out_cnt[4 * k + q] = c4[q];
 }
-void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_cnt, int nblocks, double* out_log,
-                        int* out_cnt) {
-  k_ls_finalize<<<1, 64, 0, s>>>(part_log, part_cnt, nblocks, out_log, out_cnt);
+void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_cnt, const double* part_aux,
+                        int nblocks, double* out_log, int* out_cnt) {
+  k_ls_finalize<<<1, 64, 0, s>>>(part_log, part_cnt, part_aux, nblocks, out_log, out_cnt);
 }
 
 // ------------------------------------------------------------------------------------------------

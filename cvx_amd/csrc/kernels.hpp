@@ -17,9 +17,13 @@ struct TileList {
 // Constraint.scala:23).
 void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int n_cols, const double* x,
                             const double* r, const double* ub, double* c, double* d, double* invd,
-                            double* w, double* logd, DevCtrl* ctrl, const double* extra = nullptr);
+                            double* w, double* logd, DevCtrl* ctrl, const double* extra = nullptr,
+                            double* cabs = nullptr);
 // y = M v (row-major, one wave per row); rows, cols multiples of 128 / any.
 void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y);
+// y = M v and yabs = |M| |v| in the same sweep
+void launch_rowdot_abs(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y,
+                       double* yabs);
 // part[chunk][j] = sum_{i in chunk} M[i][j] v[i]  (chunks of COLDOT_ROWS rows; rows % 64 == 0)
 int coldot_chunks(int rows);
 void launch_coldot_partials(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
@@ -30,6 +34,16 @@ void launch_gradient_finalize(hipStream_t s, const double* a0, const double* Px,
 // single-block deterministic sums into ctrl->sc[slot]
 void launch_dot(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot);
 void launch_sum(hipStream_t s, const double* u, int n, DevCtrl* ctrl, int slot);
+// sum_i |u_i| |v_i| (v NULL: sum_i |u_i|) into ctrl->sc[slot]
+void launch_dot_abs(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot);
+struct AbsDots {
+  const double* u[4];
+  const double* v[4];
+  int n[4];
+  int slot[4];
+  int count;
+};
+void launch_dots_abs(hipStream_t s, const AbsDots& a, DevCtrl* ctrl);
 // out = u + v*alpha (alpha read from device scalar pointer or host value)
 void launch_axpy(hipStream_t s, const double* u, const double* v, double alpha, int n, double* out);
 void launch_scale_vec(hipStream_t s, const double* u, const double* d, int n, double* out);  // out = d*u
@@ -99,10 +113,13 @@ void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* L
 // ---- line search ----------------------------------------------------------------------------------
 // For trials k in [0, LS_TRIALS): t_k = tbase*beta^k; g_i = c_i + t_k e_i; per-block partials of
 // (#violations of g*(1+3e-16)<ub, #(ub-g<=0), sum log(ub-g)).
+// With cabs / eabs (|r| + |a|.|x|, |a|.|s|) the trials also report sure / ambiguous violation counts and the log-sum
+// error bound (certified decisions, see k_vec.hip); part_aux: 2 doubles per (block, trial).
 void launch_ls_trials(hipStream_t s, const double* c, const double* e, const double* ub, int m, double tbase,
-                      double beta, double* part_log, int* part_cnt, const double* f = nullptr);
-void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_cnt, int nblocks,
-                        double* out_log, int* out_cnt);
+                      double beta, double* part_log, int* part_cnt, const double* f, const double* cabs,
+                      const double* eabs, double gamma, double* part_aux);
+void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_cnt, const double* part_aux,
+                        int nblocks, double* out_log, int* out_cnt);
 int ls_blocks(int m);
 // KL dual objective (Dist_KL.scala:146-170): y = R exp(-v) (masked padding); trial sums of R exp(-(v + t_k u))
 void launch_kl_eval(hipStream_t s, const double* v, int nout, int noutp, double R, double* y);

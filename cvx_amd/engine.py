@@ -197,6 +197,12 @@ class Engine:
     def centering_begin(self, t: float):
         self._check(self.lib.cvxg_centering_begin(self.h, float(t)))
 
+    def centering_resume(self, t: float, iter_: int, trust_radius: float = float("nan"), grad=None):
+        """cvxg_centering_resume: the inner loop's state before iteration `iter_` (trust radius frozen at
+        iteration 0; grad = the host's y, or None for the engine's own)."""
+        g = None if grad is None else _f64(grad)
+        self._check(self.lib.cvxg_centering_resume(self.h, float(t), int(iter_), float(trust_radius), _dp(g)))
+
     def newton_step(self, pars) -> L.cvxg_step_info:
         info = L.cvxg_step_info()
         ps = params_struct(pars)

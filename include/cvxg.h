@@ -68,6 +68,8 @@ typedef struct cvxg_step_info {
   int took_step;            /* 1 if x moved */
   int done;                 /* 1 if the centering loop terminates after this iteration */
   int iter;                 /* inner iteration index */
+  int ls_fresh;             /* line-search feasibility trials evaluated fresh (margin inside the rounding band) */
+  int ls_ties;              /* Armijo decisions inside the rounding band of the barrier value (rounding noise) */
 } cvxg_step_info;
 
 /* UnconstrainedSolver / EqualityConstrainedSolver result (Solution.scala:32-43). */
@@ -161,6 +163,12 @@ int cvxg_newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, cons
 /* Start the inner solver at barrier parameter t from the current iterate (new UnconstrainedSolver /
  * EqualityConstrainedSolver, BarrierSolver.scala:97,154). */
 int cvxg_centering_begin(cvxg_ctx* ctx, double t);
+
+/* Resume the inner solver in the middle of a centering, as the reference's loop state stands before inner iteration
+ * `iter` (UnconstrainedSolver.scala:47-48): barrier parameter t, the trust radius frozen at iteration 0
+ * (trustRadius, :86; ignored when iter == 0) and, when grad != NULL, the host's gradient y (:44,131) in place of the
+ * engine's.  Lets a Scala caller that keeps its own loop hand over any iteration, and replays recorded steps. */
+int cvxg_centering_resume(cvxg_ctx* ctx, double t, int iter, double trust_radius, const double* grad);
 
 /* One inner Newton iteration on the device-resident iterate: assemble, equilibrate, factor, solve,
  * line search, update (UnconstrainedSolver.scala:47-134 or EqualityConstrainedSolver.scala:60-111).

@@ -3,6 +3,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 microbench/lat.hip -o microbench/lat
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <utility>
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -13,6 +14,23 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+
+template <int L>
+__device__ __forceinline__ double dpp_bcast(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x150 + L, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x150 + L, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int... Q>
+__device__ __forceinline__ double dpp16(double v, double acc, std::integer_sequence<int, Q...>) {
+  ((acc = fma(dpp_bcast<Q>(v), 1.0000001, acc)), ...);
+  return acc;
+}
+__device__ __forceinline__ double rl16(double v, double acc) {
+  for (int q = 0; q < 16; ++q) acc = fma(readlane_d(v, q), 1.0000001, acc);
+  return acc;
+}
 constexpr int IT = 256;
 
 __global__ void k_lat(double* out, long long* res, double x) {
@@ -76,7 +94,26 @@ __global__ void k_lat(double* out, long long* res, double x) {
   });
   // 10: DPP row broadcast style: __shfl_xor 1 chain
   MEASURE(v = __shfl_xor(v, 1, 64) * 1.0000001);
-  out[threadIdx.x] = v + acc[0] + a1[1] + a2[2] + a3[3];
+  // 11: DPP row_newbcast (lane 1 of each row of 16) f64 chain
+  MEASURE({
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x151, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x151, 0xf, 0xf, false);
+    v = __longlong_as_double(((long long)hi << 32) | (unsigned)lo) * 1.0000001;
+  });
+  // 12: permlane32_swap f64 chain
+  MEASURE({
+    const long long b = __double_as_longlong(v);
+    auto r0 = __builtin_amdgcn_permlane32_swap((int)b, (int)b, false, false);
+    auto r1 = __builtin_amdgcn_permlane32_swap((int)(b >> 32), (int)(b >> 32), false, false);
+    v = __longlong_as_double(((long long)r1[0] << 32) | (unsigned)r0[0]) * 1.0000001;
+  });
+  // 13: 16 independent readlane_d (throughput per readlane_d)
+  double acc16 = 0.0;
+  MEASURE({ acc16 = rl16(v, acc16); v = v + acc16 * 1e-30; });
+  // 14: 16 independent DPP newbcast f64 (throughput)
+  MEASURE({ acc16 = dpp16(v, acc16, std::make_integer_sequence<int, 16>{}); v = v + acc16 * 1e-30; });
+  out[threadIdx.x] = v + acc[0] + a1[1] + a2[2] + a3[3] + acc16;
 }
 
 int main() {
@@ -86,14 +123,14 @@ int main() {
   (void)hipMalloc(&r, 1024);
   const char* names[] = {"fma_f64 dep", "rsq_f64 dep", "rsq+2NR", "readlane f64+mul", "shfl(bpermute)+mul",
                          "lds st->ld+mul", "mfma_f64_16x16x4 dep", "mfma x4 indep (per 4)", "s_barrier",
-                         "rcp+2NR", "shfl_xor1+mul"};
+                         "rcp+2NR", "shfl_xor1+mul", "dpp newbcast f64+mul", "permlane32_swap f64+mul", "16x readlane_d+fma (per 16)", "16x dpp bcast f64+fma (per 16)"};
   for (int wpb : {1, 4}) {
     for (int rep = 0; rep < 2; ++rep) k_lat<<<1, 64 * wpb>>>(o, r, 0.5);
     (void)hipDeviceSynchronize();
-    long long h[32];
+    long long h[64];
     (void)hipMemcpy(h, r, sizeof(h), hipMemcpyDeviceToHost);
     printf("waves/block = %d\n", wpb);
-    for (int s = 0; s < 11; ++s)
+    for (int s = 0; s < 15; ++s)
       printf("  %-26s %8.1f ticks  %7.2f ns per op\n", names[s], (double)h[2 * s] / IT, 10.0 * h[2 * s + 1] / IT);
   }
   return 0;

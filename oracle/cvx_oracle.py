@@ -636,6 +636,53 @@ def newton_direction(pb: Problem, t: float, x: np.ndarray, y: np.ndarray, tolEqS
     return d
 
 
+def unconstrained_line_search(pb: Problem, t: float, x: np.ndarray, d: np.ndarray, q: float, f: float, it_n: int,
+                              trustRadius: float, pars: SolverParams):
+    """UnconstrainedSolver.scala:86-113: the trust-region scaling (radius frozen at iteration 0) and the two
+    backtracking loops.  Returns (s, t_accepted, k1, it): the direction actually stepped along, the accepted step,
+    the halvings into C and the shared counter."""
+    alpha, beta = pars.alpha, pars.beta
+    hNorm_d = math.sqrt(-q)
+    s = d if (it_n == 0 or hNorm_d <= trustRadius) else d * (trustRadius / hNorm_d)
+    it = 0
+    st = 1.0
+    while (not is_in_set(pb, x + s * st)) and it < 200:
+        st *= beta
+        it += 1
+    if it == 100:
+        raise NotConvergedException("Line search: backtracking into the set C failed.")
+    k1 = it
+    # trust-radius update: rho == 1 so both branches are no-ops (the f_new evaluation has no
+    # observable effect when x+s is in C, and is skipped).
+    while barrier_value(pb, t, x + s * st) > f + alpha * st * q and it < 200:
+        st *= beta
+        it += 1
+    if it == 100:
+        raise NotConvergedException("Line search: sufficient decrease not reached")
+    return s, st, k1, it
+
+
+def equality_line_search(pb: Problem, t: float, x: np.ndarray, d: np.ndarray, q: float, f: float,
+                         pars: SolverParams):
+    """EqualityConstrainedSolver.scala:78-97: no trust region, shared counter bound 100.  Returns (t_accepted, k1,
+    it)."""
+    alpha, beta = pars.alpha, pars.beta
+    it = 0
+    st = 1.0
+    while (not is_in_set(pb, x + d * st)) and it < 100:
+        st *= beta
+        it += 1
+    if it == 100:
+        raise NotConvergedException("Line search: backtracking into the set C failed.")
+    k1 = it
+    while barrier_value(pb, t, x + d * st) > f + alpha * st * q and it < 100:
+        st *= beta
+        it += 1
+    if it == 100:
+        raise NotConvergedException("Line search: sufficient decrease not reached")
+    return st, k1, it
+
+
 def unconstrained_solve(pb: Problem, t: float, x0: np.ndarray, pars: SolverParams,
                         record: bool = False, max_steps: Optional[int] = None) -> Solution:
     """UnconstrainedSolver.scala:34-125 with objF = the barrier objective at parameter t.
@@ -664,22 +711,7 @@ def unconstrained_solve(pb: Problem, t: float, x0: np.ndarray, pars: SolverParam
             hNorm_d = math.sqrt(-q)
             if it_n == 0:
                 trustRadius = hNorm_d
-            s = d if (it_n == 0 or hNorm_d <= trustRadius) else d * (trustRadius / hNorm_d)
-            it = 0
-            st = 1.0
-            while (not is_in_set(pb, x + s * st)) and it < 200:
-                st *= beta
-                it += 1
-            if it == 100:
-                raise NotConvergedException("Line search: backtracking into the set C failed.")
-            k1 = it
-            # trust-radius update: rho == 1 so both branches are no-ops (the f_new evaluation has no
-            # observable effect when x+s is in C, and is skipped).
-            while barrier_value(pb, t, x + s * st) > f + alpha * st * q and it < 200:
-                st *= beta
-                it += 1
-            if it == 100:
-                raise NotConvergedException("Line search: sufficient decrease not reached")
+            s, st, k1, it = unconstrained_line_search(pb, t, x, d, q, f, it_n, trustRadius, pars)
             x = x + s * st
             y = barrier_gradient(pb, t, x)
             normGrad = float(np.linalg.norm(y))
@@ -714,19 +746,7 @@ def equality_constrained_solve(pb: Problem, t: float, x0: np.ndarray, pars: Solv
         rec = NewtonStepRecord(x=x.copy(), grad=y.copy(), f=f, dx=d.copy(), q=q,
                                newton_decrement=newtonDecrement, fallback=info.get("fallback", 0))
         if newtonDecrement > tol:
-            it = 0
-            st = 1.0
-            while (not is_in_set(pb, x + d * st)) and it < 100:
-                st *= beta
-                it += 1
-            if it == 100:
-                raise NotConvergedException("Line search: backtracking into the set C failed.")
-            k1 = it
-            while barrier_value(pb, t, x + d * st) > f + alpha * st * q and it < 100:
-                st *= beta
-                it += 1
-            if it == 100:
-                raise NotConvergedException("Line search: sufficient decrease not reached")
+            st, k1, it = equality_line_search(pb, t, x, d, q, f, pars)
             x = x + d * st
             y = barrier_gradient(pb, t, x)
             normGrad = float(np.linalg.norm(y))
