@@ -258,6 +258,8 @@ def barrier_hessian(pb: Problem, t: float, x: np.ndarray, literal: bool = True) 
     """
     if isinstance(pb, AffineView):  # BarrierSolver.scala:229-230 — (F.t * self.hessianBarrierFunction(t, z0 + F u)) * F
         return (pb.F.T @ barrier_hessian(pb.pb, t, pb.x_of(x), literal)) @ pb.F
+    if literal == "blas":
+        return _barrier_hessian_blas(pb, t, x)
     n = pb.n
     s = objective_hessian(pb, x) * t
     for i in range(pb.m):
@@ -275,6 +277,21 @@ def barrier_hessian(pb: Problem, t: float, x: np.ndarray, literal: bool = True) 
         else:
             s = s + GGt / (d * d)
     return s
+
+
+def _barrier_hessian_blas(pb: Problem, t: float, x: np.ndarray) -> np.ndarray:
+    """The same sum as the fold above in BLAS order, t P + A' diag(1/d^2) A (one dgemm): for the C2/C3-size golden
+    fixtures, where the per-constraint fold of n x n outer products would take minutes per Hessian.  Linear rows
+    only; the two orders differ by rounding (~n u |H|)."""
+    assert pb.qrows is None and pb.kl_B is None
+    d = pb.ub - (pb.r + pb.A @ x)
+    if np.any(d <= 0):
+        raise NotStrictlyFeasible("hessianBarrierFunction: x not strictly feasible")
+    W = pb.A / d[:, None]
+    H = W.T @ W
+    if pb.P is not None:
+        H = H + pb.P * t
+    return 0.5 * (H + H.T)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -597,6 +614,8 @@ class NewtonStepRecord:
     rel_err: float = float("nan")
     d_ruiz: Optional[np.ndarray] = None
     diagL: Optional[np.ndarray] = None
+    it_n: int = 0                    # iteration within its centering
+    radius: float = float("nan")     # trust radius frozen at iteration 0 of the centering
 
 
 @dataclass
@@ -615,9 +634,10 @@ class Solution:
 
 
 def newton_direction(pb: Problem, t: float, x: np.ndarray, y: np.ndarray, tolEqSolve: float,
-                     rec: Optional[NewtonStepRecord] = None, fast_subst: bool = False) -> np.ndarray:
-    """UnconstrainedSolver.scala:50-67 — H at x, choleskySolve(H,-y) -> choleskySolve(H+1e-9 I,-y) -> symSolve."""
-    H = barrier_hessian(pb, t, x, literal=False)
+                     rec: Optional[NewtonStepRecord] = None, fast_subst: bool = False, hess="fold") -> np.ndarray:
+    """UnconstrainedSolver.scala:50-67 — H at x, choleskySolve(H,-y) -> choleskySolve(H+1e-9 I,-y) -> symSolve.
+    ``hess="blas"`` forms H in BLAS order (large golden fixtures only, see _barrier_hessian_blas)."""
+    H = barrier_hessian(pb, t, x, literal="blas" if hess == "blas" else False)
     info = CholSolveInfo()
     fb = 0
     try:
@@ -684,7 +704,8 @@ def equality_line_search(pb: Problem, t: float, x: np.ndarray, d: np.ndarray, q:
 
 
 def unconstrained_solve(pb: Problem, t: float, x0: np.ndarray, pars: SolverParams,
-                        record: bool = False, max_steps: Optional[int] = None) -> Solution:
+                        record: bool = False, max_steps: Optional[int] = None, hess="fold",
+                        fast_subst: bool = False) -> Solution:
     """UnconstrainedSolver.scala:34-125 with objF = the barrier objective at parameter t.
 
     Quirks reproduced: rho = 1+1/4 == 1 (integer), so the trust radius stays
@@ -703,14 +724,16 @@ def unconstrained_solve(pb: Problem, t: float, x0: np.ndarray, pars: SolverParam
             break
         f = barrier_value(pb, t, x)
         rec = NewtonStepRecord(x=x.copy(), grad=y.copy(), f=f, dx=None, q=0.0, newton_decrement=0.0)
-        d = newton_direction(pb, t, x, y, tolEq, rec)
+        d = newton_direction(pb, t, x, y, tolEq, rec, fast_subst=fast_subst, hess=hess)
         q = float(np.dot(d, y))
         newtonDecrement = -q / 2
         rec.dx, rec.q, rec.newton_decrement = d.copy(), q, newtonDecrement
+        rec.it_n = it_n
         if newtonDecrement > tol:
             hNorm_d = math.sqrt(-q)
             if it_n == 0:
                 trustRadius = hNorm_d
+            rec.radius = trustRadius
             s, st, k1, it = unconstrained_line_search(pb, t, x, d, q, f, it_n, trustRadius, pars)
             x = x + s * st
             y = barrier_gradient(pb, t, x)

@@ -1,0 +1,104 @@
+"""Golden Newton steps at the BASELINE sizes C2 (n=1024, m=2048) and C3 (n=4096, m=8192), from the CPU oracle.
+
+The problem itself is NOT stored (A alone is 268 MB at C3): the GPU test regenerates it with
+cvx_amd.problems.random_qp(n, m, instance) and first checks the fingerprint recorded here (SHA-256 of the
+RNG-only arrays A and ub; sums of the BLAS-derived P and a0, which may differ in the last bit between BLAS
+thread counts and are checked to 1e-12 relative).
+
+The trajectory is the oracle's barrier t-loop (oracle.unconstrained_solve, warm start, t = 1, 10, ...) from
+x0 = 0 up to the second step of the t = 1e4 centering, with H formed in BLAS order (t P + A' diag(1/d^2) A,
+oracle._barrier_hessian_blas) and LAPACK substitutions: the per-constraint fold of n x n outer products
+would take minutes per Hessian at C3.  At the recorded steps the direction is recomputed from the fixture's
+(t, x, grad):
+  * C2: with the reference's per-constraint fold (BarrierSolver.scala:303-315, oracle.barrier_hessian) and the
+    scalar substitutions (MatrixUtils.scala:383-430) -- the literal restatement;
+  * C3: with the BLAS-ordered H and dtrtrs (hess_form = "blas" in the fixture).
+The line-search decisions (accepted step, both backtracking counters) are the reference's line search
+(UnconstrainedSolver.scala:83-113, oracle.unconstrained_line_search) run on that direction from the
+recorded (iteration, frozen trust radius).
+
+Run:  python tests/golden/make_golden_big.py [C2] [C3]   (C3 takes several minutes and ~6 GB of RAM)
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from cvx_amd import problems as Z  # noqa: E402
+from oracle import cvx_oracle as O  # noqa: E402
+
+CONFIGS = {
+    # name: (n, m, instance, recorded (t, iteration-within-centering) pairs, form of the recorded directions)
+    "C2": (1024, 2048, 0, [(1.0, 0), (1.0, 1), (1e2, 0), (1e4, 0), (1e4, 1)], "fold"),
+    "C3": (4096, 8192, 0, [(1.0, 0), (1e2, 0), (1e4, 0), (1e4, 1)], "blas"),
+}
+
+
+def fingerprint(spec):
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(spec["A"]).tobytes())
+    h.update(np.ascontiguousarray(spec["ub"]).tobytes())
+    return h.hexdigest(), float(np.sum(spec["P"])), float(np.sum(spec["a0"]))
+
+
+def make(name):
+    n, m, inst, want, form = CONFIGS[name]
+    t0 = time.time()
+    spec = Z.random_qp(n, m, instance=inst)
+    pb = O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"])
+    pars = O.standard_params()
+    sha, psum, a0sum = fingerprint(spec)
+    t_last = max(t for t, _ in want)
+    x = spec["x0"].copy()
+    t = 1.0
+    states = []  # (t, it_n, radius, x, grad)
+    while t <= t_last:
+        max_steps = max(k for tt, k in want if tt == t) + 1 if t == t_last else None
+        sol = O.unconstrained_solve(pb, t, x, pars, record=True, max_steps=max_steps, hess="blas", fast_subst=True)
+        for rc in sol.records:
+            if (t, rc.it_n) in want:
+                states.append((t, rc.it_n, rc.radius, rc.x.copy(), rc.grad.copy()))
+        print(f"{name}: t={t:g} {sol.newton_steps} steps ({time.time() - t0:.0f} s)", flush=True)
+        x = sol.x
+        t *= 10.0
+    assert len(states) == len(want), (len(states), want)
+    out = {k: [] for k in ("t", "it_n", "radius", "x", "grad", "f", "dx", "q", "step", "kc", "ka", "ruiz", "reg",
+                           "rel_err")}
+    for (t, it_n, radius, x, g) in states:
+        rec = O.NewtonStepRecord(x=x, grad=g, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
+        if form == "fold":
+            d = O.newton_direction(pb, t, x, g, pars.tolEqSolve, rec)
+        else:
+            d = O.newton_direction(pb, t, x, g, pars.tolEqSolve, rec, fast_subst=True, hess="blas")
+        assert rec.fallback == 0
+        q = float(np.dot(d, g))
+        if it_n == 0:
+            radius = math.sqrt(-q)
+        f = O.barrier_value(pb, t, x)
+        _, st, k1, it = O.unconstrained_line_search(pb, t, x, d, q, f, it_n, radius, pars)
+        for k, v in (("t", t), ("it_n", it_n), ("radius", radius), ("x", x), ("grad", g), ("f", f), ("dx", d),
+                     ("q", q), ("step", st), ("kc", k1), ("ka", it - k1), ("ruiz", rec.ruiz_sweeps),
+                     ("reg", rec.regularized), ("rel_err", rec.rel_err)):
+            out[k].append(v)
+        print(f"{name}: t={t:g} it={it_n} q={q:.6e} step={st:g} kc={k1} ka={it - k1} ruiz={rec.ruiz_sweeps} "
+              f"reg={rec.regularized}", flush=True)
+    arrays = {k: np.array(v) for k, v in out.items()}
+    arrays.update(n=np.array(n), m=np.array(m), instance=np.array(inst), sha256=np.array(sha), P_sum=np.array(psum),
+                  a0_sum=np.array(a0sum), hess_form=np.array(form))
+    path = os.path.join(HERE, "big", f"{name}_n{n}_m{m}.npz")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    np.savez_compressed(path, **arrays)
+    print(f"{name}: wrote {path} ({os.path.getsize(path) / 1e3:.0f} KB, {time.time() - t0:.0f} s)")
+
+
+if __name__ == "__main__":
+    for nm in (sys.argv[1:] or ["C2", "C3"]):
+        make(nm)

@@ -65,3 +65,59 @@ def test_bad_arguments_rejected(lib):
     assert lib.cvxg_create(0, 0, 4, 0, C.byref(h)) == _lib.CVXG_E_DIM
     assert lib.cvxg_create(0, 4, 4, _lib.CVXG_MAX_EQ + 1, C.byref(h)) == _lib.CVXG_E_UNSUPPORTED
     assert lib.cvxg_newton_step(None, None, None) == _lib.CVXG_E_ARG
+
+
+# A stand-in for the few JNI declarations jni/cvxg_jni.c uses, with the JDK's C signatures (jni.h: JNIEnv is a
+# pointer to the function table; jdoubleArray / jintArray are jarray = jobject).  A compile check of the glue only:
+# it proves nothing about JVM linkage.
+_JNI_STANDIN = r"""
+#ifndef JNI_STANDIN_H
+#define JNI_STANDIN_H
+typedef int jint;
+typedef long jlong;
+typedef double jdouble;
+typedef jint jsize;
+typedef struct _jobject* jobject;
+typedef jobject jclass;
+typedef jobject jstring;
+typedef jobject jarray;
+typedef jarray jdoubleArray;
+typedef jarray jintArray;
+struct JNINativeInterface_;
+typedef const struct JNINativeInterface_* JNIEnv;
+struct JNINativeInterface_ {
+  jclass (*FindClass)(JNIEnv*, const char*);
+  jint (*ThrowNew)(JNIEnv*, jclass, const char*);
+  jstring (*NewStringUTF)(JNIEnv*, const char*);
+  jsize (*GetArrayLength)(JNIEnv*, jarray);
+  void (*GetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, jint*);
+  void (*GetDoubleArrayRegion)(JNIEnv*, jdoubleArray, jsize, jsize, jdouble*);
+  void (*SetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, const jint*);
+  void (*SetDoubleArrayRegion)(JNIEnv*, jdoubleArray, jsize, jsize, const jdouble*);
+};
+#define JNIEXPORT __attribute__((visibility("default")))
+#define JNICALL
+#endif
+"""
+
+
+def test_jni_glue_compiles_against_jni_declarations(tmp_path):
+    (tmp_path / "jni.h").write_text(_JNI_STANDIN)
+    src = os.path.join(ROOT, "jni", "cvxg_jni.c")
+    r = subprocess.run(["gcc", "-std=c99", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-I", str(tmp_path), "-I",
+                        os.path.join(ROOT, "include"), src], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_jni_glue_binds_every_scala_native_and_every_step_entry():
+    """Every `@native def` of CvxgNative in INTEGRATION.md has its Java_cvx_gpu_CvxgNative_* function in the glue and
+    vice versa; the per-t / per-step entry points a Scala-owned t-loop needs are among them."""
+    c_src = open(os.path.join(ROOT, "jni", "cvxg_jni.c")).read()
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    c_names = set(re.findall(r"Java_cvx_gpu_CvxgNative_(\w+)\s*\(", c_src))
+    scala_names = set(re.findall(r"@native def (\w+)", doc))
+    assert c_names == scala_names, (c_names ^ scala_names)
+    for s in ("centering", "centeringBegin", "centeringResume", "newtonStep", "newtonDirection", "barrierEval",
+              "constraintValues", "activeSet", "setQuad"):
+        assert s in c_names
+    assert "GetPrimitiveArrayCritical" not in c_src  # no critical region spans a GPU call

@@ -876,3 +876,50 @@ def test_reduced_known_minimizer_rank_one_simplex(mods):
     assert abs(x.sum() - 1.0) < 1e-12
     red.engine.close()
     solver.engine.close()
+
+
+def _big_fixtures():
+    return sorted(glob.glob(os.path.join(HERE, "golden", "big", "*.npz")))
+
+
+@pytest.mark.parametrize("path", _big_fixtures(), ids=lambda p: os.path.basename(p))
+def test_golden_baseline_sizes(mods, path):
+    """North-star parity at the BASELINE sizes C2 (n=1024, m=2048) and C3 (n=4096, m=8192): the problem is
+    regenerated from its seed and checked against the fixture's fingerprint; at every recorded step (t in {1, 1e2,
+    1e4}, warm-started central-path x from the oracle's t-loop; tests/golden/make_golden_big.py) the Newton
+    direction from the oracle's (t, x, grad) is within 1e-8 relative of the oracle's, the Ruiz sweep count and the
+    regularisation flag are identical, and the line search replayed from the recorded (iteration, trust radius)
+    takes exactly the reference's accepted step and backtracking counters."""
+    import hashlib
+    Z, SP, Engine, O = mods
+    fx = dict(np.load(path))
+    n, m, inst = int(fx["n"]), int(fx["m"]), int(fx["instance"])
+    spec = Z.random_qp(n, m, instance=inst)
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(spec["A"]).tobytes())
+    h.update(np.ascontiguousarray(spec["ub"]).tobytes())
+    assert h.hexdigest() == str(fx["sha256"]), "regenerated A / ub differ from the fixture's"
+    assert abs(np.sum(spec["P"]) - float(fx["P_sum"])) <= 1e-12 * abs(float(fx["P_sum"]))
+    assert abs(np.sum(spec["a0"]) - float(fx["a0_sum"])) <= 1e-12 * np.sum(np.abs(spec["a0"]))
+    eng = _engine(Engine, spec)
+    pars = SP.standardParams()
+    rels = []
+    for k in range(fx["t"].shape[0]):
+        t, x, g = float(fx["t"][k]), fx["x"][k], fx["grad"][k]
+        dx, _, info = eng.newton_direction(pars, t, x, grad=g)
+        rel = np.linalg.norm(dx - fx["dx"][k]) / np.linalg.norm(fx["dx"][k])
+        rels.append(rel)
+        assert rel < 1e-8, f"step {k} (t={t:g}): rel {rel:.3e}"
+        assert info.fallback == 0
+        assert info.ruiz_sweeps == int(fx["ruiz"][k]), (k, info.ruiz_sweeps, int(fx["ruiz"][k]))
+        assert info.regularized == int(fx["reg"][k])
+        assert (-info.q / 2 > pars.tolSolver) == (-float(fx["q"][k]) / 2 > pars.tolSolver)
+        eng.set_x(x)
+        eng.centering_resume(t, int(fx["it_n"][k]), float(fx["radius"][k]), grad=g)
+        st = eng.newton_step(pars)
+        assert st.took_step == 1
+        assert st.ls_ties == 0 and st.ls_fresh == 0, (k, t, st.ls_ties, st.ls_fresh)
+        got = (st.step, st.backtracks_c, st.backtracks_armijo)
+        assert got == (float(fx["step"][k]), int(fx["kc"][k]), int(fx["ka"][k])), (k, t, got)
+    eng.close()
+    print(f"{os.path.basename(path)} ({fx['hess_form']} H): max rel dx {max(rels):.2e} over {len(rels)} steps")
