@@ -61,6 +61,61 @@ class Solution:
     normDualResidual: Optional[float] = None  # PrimalDualSolver (Solution.scala:24)
 
 
+@dataclass
+class OptimizationState:
+    """OptimizationState.scala:22-29: what a termination criterion sees after each pass of the t-loop."""
+    normGradient: Optional[float]
+    newtonDecrement: Optional[float]
+    dualityGap: Optional[float]
+    equalityGap: Optional[float]
+    objectiveFunctionValue: float
+    normDualResidual: Optional[float] = None
+
+
+class CvxUtils:
+    """The termination criteria of CvxUtils.scala:61-87."""
+
+    @staticmethod
+    def standardTerminationCriterion(pars: "SolverParams"):
+        def tc(st: OptimizationState) -> bool:
+            assert st.dualityGap is not None, "Nonempty duality gap required, Solver should be Barrier or PrimalDual."
+            return st.dualityGap < pars.tolSolver and (st.equalityGap is None or st.equalityGap < pars.tolSolver)
+        return tc
+
+    @staticmethod
+    def phase_I_TerminationCriterion():
+        def tc(st: OptimizationState) -> bool:
+            assert st.dualityGap is not None, "Nonempty duality gap required, Solver should be Barrier or PrimalDual."
+            return st.objectiveFunctionValue < 0 and (st.equalityGap is None or st.equalityGap < 1e-6)
+        return tc
+
+
+class FeasibilityReport:
+    """FeasibilityReport.scala:12-40 (basic phase I: s has one entry)."""
+
+    def __init__(self, x0, s, isStrictlySatisfied: bool, constraintSet, equalityConstraintError=None):
+        self.x0 = np.asarray(x0, dtype=np.float64)
+        self.s = np.atleast_1d(np.asarray(s, dtype=np.float64))
+        self.isStrictlySatisfied = isStrictlySatisfied
+        self.constraintSet = constraintSet
+        self.equalityConstraintError = equalityConstraintError
+
+    def violatedConstraints(self, tol: float):
+        return [c for c in self.constraintSet.constraints if not c.isSatisfiedWithTolerance(self.x0, tol)]
+
+    def isFeasible(self, tol: float) -> bool:
+        return float(np.max(self.s)) < tol and (self.equalityConstraintError or 0.0) < tol
+
+
+class InfeasibleProblemException(Exception):
+    """InfeasibleProblemException.scala:6-7: phase I found no feasible point."""
+
+    def __init__(self, report: FeasibilityReport, tol: float):
+        super().__init__(f"No feasible point found: phase I ended with s = {report.s}, "
+                         f"{len(report.violatedConstraints(tol))} constraint(s) violated at tolerance {tol}")
+        self.report = report
+
+
 class ObjectiveFunction:
     def __init__(self, dim: int):
         self.dim = dim
@@ -164,6 +219,10 @@ class LinearConstraint:
 
     def isSatisfiedStrictly(self, x):
         return self.valueAt(x) * (1 + 3e-16) < self.ub
+
+    def isSatisfiedWithTolerance(self, x, tol: float):
+        """Constraint.scala:24."""
+        return self.valueAt(x) < self.ub + tol
 
     def isActive(self, x, tol: float = 1e-12):
         return abs(self.valueAt(x) - self.ub) < tol
@@ -287,45 +346,81 @@ class ConstraintSet:
         return cs
 
     # --- phase I on the same engine (ConstraintSet.scala:123-168, 326-395, 556-575) ------------------
-    def phase_I_Analysis(self, eqs: Optional[EqualityConstraint], pars: SolverParams):
+    def phase_I_Analysis(self, eqs: Optional[EqualityConstraint], pars: SolverParams) -> FeasibilityReport:
+        """phase_I_Analysis (ConstraintSet.scala:394-404): the basic phase-I barrier problem on the engine, with the
+        equalities as inequalities of tolerance 1e-6 (phase_I_Analysis_withEqs, :324-347).  The phase-I objects are
+        packed from this list (the Scala glue's GpuBarrierSolver.phaseI): rows (a_i, -1) (Constraint.phase_I,
+        Constraint.scala:64-89), quadratic P_k padded with a zero row and column for s, objective f(x, s) = s
+        (:129-141), feasible point (x0, 1 + max_j (g_j(x0) - ub_j)) (:161-164); solved under
+        CvxUtils.phase_I_TerminationCriterion (:369-372)."""
         cnts = list(self.constraints)
         if eqs is not None:
-            cnts = cnts + eqs.asInequalities(1e-6)  # phase_I_Analysis_withEqs (:326-347)
-        A, r, ub = ConstraintSet(self.dim, cnts).packed()
+            cnts = cnts + eqs.asInequalities(1e-6)
+        cs = ConstraintSet(self.dim, cnts, self.pointWhereDefined)
+        A, r, ub = cs.packed()
         m, n = A.shape
         x0 = self.pointWhereDefined
-        A1 = np.hstack([A, -np.ones((m, 1))])                 # g_j(x) - s <= ub_j  (Constraint.scala:64-89)
+        A1 = np.hstack([A, -np.ones((m, 1))])
         a0 = np.zeros(n + 1)
-        a0[n] = 1.0                                            # f(x,s) = s        (:129-140)
+        a0[n] = 1.0
         y0 = max(cnts[j].valueAt(x0) - ub[j] for j in range(m))
-        fp = np.concatenate([x0, [1 + y0]])                    # feasible point    (:161-164)
-        qrows, qP = ConstraintSet(self.dim, cnts).quadratic()
+        fp = np.concatenate([x0, [1 + y0]])
+        qrows, qP = cs.quadratic()
         eng = Engine(n + 1, m, 0)
         try:
             eng.set_objective(a0, 0.0, None)
             eng.set_ineq(A1, r, ub)
-            if qrows is not None:  # Constraint.phase_I: hessianAt pads P with a zero row/column for s (:82-88)
+            if qrows is not None:
                 qP1 = np.zeros((len(qrows), n + 1, n + 1))
                 qP1[:, :n, :n] = qP
                 eng.set_quad(qrows, qP1)
-            eng.set_x(fp)
-            eng.barrier_solve(pars, termination=1)             # phase_I_TerminationCriterion
-            w = eng.get_x()
+            sol = barrier_t_loop(eng, lambda w: float(w[n]), m, False, CvxUtils.phase_I_TerminationCriterion(), pars,
+                                 fp)
         finally:
             eng.close()
-        return w[:n], float(w[n])
+        w = sol.x
+        x_feas, s_feas = w[:n], float(w[n])
+        return FeasibilityReport(x_feas, [s_feas], s_feas < 0.0, cs, 0.0)
 
     def withFeasiblePoint(self, eqs: Optional[EqualityConstraint], pars: SolverParams) -> "ConstraintSet":
-        """ConstraintSet.scala:556-575."""
+        """ConstraintSet.scala:556-575: phase I, InfeasibleProblemException unless the report is feasible at
+        pars.tolSolver."""
         if self.feasiblePoint is not None:
             return self
-        x_feas, s_feas = self.phase_I_Analysis(eqs, pars)
-        if not s_feas < pars.tolSolver:  # FeasibilityReport.isFeasible
-            raise ValueError(f"InfeasibleProblemException: phase I ended with s = {s_feas}")
-        return self.addFeasiblePoint(x_feas)
+        report = self.phase_I_Analysis(eqs, pars)
+        if not report.isFeasible(pars.tolSolver):
+            raise InfeasibleProblemException(report, pars.tolSolver)
+        return self.addFeasiblePoint(report.x0)
 
 
 # ------------------------------------------------------------------------------------------------
+
+
+_DOUBLE_MAX = 1.7976931348623157e308  # Double.MaxValue
+
+
+def barrier_t_loop(engine: Engine, objF_value, m: int, with_eqs: bool, terminationCriterion, pars: SolverParams,
+                   x0) -> Solution:
+    """BarrierSolver.solveWithoutEQs / solveWithEQs (BarrierSolver.scala:70-177) on the host, exactly as the Scala glue
+    runs it: t = 1, mu = 10, at most 1000/mu passes, the caller's termination criterion on the
+    reference's OptimizationState; the inner solver of each pass (UnconstrainedSolver / EqualityConstrainedSolver
+    .solve, :97-98, :154-155) is one cvxg_centering on the device-resident iterate."""
+    mu = 10.0
+    t = 1.0
+    engine.set_x(x0)
+    state = OptimizationState(None, None, _DOUBLE_MAX, _DOUBLE_MAX if with_eqs else None, _DOUBLE_MAX)
+    it, total, ci, x = 0, 0, None, np.asarray(x0, dtype=np.float64)
+    while not terminationCriterion(state) and it < 1000 / mu:
+        ci = engine.centering(pars, t)
+        total += ci.iter
+        x = engine.get_x()
+        state = OptimizationState(None, None, m / t, ci.equality_gap if with_eqs else 0.0, objF_value(x))
+        t = mu * t
+        it += 1
+    if ci is None:  # the criterion held before the first pass: the reference would dereference a null Solution
+        raise AssertionError("termination criterion satisfied before the first centering")
+    return Solution(x, ci.newton_decrement, state.dualityGap, state.equalityGap if with_eqs else None, ci.norm_grad,
+                    ci.iter, bool(ci.maxed_out), total, it)
 
 
 class GpuBarrierSolver:
@@ -370,15 +465,14 @@ class GpuBarrierSolver:
     def hessianBarrierFunction(self, t, x):
         return self.engine.barrier_eval(t, x, want_grad=False, want_hess=True)[2]
 
-    def solveSpecial(self, termination: int = 0) -> Solution:
-        self.engine.set_x(self.startingPoint)
-        s = self.engine.barrier_solve(self.pars, termination)
-        return Solution(self.engine.get_x(), s.newton_decrement, s.duality_gap,
-                        s.equality_gap if self.eqs is not None else 0.0, s.norm_grad, s.iter, bool(s.maxed_out),
-                        s.newton_steps, s.outer_iters)
+    def solveSpecial(self, terminationCriterion, debugLevel: int = 0) -> Solution:
+        """BarrierSolver.solveSpecial (BarrierSolver.scala:178-180) with any criterion (host t-loop)."""
+        return barrier_t_loop(self.engine, self.objF.valueAt, self.numConstraints, self.eqs is not None,
+                              terminationCriterion, self.pars, self.startingPoint)
 
     def solve(self, debugLevel: int = 0) -> Solution:
-        return self.solveSpecial(0)
+        """BarrierSolver.solve (BarrierSolver.scala:183-187): the standard criterion."""
+        return self.solveSpecial(CvxUtils.standardTerminationCriterion(self.pars), debugLevel)
 
     # --- affine re-parametrisation (BarrierSolver.scala:191-256) -------------------------------------
     def affineTransformed(self, z0, F, u0=None) -> "AffineGpuBarrierSolver":
@@ -417,6 +511,11 @@ class AffineGpuBarrierSolver(GpuBarrierSolver):
     def x_of(self, u) -> np.ndarray:
         """x = z0 + F u on the device (cvxg_affine_map)."""
         return self.engine.affine_map(u)
+
+    def solveSpecial(self, terminationCriterion, debugLevel: int = 0) -> Solution:
+        """The t-loop in u; the objective value is objF.affineTransformed(z0, F) (BarrierSolver.scala:221)."""
+        return barrier_t_loop(self.engine, lambda u: self.objF.valueAt(self.z0 + self.F @ u), self.numConstraints,
+                              self.eqs is not None, terminationCriterion, self.pars, self.startingPoint)
 
 
 class SolutionSpace:
@@ -531,11 +630,53 @@ class Dist_KL(OptimizationProblem):
         super().__init__(id, None, None)
 
     @staticmethod
+    def objectiveFunction(n: int) -> ObjectiveFunction:
+        """Dist_KL.objectiveFunction (Dist_KL.scala:223-239): x . log(n x); its primal solve is not on the engine."""
+        class _KL(ObjectiveFunction):
+            def valueAt(self, x):
+                return float(x @ np.log(x * float(n)))
+
+            def gradientAt(self, x):
+                return 1.0 + np.log(x) + np.log(n)
+
+            def hessianAt(self, x):
+                return np.diag(1.0 / x)
+        return _KL(n)
+
+    @staticmethod
+    def equalityConstraint(n: int, A=None, r=None) -> EqualityConstraint:
+        """Dist_KL.scala:245-256: E_Q[A] = r stacked above sum(Q) = 1 (EqualityConstraint.addEqualities)."""
+        ones = np.ones((1, n))
+        if A is None:
+            return EqualityConstraint(ones, np.ones(1))
+        return EqualityConstraint(np.vstack([np.atleast_2d(A), ones]),
+                                  np.concatenate([np.asarray(r, dtype=np.float64).reshape(-1), np.ones(1)]))
+
+    @staticmethod
     def apply(id, n, H, u, A, r, solverType: str = "BR", pars=None, device: int = 0) -> "Dist_KL":
-        """Dist_KL.apply (Dist_KL.scala:264-315); solverType "BR" (the dual runs on the GPU engine)."""
-        if solverType not in ("BR", "GPU"):
+        """Dist_KL.apply (Dist_KL.scala:270-315), including its construction-time phase I on the engine
+        (ineqs.withFeasiblePoint(Some(eqs), ...), :303-307): the rows of H (ConstraintSet(H, u, C), ConstraintSet.scala:
+        621-638) followed by x_j >= 0 for all j (Constraints.allCoordinatesPositive), the equalities A; 1' as
+        inequalities of tolerance 1e-6, from x = 1/n; raises InfeasibleProblemException when phase I fails.  The
+        solver itself then runs on the dual (solveDual); "PD" is accepted as in the reference, but the engine's
+        primal-dual solver has no KL dual objective (dualProblem("PD") raises TypeError)."""
+        if solverType not in ("BR", "PD", "GPU"):
             raise ValueError(f"Unknown solver: {solverType}")
-        return Dist_KL(id, n, H, u, A, r, device)
+        if H is None and A is None:
+            raise ValueError("Must have some inequality or equality constraints")
+        pars = pars or SolverParams.standardParams()
+        eqs = Dist_KL.equalityConstraint(n, A, r)
+        cnts = []
+        if H is not None:
+            Hm = np.atleast_2d(np.asarray(H, dtype=np.float64))
+            uv = np.asarray(u, dtype=np.float64).reshape(-1)
+            cnts += [LinearConstraint(f"row_{i}(H)x<=u({i})", n, uv[i], 0.0, Hm[i]) for i in range(Hm.shape[0])]
+        cnts += Constraints.allCoordinatesPositive(n)
+        ineqs = ConstraintSet(n, cnts, np.full(n, 1.0 / n))
+        prob = Dist_KL(id, n, H, u, A, r, device)
+        prob.ineqsWithFeasiblePoint = ineqs.withFeasiblePoint(eqs, pars)  # phase I
+        prob.solverType = solverType
+        return prob
 
     def primalOptimum(self, z):
         """Dist_KL.scala:170: Q = vec_R :* exp(-mat_B.t * z)."""
@@ -551,6 +692,8 @@ class Dist_KL(OptimizationProblem):
             cnts.append(LinearConstraint(f"x_{j}>0", k, 0.0, 0.0, a))
         ineqs = ConstraintSet(k, cnts, np.zeros(k)).addFeasiblePoint(np.full(k, 0.001))
         objF = DualKLObjectiveFunction(self.mat_B, self.vec_w, self.R)
+        if solverType == "PD":
+            raise TypeError("GPU primal-dual engine: the KL dual objective is not supported (barrier solver only)")
         return OptimizationProblem.apply(self.id + " dual problem", objF, ineqs, None, solverType, pars, self.device)
 
     def solveDual(self, solverType: str = "BR", pars: Optional[SolverParams] = None) -> Solution:
@@ -585,7 +728,8 @@ def problem_from_spec(spec: dict):
     return objF, cs, eqs
 
 
-__all__ = ["SolverParams", "Solution", "ObjectiveFunction", "QuadraticObjectiveFunction", "LinearObjectiveFunction",
+__all__ = ["SolverParams", "Solution", "OptimizationState", "CvxUtils", "FeasibilityReport",
+           "InfeasibleProblemException", "barrier_t_loop", "ObjectiveFunction", "QuadraticObjectiveFunction", "LinearObjectiveFunction",
            "DualKLObjectiveFunction", "Dist_KL",
            "LinearConstraint", "QuadraticConstraint", "Constraints", "EqualityConstraint", "ConstraintSet", "GpuBarrierSolver", "BarrierSolver",
            "GpuPrimalDualSolver", "PrimalDualSolver",

@@ -923,3 +923,110 @@ def test_golden_baseline_sizes(mods, path):
         assert got == (float(fx["step"][k]), int(fx["kc"][k]), int(fx["ka"][k])), (k, t, got)
     eng.close()
     print(f"{os.path.basename(path)} ({fx['hess_form']} H): max rel dx {max(rels):.2e} over {len(rels)} steps")
+
+
+def test_host_t_loop_with_caller_criterion(mods):
+    """The mirror's BarrierSolver.solveSpecial runs the reference's t-loop on the host (as the Scala glue does,
+    INTEGRATION.md §2) with any termination criterion, one cvxg_centering per pass: with the standard criterion it
+    reproduces cvxg_barrier_solve bit for bit; a caller criterion (gap < 1e-3) stops where the oracle's t-loop with
+    the same criterion stops."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import BarrierSolver, CvxUtils, OptimizationState, problem_from_spec
+    spec = Z.random_qp(60, 140, instance=41)
+    pars = SP.standardParams()
+    objF, cs, _ = problem_from_spec(spec)
+    solver = BarrierSolver.apply(objF, cs.addFeasiblePoint(spec["x0"]), None, pars)
+    sol = solver.solve()
+    eng = _engine(Engine, spec)
+    eng.set_x(spec["x0"])
+    ref = eng.barrier_solve(pars, termination=0)
+    assert np.array_equal(sol.x, eng.get_x())
+    assert sol.newtonSteps == ref.newton_steps and sol.outerIters == ref.outer_iters
+    assert sol.dualityGap == ref.duality_gap and sol.dualityGap < pars.tolSolver
+    eng.close()
+    early = solver.solveSpecial(lambda st: st.dualityGap < 1e-3)
+    oref = O.barrier_solve(_opb(O, spec), spec["x0"], pars, tc=lambda st: st["dualityGap"] < 1e-3)
+    assert early.outerIters == 7  # m/t < 1e-3 first at t = 1e6
+    assert early.dualityGap == oref.dualityGap and 1e-4 <= early.dualityGap < 1e-3
+    assert np.linalg.norm(early.x - oref.x) <= 1e-8 * np.linalg.norm(oref.x)
+    assert CvxUtils.standardTerminationCriterion(pars)(OptimizationState(None, None, 1e-9, None, 0.0))
+    solver.engine.close()
+
+
+def test_infeasible_kl_problem_phase_I_outcome(mods):
+    """OptimizationProblems.infeasible_kl_1(12) (OptimizationProblems.scala:375-405, run by MinimizationTests.scala:
+    145-149): p(A) >= 0.51 and p(B) >= 0.51 for disjoint A, B on the probability simplex.  The problem is built by
+    OptimizationProblem.withoutFeasiblePoint, whose phase I (ConstraintSet.withFeasiblePoint, ConstraintSet.scala:
+    556-575) runs first.  The restated reference never reaches its InfeasibleProblemException check there: the phase-I
+    t-loop cannot push s below 0, keeps raising t, and the equality slab 1'x within 1e-6 of 1 (phase_I_Analysis_withEqs,
+    :324-347) plus the (1 + 3e-16) guard of isSatisfiedStrictly (which passes g == ub for negative ub) let an iterate
+    land on the boundary, so barrierFunction throws IllegalArgumentException "x not strictly feasible"
+    (BarrierSolver.scala:285).  The engine ends the same way (CVXG_E_INFEASIBLE_X -> NotStrictlyFeasible), through
+    OptimizationProblem.withoutFeasiblePoint and through Dist_KL.apply's construction-time phase I (Dist_KL.scala:
+    303-307); a feasible Dist_KL (kl_1A) passes that phase I with a strictly feasible point."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import Constraints, ConstraintSet, Dist_KL, LinearConstraint, NotStrictlyFeasible, OptimizationProblem
+    n = 12
+    pars = SP.standardParams()
+    I_A = np.array([1.0 if j < 3 else 0.0 for j in range(n)])
+    I_B = np.array([1.0 if j >= n // 2 else 0.0 for j in range(n)])
+    ct1 = LinearConstraint("P(A) >= 0.51", n, -0.51, 0.0, -I_A)   # Constraints.expectation_lt_r(I_A*sgn, pA*sgn)
+    ct2 = LinearConstraint("P(B) >= 0.51", n, -0.51, 0.0, -I_B)
+    ineqs = ConstraintSet(n, [ct2, ct1] + Constraints.allCoordinatesPositive(n), np.full(n, 1.0 / n))
+    probEq = Dist_KL.equalityConstraint(n)
+    A = np.vstack([-I_B, -I_A, -np.eye(n)])
+    pb = O.Problem(a0=np.zeros(n), A=A, r=np.zeros(n + 2), ub=np.concatenate([[-0.51, -0.51], np.zeros(n)]),
+                   Aeq=np.ones((1, n)), beq=np.ones(1))
+    with pytest.raises(O.NotStrictlyFeasible):  # the restated reference
+        O.with_feasible_point(pb, np.full(n, 1.0 / n), pars)
+    with pytest.raises(NotStrictlyFeasible):
+        OptimizationProblem.withoutFeasiblePoint("dist_KL problem 3 (infeasible)", Dist_KL.objectiveFunction(n),
+                                                 ineqs, probEq, "BR", pars)
+    with pytest.raises(NotStrictlyFeasible):
+        Dist_KL.apply("infeasible", n, np.vstack([-I_B, -I_A]), np.array([-0.51, -0.51]), None, None, "BR", pars)
+    H1, u1 = O.kl1A_data(n)
+    prob = Dist_KL.apply("dist_KL_1A", n, H1, u1, None, None, "PD", pars)  # "PD" accepted, as in the reference
+    fp = prob.ineqsWithFeasiblePoint.feasiblePoint
+    assert np.all(H1 @ fp < u1) and np.all(fp > 0) and abs(fp.sum() - 1.0) < 1e-5
+
+
+def test_regularized_cholesky_retry_branch(mods):
+    """regularizedCholesky's second branch (MatrixUtils.scala:452-461): chol(Q) succeeds but min diag(L) <= 1e-7, so
+    the factor of Q + 1e-10 I is used.  Columns 0 and 1 of A nearly parallel (relative 1.8e-7) leave the equilibrated
+    Q one eigenvalue of ~5e-15 (min diag(L) ~7e-8, 30 % inside the threshold and ~50x above the pivot's rounding).
+    The oracle (LAPACK dpotrf) takes that branch; the engine reports regularized = 1 and the accepted factor's
+    min diag(L) = sqrt(~1e-10) as the oracle's.  dx = d o y with (Q + 1e-10 I) y = d o (-g) has cond ~1.6e10, so two
+    FP64 solves differ along Q's weakest eigenvector q by ~u cond (observed 1.7e-6 relative); dx is held to the FP64
+    bounds of that system: |dx - dref| <= 64 u cond(Q + 1e-10 I) |dref|, and in y-space the error orthogonal to q
+    (where the system is well conditioned) <= 64 u (lambda_max / lambda_2) |y|."""
+    Z, SP, Engine, O = mods
+    from scipy.linalg import lapack
+    n, m = 8, 20
+    rng = np.random.default_rng(3)
+    A = rng.uniform(-1, 1, (m, n))
+    A[:, 1] = A[:, 0] * (1 + 1.8e-7 * rng.uniform(-1, 1, m))
+    spec = dict(a0=rng.uniform(-1, 1, n), r0=0.0, P=None, A=A, r=np.zeros(m), ub=rng.uniform(0.1, 0.2, m),
+                Aeq=None, beq=None)
+    pb = _opb(O, spec)
+    x = np.zeros(n)
+    H = O.barrier_hessian(pb, 1.0, x, literal=False)
+    d, Q, _ = O.ruiz_equilibrate(H)
+    L0, info0 = lapack.dpotrf(np.tril(Q), lower=1, clean=1)
+    assert info0 == 0 and 3e-8 < np.min(np.diag(L0)) <= 1e-7  # the oracle's second branch
+    pars = SP.standardParams()
+    g = O.barrier_gradient(pb, 1.0, x)
+    rec = O.NewtonStepRecord(x=x, grad=g, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
+    dref = O.newton_direction(pb, 1.0, x, g, pars.tolEqSolve, rec)
+    assert rec.regularized == 1 and rec.fallback == 0
+    eng = _engine(Engine, spec)
+    dx, _, info = eng.newton_direction(pars, 1.0, x, grad=g)
+    eng.close()
+    assert info.regularized == 1 and info.fallback == 0
+    assert abs(info.min_diag - np.min(rec.diagL)) <= 1e-6 * np.min(rec.diagL)
+    w, V = np.linalg.eigh(Q + 1e-10 * np.eye(n))
+    u = np.finfo(float).eps / 2
+    q = V[:, 0]
+    ye, yr = dx / d, dref / d
+    err_perp = (ye - yr) - q * (q @ (ye - yr))
+    assert np.linalg.norm(err_perp) <= 64 * u * (w[-1] / w[1]) * np.linalg.norm(yr)
+    assert np.linalg.norm(dx - dref) <= 64 * u * (w[-1] / w[0]) * np.linalg.norm(dref)
