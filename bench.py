@@ -28,36 +28,58 @@ FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix peak (spec; BASELINE.m
 HBM_PEAK_GBS = 8000.0
 
 
-def cpu_baseline(spec, seconds_budget: float = 60.0):
+def _fold_sample(job):
+    """One single-thread worker of the fold sample: the rank-1 fold of BarrierSolver.scala:303-315 (with the
+    reference's n x n temporaries) over a contiguous run of constraints in list order, starting from t P; returns the
+    per-constraint wall times (stops early at the time budget)."""
+    P, A_rows, r_rows, ub_rows, x, budget = job
+    from threadpoolctl import threadpool_limits
+    n = P.shape[0]
+    per = []
+    with threadpool_limits(1):
+        s = P * 1.0
+        t0 = time.perf_counter()
+        for k in range(A_rows.shape[0]):
+            tk = time.perf_counter()
+            d = ub_rows[k] - (r_rows[k] + float(np.dot(A_rows[k], x)))  # LinearConstraint.valueAt
+            G = A_rows[k]
+            s = s + np.outer(G, G) / (d * d) + np.zeros((n, n)) / d
+            per.append(time.perf_counter() - tk)
+            if time.perf_counter() - t0 > budget:
+                break
+    return per
+
+
+def cpu_baseline(spec, seconds_budget: float = 30.0, fraction: float = 0.25, workers: int = 0):
     """Reference-faithful CPU port timed on this host (oracle/cvx_oracle.py = restatement of the Breeze path):
     the per-constraint rank-1 Hessian fold of BarrierSolver.scala:303-315 with all of its n x n temporaries,
-    timed on a bounded sample of constraints and scaled to m, plus one Ruiz + regularizedCholesky +
-    substitution solve (MatrixUtils.scala:240-516) at full n, plus m dot products per line-search trial.
-    Every constraint of the fold does identical work (n x n temporaries), so the per-constraint time is
-    shape-invariant; the sample string states its size and spread."""
+    timed on `fraction` of the constraints and scaled to m, plus one Ruiz + regularizedCholesky + substitution solve
+    (MatrixUtils.scala:240-516) at full n, plus m dot products per line-search trial.  The fold sample is split into
+    contiguous runs over a few concurrent single-thread worker processes (spawned children that touch no GPU) so that
+    a quarter of C3's 8192 constraints fits the time budget; each per-constraint time is a single-thread cost (the
+    concurrent workers share memory bandwidth, which can only make them slower).  Every constraint of the fold does
+    identical work (n x n temporaries), so the per-constraint time is shape-invariant; the sample string states the
+    sample size and spread."""
+    import multiprocessing as mp
+
     from threadpoolctl import threadpool_limits
 
     from oracle import cvx_oracle as O
     n, m = spec["A"].shape[1], spec["A"].shape[0]
     pb = O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"])
     x = spec["x0"]
+    nw = workers or max(1, min(4, cpu_threads() // 2))
+    want = max(1, int(round(fraction * m)))
+    runs = np.array_split(np.arange(want), nw)
+    jobs = [(spec["P"], spec["A"][r], spec["r"][r], spec["ub"][r], x, seconds_budget) for r in runs]
+    t_wall = time.perf_counter()
+    with mp.get_context("spawn").Pool(nw) as pool:
+        per = [t for part in pool.map(_fold_sample, jobs) for t in part]
+    t_wall = time.perf_counter() - t_wall
+    k = len(per)
+    t_fold = float(np.mean(per)) * m
+    cv = float(np.std(per) / np.mean(per)) if k > 1 else 0.0
     with threadpool_limits(1):
-        # (1) fold sample, constraints taken in list order
-        k = 0
-        s = spec["P"] * 1.0
-        per = []
-        t0 = time.perf_counter()
-        budget_fold = 0.75 * seconds_budget
-        while k < m and (time.perf_counter() - t0) < budget_fold:
-            tk = time.perf_counter()
-            d = pb.ub[k] - O.constraint_value(pb, k, x)
-            G = pb.A[k]
-            s = s + np.outer(G, G) / (d * d) + np.zeros((n, n)) / d
-            per.append(time.perf_counter() - tk)
-            k += 1
-        t_fold = float(np.mean(per)) * m
-        cv = float(np.std(per) / np.mean(per)) if len(per) > 1 else 0.0
-        del s
         # (2) equilibrate + factor + solve at full size
         dd = spec["ub"] - spec["A"] @ x
         H = spec["P"] + spec["A"].T @ (spec["A"] / (dd * dd)[:, None])
@@ -72,11 +94,11 @@ def cpu_baseline(spec, seconds_budget: float = 60.0):
         t_trial = (time.perf_counter() - t2) / min(m, 2048) * m * 2
     t_step = t_fold + t_solve + t_trial
     return {"value": 1.0 / t_step, "unit": "Newton KKT solves/s", "cores": 1, "kind": "port",
-            "sample": (f"reference-faithful numpy port (oracle/cvx_oracle.py), 1 thread: rank-1 Hessian fold "
-                       f"timed on {k} of {m} constraints ({100.0 * k / m:.1f} %, per-constraint time spread "
-                       f"{100 * cv:.1f} % CV) and scaled to m ({t_fold:.1f} s/Hessian), Ruiz+"
-                       f"regularizedCholesky+dtrtrs solve at n={n} ({t_solve:.2f} s), 2 trial sweeps "
-                       f"({t_trial:.2f} s); projected {t_step:.1f} s per Newton step")}
+            "sample": (f"reference-faithful numpy port (oracle/cvx_oracle.py), single-thread costs: rank-1 Hessian "
+                       f"fold timed on {k} of {m} constraints ({100.0 * k / m:.1f} %, {nw} concurrent single-thread "
+                       f"workers, {t_wall:.1f} s wall; per-constraint time spread {100 * cv:.1f} % CV) and scaled to m "
+                       f"({t_fold:.1f} s/Hessian), Ruiz+regularizedCholesky+dtrtrs solve at n={n} ({t_solve:.2f} s), "
+                       f"2 trial sweeps ({t_trial:.2f} s); projected {t_step:.1f} s per Newton step")}
 
 
 def ruiz_blas(H, max_iter: int = 20, tol: float = 1e-6):
@@ -162,33 +184,9 @@ def pmc_traffic(kernel_prefixes):
     return total, os.path.relpath(PMC_TRAFFIC, ROOT) + ":" + "+".join(used)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C3B", "C4", "C2PD", "C3PD"],
-                    help="C3 (default, the metric's config): random dense QP n=4096 m=8192; C2: n=1024 m=2048; "
-                         "C3B: C3 plus 9216 sparse bound / difference rows; C4: KL dual, 2048 outcomes, k=512; "
-                         "C2PD / C3PD: the primal-dual solver (solverType PD) on C2 / C3, steps = its KKT solves")
-    ap.add_argument("--n", type=int, default=None)
-    ap.add_argument("--m", type=int, default=None)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=60.0)
-    args = ap.parse_args()
-
-    import torch
-
-    from cvx_amd import dist as D
+def workload_spec(args, rank):
+    """The per-rank synthetic instance of the selected workload (seed 20261015 + rank): (spec, n, m, SYRK rows, name)."""
     from cvx_amd import problems as Z
-    from cvx_amd.api import SolverParams
-    from cvx_amd.engine import Engine
-
-    rank, local_rank, world = D.env_rank()
-    if world > 1:
-        D.init("nccl")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
     wl = args.workload
     if wl == "C4":
         nout, k = args.m or 2048, (args.n or 513) - 1
@@ -197,21 +195,51 @@ def main():
         syrk_rows = nout  # the B diag(y) B' Hessian: a weighted SYRK over the outcomes; the bound rows are sparse
         workload = (f"C4: KL dual barrier (Dist_KL via Duality), {nout} outcomes, dual dimension {n}, {k} bound rows"
                     f", full barrier Newton iterations")
-    else:
-        n = args.n or (1024 if wl in ("C2", "C2PD") else 4096)
-        m0 = args.m or (2048 if wl in ("C2", "C2PD") else 8192)
-        spec = Z.random_qp_bounds(n, m0, instance=rank) if wl == "C3B" else Z.random_qp(n, m0, instance=rank)
-        m = spec["A"].shape[0]
-        syrk_rows = m0  # dense rows (the sparse rows' Hessian entries are per-entry sums, not SYRK work)
-        workload = (f"{wl}: random dense QP n={n} m={m0}" + (f" plus {m - m0} sparse bound/difference rows"
-                                                               if wl == "C3B" else "") +
-                    (", primal-dual iterations (PrimalDualSolver: KKT-matrix SYRK + 2x Ruiz + Cholesky + solves + "
-                     "residual line search)" if wl.endswith("PD") else
-                     ", full barrier Newton iterations (assembly + Ruiz + Cholesky + solves + line search)") +
-                    " on one MI355X per rank")
+        return spec, n, m, syrk_rows, workload
+    n = args.n or (1024 if wl in ("C2", "C2PD") else 4096)
+    m0 = args.m or (2048 if wl in ("C2", "C2PD") else 8192)
+    spec = Z.random_qp_bounds(n, m0, instance=rank) if wl == "C3B" else Z.random_qp(n, m0, instance=rank)
+    m = spec["A"].shape[0]
+    syrk_rows = m0  # dense rows (the sparse rows' Hessian entries are per-entry sums, not SYRK work)
+    workload = (f"{wl}: random dense QP n={n} m={m0}" + (f" plus {m - m0} sparse bound/difference rows"
+                                                           if wl == "C3B" else "") +
+                (", primal-dual iterations (PrimalDualSolver: KKT-matrix SYRK + 2x Ruiz + Cholesky + solves + "
+                 "residual line search)" if wl.endswith("PD") else
+                 ", full barrier Newton iterations (assembly + Ruiz + Cholesky + solves + line search)") +
+                " on one MI355X per rank")
+    return spec, n, m, syrk_rows, workload
+
+
+def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
+    """The per-rank body of bench.py (config C5 when WORLD_SIZE > 1): process-group init from the torchrun
+    environment, device selection (cuda:LOCAL_RANK), this rank's independent instance on its engine, W untimed and K
+    timed steps bracketed by a barrier + device synchronize on both sides, the MAX of the elapsed time over ranks and
+    one gather of {stats, x} to rank 0 (cvx_amd/dist.py).  engine_cls / backend / device let the world-size-2 gloo
+    test run this same body on the CPU with a stand-in engine.  Returns (result dict, gathered records) on rank 0,
+    (None, None) elsewhere."""
+    import torch
+
+    from cvx_amd import dist as D
+    from cvx_amd.api import SolverParams
+    if engine_cls is None:
+        from cvx_amd.engine import Engine as engine_cls
+
+    rank, local_rank, world = D.env_rank()
+    if world > 1:
+        D.init(backend)
+    if device is None:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    wl = args.workload
+    spec, n, m, syrk_rows, workload = workload_spec(args, rank)
     pars = SolverParams.standardParams()
 
-    eng = Engine(n, m, 0, device=local_rank)
+    eng = engine_cls(n, m, 0, device=local_rank)
     eng.load_problem(spec)
     eng.set_x(spec["x0"])
     state = {"t": 1.0}
@@ -230,17 +258,20 @@ def main():
 
     syrk_ms, chol_ms, solve_ms, ruiz_ms, ls_ms = [], [], [], [], []
 
-    def pd_solve():  # one whole PrimalDualSolver.solve from x0; returns its KKT solves
-        eng.set_x(spec["x0"])
-        s_ = eng.pd_solve(pars)
-        ph = eng.phase_times()
+    def record(ph):
         syrk_ms.append(ph[5])
         ruiz_ms.append(ph[1])
         chol_ms.append(ph[2])
         solve_ms.append(ph[3])
         ls_ms.append(ph[4])
+
+    def pd_solve():  # one whole PrimalDualSolver.solve from x0; returns its KKT solves
+        eng.set_x(spec["x0"])
+        s_ = eng.pd_solve(pars)
+        record(eng.phase_times())
         return s_.newton_steps
 
+    steps = args.steps
     if wl.endswith("PD"):
         eng.set_timing(True)
         pd_solve()  # warm-up solve
@@ -250,85 +281,105 @@ def main():
             one_step()
         eng.set_timing(True)
     D.barrier(device)
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     if wl.endswith("PD"):  # whole solves until at least `steps` KKT solves were timed
         done = 0
-        while done < args.steps:
+        while done < steps:
             done += pd_solve()
-        args.steps = done
-    for _ in range(0 if wl.endswith("PD") else args.steps):
-        st = one_step()
-        ph = eng.phase_times()
-        syrk_ms.append(ph[5])
-        ruiz_ms.append(ph[1])
-        chol_ms.append(ph[2])
-        solve_ms.append(ph[3])
-        ls_ms.append(ph[4])
-    torch.cuda.synchronize()
+        steps = done
+    for _ in range(0 if wl.endswith("PD") else steps):
+        one_step()
+        record(eng.phase_times())
+    sync()
     D.barrier(device)
     elapsed = time.perf_counter() - t0
     elapsed = D.max_over_ranks(elapsed, device)
     eng.set_timing(False)
 
     x_final = eng.get_x()
-    stats = np.array([rank, args.steps, elapsed, state["t"]], dtype=np.float64)
+    stats = np.array([rank, steps, elapsed, state["t"]], dtype=np.float64)
     gathered = D.gather_results(x_final, stats, device)
+    eng.close()
+    if rank != 0:
+        return None, None
 
+    total_steps = steps * world
+    value = total_steps / elapsed
+    syrk = float(np.mean(syrk_ms))
+    chol = float(np.mean(chol_ms))
+    tf = (lambda fl, ms: fl / (ms * 1e-3) / 1e12 if ms > 0 else None)  # noqa: E731
+    flops_syrk = float(syrk_rows) * n * (n + 1)  # lower triangle incl. diagonal
+    ach = tf(flops_syrk, syrk)
+    kkt_ms = float(np.mean(ruiz_ms)) + chol + float(np.mean(solve_ms))
+    flops_chol = n ** 3 / 3.0 + n * n / 2.0 + n / 6.0  # dpotrf flops; all but O(n^2) are trailing SYRK/GEMM
+    frac = (lambda a: a / FP64_MFMA_PEAK_TFLOPS if a is not None else None)  # noqa: E731
+    trailing = {"kernel": "k_chol_dataflow (trailing SYRK/GEMM updates + 64x64 POTRF/TRSM tasks)",
+                "flops_per_launch": flops_chol, "avg_launch_ms": chol, "achieved": tf(flops_chol, chol),
+                "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(tf(flops_chol, chol))}
+    comb_ach = tf(flops_syrk + flops_chol, syrk + chol)
+    combined = {"what": "SURVEY.md §8d: (assembly SYRK + POTRF trailing flops) / (SYRK + Cholesky kernel time)",
+                "achieved": comb_ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(comb_ach)}
+    traffic, traffic_src = (pmc_traffic(("cvxg::k_syrk_direct", "cvxg::k_syrk_reduce")) if wl == "C3"
+                            else (None, None))
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "Newton KKT solves/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded generators of cvx_amd/problems.py, SURVEY.md §8d)",
+        "config": {"workload": workload, "n": n, "m": m,
+                   "parallelism": f"replicas x{world}: one independent QP per GPU (config C5), "
+                                  "RCCL gather of results after the timed region"},
+        "roofline": {"bound": "mfma", "kernel": "k_syrk_direct (H = tP + A'diag(w)A)",
+                     "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": frac(ach), "traffic": traffic,
+                     "traffic_unit": "bytes/assembly (main wave + split-K tail + reduce)",
+                     "traffic_source": traffic_src,
+                     "flops_per_launch": flops_syrk, "avg_launch_ms": syrk,
+                     "trailing": trailing, "combined": combined},
+        "phases_ms": {"syrk": syrk, "ruiz": float(np.mean(ruiz_ms)), "cholesky_fused_fwd": chol,
+                      "bwd_solve_residual": float(np.mean(solve_ms)), "line_search": float(np.mean(ls_ms))},
+        "kkt_factor_solve_per_s": 1e3 / kkt_ms if kkt_ms > 0 else None,
+        "cholesky_tflops": tf(n ** 3 / 3, chol),
+        "gathered_ranks": len(gathered),
+    }
+    return out, gathered
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C3B", "C4", "C2PD", "C3PD"],
+                    help="C3 (default, the metric's config): random dense QP n=4096 m=8192; C2: n=1024 m=2048; "
+                         "C3B: C3 plus 9216 sparse bound / difference rows; C4: KL dual, 2048 outcomes, k=512; "
+                         "C2PD / C3PD: the primal-dual solver (solverType PD) on C2 / C3, steps = its KKT solves")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=30.0)
+    args = ap.parse_args()
+
+    from cvx_amd import dist as D
+    rank, _, world = D.env_rank()
+    out, _ = run_rank(args)
     if rank == 0:
-        total_steps = args.steps * world
-        value = total_steps / elapsed
-        syrk = float(np.mean(syrk_ms))
-        flops_syrk = float(syrk_rows) * n * (n + 1)  # lower triangle incl. diagonal
-        ach = flops_syrk / (syrk * 1e-3) / 1e12
-        chol = float(np.mean(chol_ms))
-        kkt_ms = float(np.mean(ruiz_ms)) + chol + float(np.mean(solve_ms))
-        flops_chol = n ** 3 / 3.0 + n * n / 2.0 + n / 6.0  # dpotrf flops; all but O(n^2) are trailing SYRK/GEMM
-        trailing = {"kernel": "k_chol_dataflow (trailing SYRK/GEMM updates + 64x64 POTRF/TRSM tasks)",
-                    "flops_per_launch": flops_chol, "avg_launch_ms": chol,
-                    "achieved": flops_chol / (chol * 1e-3) / 1e12, "peak": FP64_MFMA_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": flops_chol / (chol * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS}
-        comb_ach = (flops_syrk + flops_chol) / ((syrk + chol) * 1e-3) / 1e12
-        combined = {"what": "SURVEY.md §8d: (assembly SYRK + POTRF trailing flops) / (SYRK + Cholesky kernel time)",
-                    "achieved": comb_ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": comb_ach / FP64_MFMA_PEAK_TFLOPS}
-        traffic, traffic_src = (pmc_traffic(("cvxg::k_syrk_direct", "cvxg::k_syrk_reduce")) if wl == "C3"
-                                else (None, None))
-        out = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "Newton KKT solves/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (seeded generators of cvx_amd/problems.py, SURVEY.md §8d)",
-            "config": {"workload": workload, "n": n, "m": m,
-                       "parallelism": f"replicas x{world}: one independent QP per GPU (config C5), "
-                                      "RCCL gather of results after the timed region"},
-            "roofline": {"bound": "mfma", "kernel": "k_syrk_direct (H = tP + A'diag(w)A)",
-                         "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic, "traffic_unit": "bytes/assembly (main wave + split-K tail + reduce)",
-                         "traffic_source": traffic_src,
-                         "flops_per_launch": flops_syrk, "avg_launch_ms": syrk,
-                         "trailing": trailing, "combined": combined},
-            "phases_ms": {"syrk": syrk, "ruiz": float(np.mean(ruiz_ms)), "cholesky_fused_fwd": chol,
-                          "bwd_solve_residual": float(np.mean(solve_ms)), "line_search": float(np.mean(ls_ms))},
-            "kkt_factor_solve_per_s": 1e3 / kkt_ms,
-            "cholesky_tflops": (n ** 3 / 3) / (chol * 1e-3) / 1e12,
-            "gathered_ranks": len(gathered),
-        }
-        if not args.no_cpu_baseline and world == 1 and wl == "C3":
+        if not args.no_cpu_baseline and world == 1 and args.workload == "C3":
+            spec = workload_spec(args, 0)[0]
             out["cpu_baseline"] = cpu_baseline(spec, args.cpu_budget)
             out["cpu_baseline_blas"] = cpu_baseline_blas(spec)
         elif not args.no_cpu_baseline:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

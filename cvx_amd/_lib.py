@@ -94,6 +94,10 @@ SIGNATURES = {
     "cvxg_newton_step": (C.c_int, [_P, C.POINTER(cvxg_params), C.POINTER(cvxg_step_info)]),
     "cvxg_centering": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, C.POINTER(cvxg_centering_info)]),
     "cvxg_barrier_solve": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_int, C.POINTER(cvxg_solution)]),
+    "cvxg_batch_barrier_solve": (C.c_int, [C.c_int, C.POINTER(_P), C.POINTER(cvxg_params), C.c_int,
+                                           C.POINTER(cvxg_solution), C.POINTER(C.c_int)]),
+    "cvxg_batch_newton_step": (C.c_int, [C.c_int, C.POINTER(_P), C.POINTER(cvxg_params), C.POINTER(cvxg_step_info),
+                                         C.POINTER(C.c_int)]),
     "cvxg_pd_direction": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, _D, _D, _D, _D,
                                     C.POINTER(cvxg_pd_step_info)]),
     "cvxg_pd_solve": (C.c_int, [_P, C.POINTER(cvxg_params), C.POINTER(cvxg_pd_solution)]),

@@ -16,7 +16,7 @@
 #include <limits>
 #include <queue>
 #include <string>
-#include <vector>
+#include <thread>
 #include <vector>
 
 #include "../../include/cvxg.h"
@@ -1713,6 +1713,47 @@ int cvxg_barrier_solve(cvxg_ctx* ctx, const cvxg_params* pars, int termination, 
     sol->newton_steps = total;
   }
   return CVXG_OK;
+}
+
+// ---- config C5 in one host process (SURVEY.md §8b cvxg_batch_*): independent contexts, one host thread each --------
+// Each context owns its device, stream and buffers, so the solves run concurrently with no exchange; a context is only
+// ever touched by the one thread that runs it (the contexts are not thread-safe, the batch is).  status[i] = the
+// context's own return code; the call returns the first non-zero one (CVXG_OK when all succeed).
+extern "C++" {
+template <class F>
+static int batch_run(int count, cvxg_ctx* const* ctxs, int* status, F one) {
+  if (count < 0 || (count > 0 && !ctxs)) return CVXG_E_ARG;
+  for (int i = 0; i < count; ++i)
+    for (int j = 0; j < i; ++j)
+      if (!ctxs[i] || ctxs[i] == ctxs[j]) return CVXG_E_ARG;  // one thread per distinct context
+  std::vector<int> rc(count, CVXG_OK);
+  std::vector<std::thread> th;
+  th.reserve(count);
+  for (int i = 0; i < count; ++i) th.emplace_back([&, i]() { rc[i] = one(i); });
+  for (auto& t : th) t.join();
+  int first = CVXG_OK;
+  for (int i = 0; i < count; ++i) {
+    if (status) status[i] = rc[i];
+    if (first == CVXG_OK) first = rc[i];
+  }
+  return first;
+}
+}  // extern "C++"
+
+int cvxg_batch_barrier_solve(int count, cvxg_ctx* const* ctxs, const cvxg_params* pars, int termination,
+                             cvxg_solution* sols, int* status) {
+  if (!pars) return CVXG_E_ARG;
+  return batch_run(count, ctxs, status,
+                   [&](int i) { return cvxg_barrier_solve(ctxs[i], pars, termination, sols ? &sols[i] : nullptr); });
+}
+
+int cvxg_batch_newton_step(int count, cvxg_ctx* const* ctxs, const cvxg_params* pars, cvxg_step_info* infos,
+                           int* status) {
+  if (!pars) return CVXG_E_ARG;
+  return batch_run(count, ctxs, status, [&](int i) {
+    cvxg_step_info tmp;
+    return cvxg_newton_step(ctxs[i], pars, infos ? &infos[i] : &tmp);
+  });
 }
 
 int cvxg_set_timing(cvxg_ctx* ctx, int enabled) {

@@ -252,6 +252,31 @@ class Engine:
         return ms
 
 
+def batch_barrier_solve(engines, pars, termination: int = 0):
+    """cvxg_batch_barrier_solve: the barrier solves of independent engines (one per GPU, config C5) concurrently from
+    one process, one host thread per context.  Returns ([cvxg_solution], [status])."""
+    lib = L.lib()
+    k = len(engines)
+    hs = (C.c_void_p * k)(*[e.h.value for e in engines])
+    sols = (L.cvxg_solution * k)()
+    st = (C.c_int * k)()
+    ps = params_struct(pars)
+    lib.cvxg_batch_barrier_solve(k, hs, C.byref(ps), int(termination), sols, st)
+    return list(sols), list(st)
+
+
+def batch_newton_step(engines, pars):
+    """cvxg_batch_newton_step: one inner Newton iteration on each engine concurrently.  Returns ([info], [status])."""
+    lib = L.lib()
+    k = len(engines)
+    hs = (C.c_void_p * k)(*[e.h.value for e in engines])
+    infos = (L.cvxg_step_info * k)()
+    st = (C.c_int * k)()
+    ps = params_struct(pars)
+    lib.cvxg_batch_newton_step(k, hs, C.byref(ps), infos, st)
+    return list(infos), list(st)
+
+
 def solution_space(A, b, device: int = 0):
     """SolutionSpace(A, b) on the device (cvxg_solution_space; MatrixUtils.solveUnderdetermined): returns (z0, F)
     with F n x (n-p) column-orthonormal, A F = 0 and A z0 = b."""

@@ -183,6 +183,19 @@ int cvxg_centering(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg_center
  * CvxUtils.phase_I_TerminationCriterion (CvxUtils.scala:61-87). */
 int cvxg_barrier_solve(cvxg_ctx* ctx, const cvxg_params* pars, int termination, cvxg_solution* sol);
 
+/* ---- config C5 from one host process (a JVM caller): a batch of independent instances ------------------------ */
+
+/* Run cvxg_barrier_solve / cvxg_newton_step on `count` distinct contexts concurrently, one host thread per context
+ * (typically one context per GPU, each created on its own device with cvxg_create): the one-instance-per-GPU batch of
+ * config C5 without a second process.  Nothing is exchanged between instances; afterwards each instance's x is read
+ * with cvxg_get_x (the in-process counterpart of the RCCL gather of the multi-process path).  sols / infos[i] receive
+ * context i's result (may be NULL), status[i] its return code (may be NULL); the call returns the first non-zero
+ * status, CVXG_E_ARG for a NULL or repeated context. */
+int cvxg_batch_barrier_solve(int count, cvxg_ctx* const* ctxs, const cvxg_params* pars, int termination,
+                             cvxg_solution* sols, int* status);
+int cvxg_batch_newton_step(int count, cvxg_ctx* const* ctxs, const cvxg_params* pars, cvxg_step_info* infos,
+                           int* status);
+
 /* ---- primal-dual interior-point solver (PrimalDualSolver.scala, solverType "PD") ---------------- */
 
 /* One primal-dual iteration as PrimalDualSolver.solve_noEQs runs it (PrimalDualSolver.scala:421-427). */

@@ -353,6 +353,43 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_barrierSolve(JNIEnv* env, jclass 
   return rc;
 }
 
+/* batchBarrierSolve(handles[k], maxIter, params[6], termination, out[9 k], status[k]): config C5 from one JVM —
+ * the barrier solves of k independent contexts (one per GPU) concurrently (cvxg_batch_barrier_solve) */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_batchBarrierSolve(JNIEnv* env, jclass cls, jlongArray handles,
+                                                                 jint maxIter, jdoubleArray jp, jint termination,
+                                                                 jdoubleArray out, jintArray status) {
+  (void)cls;
+  cvxg_params p;
+  fill_params(env, jp, maxIter, &p);
+  jsize k = (*env)->GetArrayLength(env, handles);
+  jlong* hv = (jlong*)malloc((size_t)(k > 0 ? k : 1) * sizeof(jlong));
+  cvxg_ctx** cv = (cvxg_ctx**)malloc((size_t)(k > 0 ? k : 1) * sizeof(cvxg_ctx*));
+  cvxg_solution* sv = (cvxg_solution*)malloc((size_t)(k > 0 ? k : 1) * sizeof(cvxg_solution));
+  jint* st = (jint*)malloc((size_t)(k > 0 ? k : 1) * sizeof(jint));
+  double* o = (double*)malloc((size_t)(k > 0 ? 9 * k : 1) * sizeof(double));
+  if (!hv || !cv || !sv || !st || !o) {
+    free(hv), free(cv), free(sv), free(st), free(o);
+    throw_oom(env);
+    return CVXG_E_ARG;
+  }
+  if (k > 0) (*env)->GetLongArrayRegion(env, handles, 0, k, hv);
+  for (jsize i = 0; i < k; ++i) cv[i] = CTX(hv[i]);
+  jint rc = cvxg_batch_barrier_solve(k, cv, &p, termination, sv, (int*)st);
+  for (jsize i = 0; i < k; ++i) {
+    const cvxg_solution* s = &sv[i];
+    double* r = o + 9 * i;
+    r[0] = s->duality_gap, r[1] = s->equality_gap, r[2] = s->newton_decrement, r[3] = s->norm_grad;
+    r[4] = s->objective, r[5] = (double)s->iter, r[6] = (double)s->maxed_out, r[7] = (double)s->outer_iters;
+    r[8] = (double)s->newton_steps;
+  }
+  if (k > 0) {
+    (*env)->SetDoubleArrayRegion(env, out, 0, 9 * k, o);
+    (*env)->SetIntArrayRegion(env, status, 0, k, st);
+  }
+  free(hv), free(cv), free(sv), free(st), free(o);
+  return rc;
+}
+
 /* ---- primal-dual solver --------------------------------------------------------------------------------- */
 
 /* pdSolve(h, maxIter, params[6], out[6]) -> PrimalDualSolver.solve on the device (cvxg_pd_solve) */

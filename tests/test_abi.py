@@ -67,7 +67,7 @@ def test_bad_arguments_rejected(lib):
     assert lib.cvxg_newton_step(None, None, None) == _lib.CVXG_E_ARG
 
 
-# A stand-in for the few JNI declarations jni/cvxg_jni.c uses, with the JDK's C signatures (jni.h: JNIEnv is a
+# A stand-in for the few (nine) JNI declarations jni/cvxg_jni.c uses, with the JDK's C signatures (jni.h: JNIEnv is a
 # pointer to the function table; jdoubleArray / jintArray are jarray = jobject).  A compile check of the glue only:
 # it proves nothing about JVM linkage.
 _JNI_STANDIN = r"""
@@ -83,6 +83,7 @@ typedef jobject jstring;
 typedef jobject jarray;
 typedef jarray jdoubleArray;
 typedef jarray jintArray;
+typedef jarray jlongArray;
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_* JNIEnv;
 struct JNINativeInterface_ {
@@ -91,6 +92,7 @@ struct JNINativeInterface_ {
   jstring (*NewStringUTF)(JNIEnv*, const char*);
   jsize (*GetArrayLength)(JNIEnv*, jarray);
   void (*GetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, jint*);
+  void (*GetLongArrayRegion)(JNIEnv*, jlongArray, jsize, jsize, jlong*);
   void (*GetDoubleArrayRegion)(JNIEnv*, jdoubleArray, jsize, jsize, jdouble*);
   void (*SetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, const jint*);
   void (*SetDoubleArrayRegion)(JNIEnv*, jdoubleArray, jsize, jsize, const jdouble*);
@@ -118,6 +120,6 @@ def test_jni_glue_binds_every_scala_native_and_every_step_entry():
     scala_names = set(re.findall(r"@native def (\w+)", doc))
     assert c_names == scala_names, (c_names ^ scala_names)
     for s in ("centering", "centeringBegin", "centeringResume", "newtonStep", "newtonDirection", "barrierEval",
-              "constraintValues", "activeSet", "setQuad"):
+              "constraintValues", "activeSet", "setQuad", "batchBarrierSolve"):
         assert s in c_names
     assert "GetPrimitiveArrayCritical" not in c_src  # no critical region spans a GPU call

@@ -1030,3 +1030,42 @@ def test_regularized_cholesky_retry_branch(mods):
     err_perp = (ye - yr) - q * (q @ (ye - yr))
     assert np.linalg.norm(err_perp) <= 64 * u * (w[-1] / w[1]) * np.linalg.norm(yr)
     assert np.linalg.norm(dx - dref) <= 64 * u * (w[-1] / w[0]) * np.linalg.norm(dref)
+
+
+def test_batch_barrier_solve_matches_single_contexts(mods):
+    """cvxg_batch_barrier_solve / cvxg_batch_newton_step (config C5 from one host process, one thread per context):
+    three independent instances solved concurrently give bitwise the x, step counts and gaps of three one-at-a-time
+    cvxg_barrier_solve calls; a repeated context is rejected."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.engine import batch_barrier_solve, batch_newton_step
+    pars = SP.standardParams()
+    specs = [Z.random_qp(48, 100, instance=60 + i) for i in range(3)]
+    ref = []
+    for spec in specs:
+        e = _engine(Engine, spec)
+        e.set_x(spec["x0"])
+        s = e.barrier_solve(pars, 0)
+        ref.append((e.get_x(), s.newton_steps, s.duality_gap))
+        e.close()
+    engs = [_engine(Engine, spec) for spec in specs]
+    for e, spec in zip(engs, specs):
+        e.set_x(spec["x0"])
+    sols, st = batch_barrier_solve(engs, pars, 0)
+    assert st == [0, 0, 0]
+    for e, s, (x, steps, gap) in zip(engs, sols, ref):
+        assert np.array_equal(e.get_x(), x)
+        assert s.newton_steps == steps and s.duality_gap == gap
+    for e, spec in zip(engs, specs):
+        e.set_x(spec["x0"])
+        e.centering_begin(1.0)
+    infos, st = batch_newton_step(engs, pars)
+    assert st == [0, 0, 0] and all(i.took_step == 1 for i in infos)
+    import ctypes as C
+
+    from cvx_amd import _lib
+    from cvx_amd.engine import params_struct
+    hs = (C.c_void_p * 2)(engs[0].h.value, engs[0].h.value)
+    ps = params_struct(pars)
+    assert _lib.lib().cvxg_batch_newton_step(2, hs, C.byref(ps), None, None) == _lib.CVXG_E_ARG
+    for e in engs:
+        e.close()
