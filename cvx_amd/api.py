@@ -13,8 +13,8 @@ read like the reference:
                                     loop runs on the MI355X engine (libcvxg.so) behind the C-ABI
 * OptimizationProblem ............. OptimizationProblem.scala:133-196 (solverType "BR" = this engine)
 
-Eligibility: quadratic or linear objective, linear inequality constraints, optional
-EqualityConstraint with at most CVXG_MAX_EQ rows.  Anything else raises TypeError — the reference's
+Eligibility: quadratic or linear objective, linear (and quadratic) inequality constraints, optional
+EqualityConstraint (any number of rows p < n).  Anything else raises TypeError — the reference's
 CPU BarrierSolver remains the path for general callbacks.
 """
 from __future__ import annotations
@@ -433,8 +433,6 @@ class GpuBarrierSolver:
         if cnts.feasiblePoint is None:
             raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
         p = 0 if eqs is None else eqs.A.shape[0]
-        if p > _lib.CVXG_MAX_EQ:
-            raise TypeError(f"GPU barrier engine: at most {_lib.CVXG_MAX_EQ} equality rows")
         self.objF, self.cnts, self.eqs, self.pars = objF, cnts, eqs, pars
         self.device = device
         self.dim = cnts.dim

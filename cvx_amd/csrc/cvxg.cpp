@@ -58,6 +58,10 @@ struct cvxg_ctx {
   double *Px = nullptr, *Ps = nullptr, *e = nullptr;
   double *c = nullptr, *d = nullptr, *invd = nullptr, *w = nullptr, *logd = nullptr;
   double *eqd = nullptr, *eqtmp = nullptr;  // b - Aeq x
+  // wide KKT path (p + 1 > MAX_RHS): column-major [B' | Dq] -> X, R = B X, S, z; rocBLAS / rocSOLVER handle
+  double *kY = nullptr, *kR = nullptr, *kS = nullptr, *kzp = nullptr;
+  int* kinfo = nullptr;
+  void* blas = nullptr;
   // matrices
   double *H = nullptr, *L = nullptr, *Linv = nullptr, *Hsave = nullptr;
   double *ruiz0 = nullptr, *ruiz1 = nullptr, *dfin = nullptr, *hdiag = nullptr;
@@ -713,33 +717,11 @@ static int newton_direction_p0(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step
   return CVXG_OK;
 }
 
-// KKTSystem.solvePD(Hm, Aeq, q, b) (KKTSystem.scala:200-246) with the block elimination of
-// solveWithCholFactor (:99-167); Hm = ctx->H, q = qv (device n-vector), b = bv (device p-vector).
-static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
+// The accuracy check of KKTSystem.solveWithCholFactor (KKTSystem.scala:147-166) on the equilibrated system, with the
+// solution y = ctx->kx (Q y + B'w = -Dq, B y = b) and w = ctx->kw; x = D y into ctx->dx.
+static int kkt_residual_check(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
   hipStream_t s = ctx->s;
-  const int n = ctx->n, np = ctx->np, p = ctx->p, nr = p + 1;
-  tstart(ctx, 1);
-  ruiz(ctx);
-  tstop(ctx, 1);
-  tstart(ctx, 2);
-  int reg = 0;
-  double mind = 0.0;
-  int rc = regularized_cholesky(
-      ctx, nr,
-      [&]() {
-        launch_kkt_prep(s, ctx->Aeq, np, p, n, np, ctx->dfin, ctx->kB, ctx->rhs, nr);  // B = A diag(d), B'
-        launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, nr, p, ctx->rhs);            // D q
-      },
-      &reg, &mind);
-  tstop(ctx, 2);
-  info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
-  info->regularized = reg;
-  info->min_diag = mind;
-  if (rc != CVXG_OK) return rc;
-  tstart(ctx, 3);
-  backward_solve(ctx, nr);  // X = H^-1 [B' | Dq]
-  launch_ctrl_reset_chol(s, ctx->ctrl);
-  launch_kkt_schur(s, ctx->sol, nr, ctx->kB, np, p, np, bv, ctx->kw, ctx->kx, ctx->ctrl);
+  const int n = ctx->n, np = ctx->np, p = ctx->p;
   // residual_1 = Q y + B' w + Dq  with  Q y = d o (H (d o y)), relative to -Dq   (:148-150)
   launch_scale_vec(s, ctx->kx, ctx->dfin, np, ctx->xtmp);
   launch_rowdot(s, ctx->H, np, n, np, ctx->xtmp, ctx->vtmp);
@@ -768,17 +750,103 @@ static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, doubl
   return CVXG_OK;
 }
 
+// KKTSystem.solvePD(Hm, Aeq, q, b) (KKTSystem.scala:200-246) with the block elimination of
+// solveWithCholFactor (:99-167); Hm = ctx->H, q = qv (device n-vector), b = bv (device p-vector).
+// p + 1 <= MAX_RHS: the n x (p+1) right-hand side [B' | Dq] rides the factorization's fused forward solve and the
+// one-launch backward solve, and one workgroup forms and factors the p x p Schur complement (k_kkt_schur).
+static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
+  hipStream_t s = ctx->s;
+  const int n = ctx->n, np = ctx->np, p = ctx->p, nr = p + 1;
+  tstart(ctx, 1);
+  ruiz(ctx);
+  tstop(ctx, 1);
+  tstart(ctx, 2);
+  int reg = 0;
+  double mind = 0.0;
+  int rc = regularized_cholesky(
+      ctx, nr,
+      [&]() {
+        launch_kkt_prep(s, ctx->Aeq, np, p, n, np, ctx->dfin, ctx->kB, ctx->rhs, nr);  // B = A diag(d), B'
+        launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, nr, p, ctx->rhs);            // D q
+      },
+      &reg, &mind);
+  tstop(ctx, 2);
+  info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
+  info->regularized = reg;
+  info->min_diag = mind;
+  if (rc != CVXG_OK) return rc;
+  tstart(ctx, 3);
+  backward_solve(ctx, nr);  // X = H^-1 [B' | Dq]
+  launch_ctrl_reset_chol(s, ctx->ctrl);
+  launch_kkt_schur(s, ctx->sol, nr, ctx->kB, np, p, np, bv, ctx->kw, ctx->kx, ctx->ctrl);
+  return kkt_residual_check(ctx, qv, bv, tol, info);
+}
+
+// The same for p + 1 > MAX_RHS (any number of equality rows): the factorization carries only Dq; the whole
+// [B' | Dq] (column-major n x (p+1)) is solved with the factor by two triangular solves, R = B X by a GEMM, and the
+// p x p Schur complement S = (R + R')/2 is factored by LAPACK dpotrf -- the reference's own sequence
+// (MatrixUtils.triangularSolve = dtrtrs, KKTSystem.scala:120-144), as rocBLAS / rocSOLVER calls (kkt_wide.cpp).
+static int kkt_solve_pd_wide(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
+  hipStream_t s = ctx->s;
+  const int n = ctx->n, np = ctx->np, p = ctx->p, nr = p + 1;
+  if (!ctx->blas) {
+    if (lib_handle_create(s, &ctx->blas) != 0) return set_err(ctx, CVXG_E_HIP, "rocBLAS handle creation failed");
+    CHK(dalloc(ctx, &ctx->kY, (size_t)np * nr));
+    CHK(dalloc(ctx, &ctx->kR, (size_t)p * nr));
+    CHK(dalloc(ctx, &ctx->kS, (size_t)p * p));
+    CHK(dalloc(ctx, &ctx->kzp, (size_t)p));
+    CHK(dalloc(ctx, &ctx->kinfo, 1));
+  }
+  tstart(ctx, 1);
+  ruiz(ctx);
+  tstop(ctx, 1);
+  tstart(ctx, 2);
+  int reg = 0;
+  double mind = 0.0;
+  int rc = regularized_cholesky(
+      ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, 1, 0, ctx->rhs); }, &reg, &mind);
+  tstop(ctx, 2);
+  info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
+  info->regularized = reg;
+  info->min_diag = mind;
+  if (rc != CVXG_OK) return rc;
+  tstart(ctx, 3);
+  launch_kkt_prep_cm(s, ctx->Aeq, np, p, n, np, ctx->dfin, qv, ctx->kB, ctx->kY);  // B = A diag(d); Y = [B' | Dq]
+  bool ok = lib_llt_solve(ctx->blas, n, nr, ctx->L, np, ctx->kY, np) == 0;            // X = Q^-1 Y   (:120-121)
+  // R = B X (p x (p+1)); column p = B Hinv_q   (:126, :141)
+  ok = ok && lib_gemm_h(ctx->blas, true, false, p, nr, n, 1.0, ctx->kB, np, ctx->kY, np, 0.0, ctx->kR, p) == 0;
+  launch_kkt_sym(s, ctx->kR, p, bv, ctx->kS, ctx->kzp);  // S = (R + R')/2, z = -(b + B Hinv_q)  (:139-141)
+  ok = ok && lib_potrf(ctx->blas, p, ctx->kS, p, ctx->kinfo) == 0;  // K = cholesky(S)  (:140)
+  HIPC(ctx, hipGetLastError());
+  int hinfo = 0;
+  CHK(copy_sync(ctx, &hinfo, ctx->kinfo, sizeof(int), hipMemcpyDeviceToHost));
+  if (!ok) return set_err(ctx, CVXG_E_HIP, "KKT (p = %d): rocBLAS / rocSOLVER call failed", p);
+  if (hinfo != 0) return set_err(ctx, CVXG_E_NOT_PD, "KKT Schur complement not positive definite (dpotrf info %d)", hinfo);
+  ok = lib_potrs(ctx->blas, p, ctx->kS, p, ctx->kzp) == 0;  // w: K u = z, K' w = u  (:143-144)
+  HIPC(ctx, hipMemcpyAsync(ctx->kw, ctx->kzp, (size_t)p * sizeof(double), hipMemcpyDeviceToDevice, s));
+  // y = -(Hinv_q + Hinv_At w)  (:145)
+  HIPC(ctx, hipMemcpyAsync(ctx->kx, ctx->kY + (size_t)p * np, (size_t)np * sizeof(double), hipMemcpyDeviceToDevice, s));
+  ok = ok && lib_gemv_h(ctx->blas, np, p, -1.0, ctx->kY, np, ctx->kw, -1.0, ctx->kx) == 0;
+  if (!ok) return set_err(ctx, CVXG_E_HIP, "KKT (p = %d): rocBLAS / rocSOLVER call failed", p);
+  launch_ctrl_reset_chol(s, ctx->ctrl);
+  return kkt_residual_check(ctx, qv, bv, tol, info);
+}
+
+static int kkt_solve_any(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
+  return ctx->p + 1 <= MAX_RHS ? kkt_solve_pd(ctx, qv, bv, tol, info) : kkt_solve_pd_wide(ctx, qv, bv, tol, info);
+}
+
 // KKTSystem.solve (KKTSystem.scala:43-66): solvePD(H) -> solvePD(H + A'A, q - A'b) -> kktSymSolve.
 static int newton_direction_kkt(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
   hipStream_t s = ctx->s;
-  int rc = kkt_solve_pd(ctx, ctx->y, ctx->eqd, pars->tolEqSolve, info);
+  int rc = kkt_solve_any(ctx, ctx->y, ctx->eqd, pars->tolEqSolve, info);
   info->fallback = 0;
   if (rc == CVXG_OK || rc == CVXG_E_HIP) return rc;
   const size_t bytes = (size_t)ctx->np * ctx->np * sizeof(double);
   HIPC(ctx, hipMemcpyAsync(ctx->Hsave, ctx->H, bytes, hipMemcpyDeviceToDevice, s));
   launch_add_ata(s, ctx->H, ctx->np, ctx->Aeq, ctx->p, ctx->n);
   launch_q_minus_atb(s, ctx->y, ctx->Aeq, ctx->np, ctx->p, ctx->eqd, ctx->n, ctx->e);
-  rc = kkt_solve_pd(ctx, ctx->e, ctx->eqd, pars->tolEqSolve, info);
+  rc = kkt_solve_any(ctx, ctx->e, ctx->eqd, pars->tolEqSolve, info);
   HIPC(ctx, hipMemcpyAsync(ctx->H, ctx->Hsave, bytes, hipMemcpyDeviceToDevice, s));
   info->fallback = 1;
   if (rc == CVXG_OK || rc == CVXG_E_HIP) {
@@ -1089,7 +1157,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   if (!out) return CVXG_E_ARG;
   *out = nullptr;
   if (n <= 0 || m < 0 || p < 0) return CVXG_E_DIM;
-  if (p > CVXG_MAX_EQ) return CVXG_E_UNSUPPORTED;
+  if (p > 0 && p >= n) return CVXG_E_DIM;  // EqualityConstraint: A.rows < A.cols (EqualityConstraint.scala:18-20)
   // the dataflow Cholesky encodes tile indices in 10 bits (nblk <= 1023, n <= 65472; H alone is 34 GB there)
   if (n > 1023 * NB) return CVXG_E_UNSUPPORTED;
   cvxg_ctx* ctx = new cvxg_ctx();
@@ -1112,17 +1180,18 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     std::vector<double> one(mp, 1.0);
     CHK(copy_sync(ctx, ctx->ub, one.data(), mp * sizeof(double), hipMemcpyHostToDevice));
   }
+  const size_t pe = std::max(p, CVXG_MAX_EQ);  // equality-row buffers
   if (p > 0) {
-    CHK(dalloc(ctx, &ctx->Aeq, (size_t)CVXG_MAX_EQ * np));
-    CHK(dalloc(ctx, &ctx->beq, CVXG_MAX_EQ));
-    CHK(dalloc(ctx, &ctx->kB, (size_t)CVXG_MAX_EQ * np));
+    CHK(dalloc(ctx, &ctx->Aeq, pe * np));
+    CHK(dalloc(ctx, &ctx->beq, pe));
+    CHK(dalloc(ctx, &ctx->kB, pe * np));
     CHK(dalloc(ctx, &ctx->Hsave, np * np));
   }
-  CHK(dalloc(ctx, &ctx->kw, CVXG_MAX_EQ));
+  CHK(dalloc(ctx, &ctx->kw, pe));
   CHK(dalloc(ctx, &ctx->kx, np));
   CHK(dalloc(ctx, &ctx->kz, np));
-  CHK(dalloc(ctx, &ctx->eqd, CVXG_MAX_EQ));
-  CHK(dalloc(ctx, &ctx->eqtmp, CVXG_MAX_EQ));
+  CHK(dalloc(ctx, &ctx->eqd, pe));
+  CHK(dalloc(ctx, &ctx->eqtmp, pe));
   for (double** v : {&ctx->x, &ctx->y, &ctx->dx, &ctx->sdir, &ctx->xtmp, &ctx->vtmp, &ctx->Px, &ctx->Ps, &ctx->ruiz0,
                      &ctx->ruiz1, &ctx->dfin, &ctx->hdiag})
     CHK(dalloc(ctx, v, np));
@@ -1207,6 +1276,9 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->Psa, ctx->xtr, ctx->Pxtr, ctx->c_tr, ctx->d_tr, ctx->invd_tr, ctx->w_tr, ctx->logd_tr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (void* p : {(void*)ctx->kY, (void*)ctx->kR, (void*)ctx->kS, (void*)ctx->kzp, (void*)ctx->kinfo})
+    if (p) (void)hipFree(p);
+  lib_handle_destroy(ctx->blas);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
   if (ctx->hls) (void)hipHostFree(ctx->hls);
   if (ctx->pd_hout) (void)hipHostFree(ctx->pd_hout);
@@ -1435,10 +1507,11 @@ int cvxg_set_eq(cvxg_ctx* ctx, const double* Aeq, int ldAeq, int row_major, cons
   if (ctx->p == 0) return CVXG_OK;
   if (!Aeq || !beq) return CVXG_E_ARG;
   HIPC(ctx, hipSetDevice(ctx->dev));
-  CHK(upload_mat(ctx, ctx->Aeq, ctx->np, CVXG_MAX_EQ, Aeq, ctx->p, ctx->n, ldAeq, row_major));
-  std::vector<double> b(CVXG_MAX_EQ, 0.0);
+  const int pe = std::max(ctx->p, CVXG_MAX_EQ);
+  CHK(upload_mat(ctx, ctx->Aeq, ctx->np, pe, Aeq, ctx->p, ctx->n, ldAeq, row_major));
+  std::vector<double> b(pe, 0.0);
   memcpy(b.data(), beq, ctx->p * sizeof(double));
-  CHK(copy_sync(ctx, ctx->beq, b.data(), CVXG_MAX_EQ * sizeof(double), hipMemcpyHostToDevice));
+  CHK(copy_sync(ctx, ctx->beq, b.data(), pe * sizeof(double), hipMemcpyHostToDevice));
   ctx->have_eq = 1;
   ctx->x_eval_valid = 0;
   return CVXG_OK;

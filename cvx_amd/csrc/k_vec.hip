@@ -754,6 +754,39 @@ void launch_kkt_prep(hipStream_t s, const double* Aeq, int ld, int p, int n, int
   k_kkt_prep<<<(np + 255) / 256, 256, 0, s>>>(Aeq, ld, p, n, np, d, B, rhs, nrhs);
 }
 
+// Wide KKT path: B = Aeq diag(d) (p x ld, row-major) and the column-major n x (p+1) right-hand side Y = [B' | Dq]
+// (KKTSystem.scala:114-118), leading dimension np (padding rows zero)
+__global__ void k_kkt_prep_cm(const double* __restrict__ Aeq, int ld, int p, int n, int np, const double* __restrict__ d,
+                              const double* __restrict__ q, double* __restrict__ B, double* __restrict__ Y) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int a = blockIdx.y;  // 0..p (p: the Dq column)
+  if (i >= np) return;
+  if (a < p) {
+    const double b = (i < n) ? d[i] * Aeq[(size_t)a * ld + i] : 0.0;
+    B[(size_t)a * ld + i] = b;
+    Y[(size_t)a * np + i] = b;
+  } else {
+    Y[(size_t)p * np + i] = (i < n) ? d[i] * q[i] : 0.0;
+  }
+}
+void launch_kkt_prep_cm(hipStream_t s, const double* Aeq, int ld, int p, int n, int np, const double* d,
+                        const double* q, double* B, double* Y) {
+  k_kkt_prep_cm<<<dim3((np + 255) / 256, p + 1), 256, 0, s>>>(Aeq, ld, p, n, np, d, q, B, Y);
+}
+
+// S = (R + R')/2 (KKTSystem.scala:139) and z = -(b + R[:, p]) (:141) from R = B X (p x (p+1), column-major)
+__global__ void k_kkt_sym(const double* __restrict__ R, int p, const double* __restrict__ b, double* __restrict__ S,
+                          double* __restrict__ z) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p * p) return;
+  const int r = i % p, c = i / p;
+  S[i] = (R[(size_t)c * p + r] + R[(size_t)r * p + c]) * 0.5;
+  if (c == 0) z[r] = -(b[r] + R[(size_t)p * p + r]);
+}
+void launch_kkt_sym(hipStream_t s, const double* R, int p, const double* b, double* S, double* z) {
+  k_kkt_sym<<<(p * p + 255) / 256, 256, 0, s>>>(R, p, b, S, z);
+}
+
 // out = u + alpha*v elementwise with a strided source column: out_i = u_i + alpha * v[i*vs + vc]
 __global__ void k_axpy_strided(const double* __restrict__ u, const double* __restrict__ v, int vs, int vc,
                                double alpha, int n, double* __restrict__ out) {

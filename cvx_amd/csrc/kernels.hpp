@@ -139,6 +139,19 @@ int lib_gemm(hipStream_t s, bool ta, bool tb, int m, int n, int k, const double*
 int lib_gemv(hipStream_t s, bool ta, int rows, int cols, double alpha, const double* A, int lda, const double* x,
              double beta, double* y);
 int lib_dot(hipStream_t s, int n, const double* u, const double* v, double* out);
+// kkt_wide.cpp: persistent-handle library calls of the wide KKT path (p + 1 > MAX_RHS)
+int lib_handle_create(hipStream_t s, void** out);
+void lib_handle_destroy(void* h);
+int lib_llt_solve(void* h, int n, int k, const double* L, int ldl, double* Y, int ldy);
+int lib_gemm_h(void* h, bool ta, bool tb, int m, int n, int k, double alpha, const double* A, int lda, const double* B,
+               int ldb, double beta, double* C, int ldc);
+int lib_gemv_h(void* h, int rows, int cols, double alpha, const double* A, int lda, const double* x, double beta,
+               double* y);
+int lib_potrf(void* h, int p, double* S, int lds, int* dinfo);
+int lib_potrs(void* h, int p, const double* K, int ldk, double* z);
+void launch_kkt_prep_cm(hipStream_t s, const double* Aeq, int ld, int p, int n, int np, const double* d,
+                        const double* q, double* B, double* Y);
+void launch_kkt_sym(hipStream_t s, const double* R, int p, const double* b, double* S, double* z);
 void launch_eig_coeffs(hipStream_t s, const double* dots, const double* d, int n2, int npad, double* a, double* z);
 void launch_sum_chunks(hipStream_t s, const double* part, int nchunks, int cols, double* out);
 void launch_kkt_matrix(hipStream_t s, const double* H, int ldh, const double* Aeq, int lda, int n, int p, int ld,

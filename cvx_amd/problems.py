@@ -35,7 +35,7 @@ def random_qp(n: int, m: int, instance: int = 0, dtype=np.float64) -> Dict[str, 
 def random_qp_eq(n: int, m: int, p: int, instance: int = 0) -> Dict[str, np.ndarray]:
     """random_qp plus p dense equality rows Aeq x = beq (entries U[-1,1]) with beq = Aeq x0 at a small x0 that is
     strictly inside the inequalities: the workload of the affine reduction x = z0 + F u
-    (BarrierSolver.reduced over SolutionSpace(Aeq, beq)), including p > CVXG_MAX_EQ."""
+    (BarrierSolver.reduced over SolutionSpace(Aeq, beq)) and of the wide KKT path (p + 1 > MAX_RHS)."""
     spec = random_qp(n, m, instance)
     rng = np.random.Generator(np.random.PCG64(SEED_BASE + 104729 + instance))
     x0 = 0.01 * rng.uniform(-1.0, 1.0, size=n)

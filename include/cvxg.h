@@ -29,9 +29,12 @@ extern "C" {
 #define CVXG_E_DIM 6             /* assert dimension mismatch */
 #define CVXG_E_HIP 7             /* HIP runtime / device error */
 #define CVXG_E_ARG 8             /* invalid argument or call order */
-#define CVXG_E_UNSUPPORTED 9     /* configuration outside this build (e.g. p > CVXG_MAX_EQ) */
+#define CVXG_E_UNSUPPORTED 9     /* configuration outside this build (e.g. n > 65472) */
 
-#define CVXG_MAX_EQ 8            /* equality rows handled by the on-device KKT Schur path */
+/* Equality rows whose KKT right-hand sides ride the factorization's fused forward solve.  Wider equality blocks
+ * (any p < n) take the same KKTSystem.solveWithCholFactor sequence with the right-hand sides solved by two triangular
+ * solves on the factor and the p x p Schur complement factored by dpotrf (rocBLAS / rocSOLVER). */
+#define CVXG_MAX_EQ 8
 
 typedef struct cvxg_ctx cvxg_ctx;
 
@@ -96,8 +99,8 @@ typedef struct cvxg_solution {
 
 /* ---- context ------------------------------------------------------------------------------------ */
 
-/* Allocate a context on HIP device `device` for n variables, m linear inequalities, p equalities.
- * n <= 65472 (1023 Cholesky blocks of 64; CVXG_E_UNSUPPORTED above). */
+/* Allocate a context on HIP device `device` for n variables, m linear inequalities, p < n equalities (CVXG_E_DIM
+ * otherwise, as EqualityConstraint asserts).  n <= 65472 (1023 Cholesky blocks of 64; CVXG_E_UNSUPPORTED above). */
 int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out);
 void cvxg_destroy(cvxg_ctx* ctx);
 const char* cvxg_last_error(const cvxg_ctx* ctx);  /* NULL: the last error of a context-free call (this thread) */

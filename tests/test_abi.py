@@ -63,7 +63,8 @@ def test_bad_arguments_rejected(lib):
     from cvx_amd import _lib
     h = C.c_void_p()
     assert lib.cvxg_create(0, 0, 4, 0, C.byref(h)) == _lib.CVXG_E_DIM
-    assert lib.cvxg_create(0, 4, 4, _lib.CVXG_MAX_EQ + 1, C.byref(h)) == _lib.CVXG_E_UNSUPPORTED
+    assert lib.cvxg_create(0, 4, 4, 4, C.byref(h)) == _lib.CVXG_E_DIM  # p < n (EqualityConstraint.scala:18-20)
+    assert lib.cvxg_create(0, 1023 * 64 + 1, 4, 0, C.byref(h)) == _lib.CVXG_E_UNSUPPORTED
     assert lib.cvxg_newton_step(None, None, None) == _lib.CVXG_E_ARG
 
 

@@ -463,6 +463,45 @@ def test_equality_kkt_direction_vs_oracle(mods):
     eng.close()
 
 
+@pytest.mark.parametrize("p", [8, 9, 12, 64])
+def test_equality_kkt_direction_any_p(mods, p):
+    """KKTSystem.solve (KKTSystem.scala:43-167) for any number of equality rows: p + 1 <= 9 right-hand sides ride the
+    fused forward solve (p = 8), wider blocks take the rocBLAS / rocSOLVER sequence of solveWithCholFactor (p = 9,
+    12, 64).  dx within 1e-8 and w within 1e-7 of the oracle's KKTSystem at t = 1 and 100."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp_eq(200, 360, p, instance=3)
+    pb = _opb(O, spec)
+    eng = _engine(Engine, spec)
+    pars = SP.standardParams()
+    x = spec["x0"]
+    for t in (1.0, 100.0):
+        dx, w, info = eng.newton_direction(pars, t, x)
+        assert info.fallback == 0
+        y = O.barrier_gradient(pb, t, x)
+        H = O.barrier_hessian(pb, t, x, literal=False)
+        dref, wref = O.kkt_solve(H, pb.Aeq, y, pb.beq - pb.Aeq @ x, pars.tolEqSolve)
+        assert np.linalg.norm(dx - dref) / np.linalg.norm(dref) < 1e-8, (p, t)
+        assert np.linalg.norm(w - wref) / np.linalg.norm(wref) < 1e-7, (p, t)
+    eng.close()
+
+
+def test_equality_barrier_solve_wide_p_vs_oracle(mods):
+    """A whole equality-constrained barrier solve (EqualityConstrainedSolver, BarrierSolver.solveWithEQs) with p = 12
+    on the KKT path: final x within 1e-6 of the oracle's, equality gap and duality gap below tol."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp_eq(40, 96, 12, instance=8)
+    pars = SP.standardParams()
+    eng = _engine(Engine, spec)
+    eng.set_x(spec["x0"])
+    sol = eng.barrier_solve(pars, termination=0)
+    x = eng.get_x()
+    eng.close()
+    ref = O.barrier_solve(_opb(O, spec), spec["x0"], pars)
+    assert np.linalg.norm(x - ref.x) <= 1e-6 * max(1.0, np.linalg.norm(ref.x))
+    assert sol.duality_gap < pars.tolSolver and sol.equality_gap < pars.tolSolver
+    assert abs(sol.newton_steps - ref.newton_steps) <= max(2, int(0.05 * ref.newton_steps))
+
+
 # ---- full-size properties (oracle too slow): C2 and C3 shapes ------------------------------------------
 
 @pytest.mark.parametrize("n,m", [(1024, 2048), (4096, 8192)])
