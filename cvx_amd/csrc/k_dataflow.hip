@@ -16,7 +16,7 @@
 // handed-off bytes is an sc1 access (relaxed agent-scope atomics), each storing wave drains with
 // s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane stores the state word; the consumer polls the
 // word with sc1 loads, then a workgroup barrier, then sc1 loads of the data.  One workgroup per CU.
-#include "potrf64.hpp"
+#include "potrf64w.hpp"
 
 namespace cvxg {
 
@@ -26,7 +26,7 @@ constexpr int DF_SMEM = 4 * NB * (NB + 2) + 2 * 16 * (NB + 2) + 512;  // doubles
 
 // LDS of the critical-chain workgroup: POTRF's workspace (tile, L^-1, rhs) + the TRSM tile L_k+1,k + L' w_k
 struct ChainSmem {
-  Potrf64Smem p;
+  Potrf64wSmem p;
   double Sa[NB * (NB + 2)];       // A_b,b-1 during the TRSM slices, then L_b,b-1 (for the last rhs correction)
   double E2[2][16 * (NB + 2)];    // double-buffered row-blocks of L_b-1,b-1^-1
   double V[NB * MAX_RHS];
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     // (chain flags), so the next factorization starts ~one slice after the previous one ends.  The updated
     // diagonal tile goes straight from the MFMA accumulators into this workgroup's POTRF workspace.
     ChainSmem& cs = *reinterpret_cast<ChainSmem*>(smem);
-    Potrf64Smem& ps = cs.p;
+    Potrf64wSmem& ps = cs.p;
     const int lane = tid & 63, wv = tid >> 6;
     int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published
     auto mark = [&](int k, int step, int field) {
@@ -284,8 +284,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     const int blk_jb[4][NBLK16] = {{0, 0, 3}, {0, 1, 2}, {1, 2, -1}, {0, 1, -1}};
     for (int b = blockIdx.x; b < nblk; b += 2) {
       if (b == 0) {
-        potrf64_stage_tile<Sc1Mem>(L, ld, 0, ps);
-        potrf64_stage_rhs<Sc1Mem>(rhs, 0, nrhs, ps);
+        potrf64w_stage<Sc1Mem>(L, ld, 0, rhs, 0, nrhs, ps);
       } else {
         const int k = b - 1;
         mark(k, 1, 0);
@@ -419,14 +418,15 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         mark(k, 2, 2);
         return true;
       };
-      if (!potrf64_factor<Sc1Mem>(L, ld, b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix,
-                                  trace ? trace + 4 * (size_t)(ntasks + 3 * b) + 3 : nullptr)) {
+      potrf64w_reset(ps);
+      __syncthreads();
+      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
       publish(df_tri(b, b), b + 1);  // w_b and L_bb^-1 stored
       mark(b, 0, 2);
-      potrf64_store_L<Sc1Mem>(L, ld, b, ps);  // only the final backward solve reads L_bb
+      potrf64w_store_L<Sc1Mem>(L, ld, b, ps);  // only the final backward solve reads L_bb
       __syncthreads();  // the potrf workspace is reused by the next TRSM slices
     }
     return;
