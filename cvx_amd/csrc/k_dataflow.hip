@@ -200,9 +200,12 @@ __device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0,
   }
 }
 
-// TRSM(i,k): X = A_ik Linv_kk^T into tile (i,k); rhs_i -= X w_k (w_k = rhs block k after POTRF(k)).
-__device__ void df_trsm(double* __restrict__ L, int ld, int i, int k, double* __restrict__ rhs, int nrhs,
-                        double* __restrict__ Linv, double* smem) {
+// TRSM(i,k): X = A_ik Linv_kk^T into tile (i,k); rhs_i -= X w_k (w_k = rhs block k after POTRF(k)).  The task
+// starts once all of Linv_kk is published (chain flag) and waits for w_k (state(k,k) == k + 1, the end of POTRF(k))
+// only before the rhs update, so the L tile is not held back by POTRF's forward solve.  False: the launch aborted.
+__device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __restrict__ rhs, int nrhs,
+                        double* __restrict__ Linv, double* smem, const int* state, int* abortw, DevCtrl* ctrl,
+                        int* s_ok) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   double* Pi = smem;
@@ -230,6 +233,10 @@ __device__ void df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
         mA.st(row * ld + col, acc[mi][nj][r]);
         Pi[row * DF_SP + col] = acc[mi][nj][r];
       }
+  if (tid == 0) *s_ok = df_wait(state, df_tri(k, k), k + 1, abortw, ctrl);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the w_k loads behind the poll
+  __syncthreads();
+  if (!*s_ok) return false;
   double* wk = Pj;  // [64][nrhs]
   for (int t = tid; t < NB * nrhs; t += 256) wk[t] = mW.ld(t);
   __syncthreads();
@@ -240,6 +247,52 @@ __device__ void df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
     for (int c = 0; c < NB; ++c) s = fma(Pi[row * DF_SP + c], wk[c * nrhs + rho], s);
     mR.st(t, mR.ld(t) - s);
   }
+  return true;
+}
+
+// ---- chain slices (ping-pong consumer below): operands read from LDS in one batch, then the MFMAs back to back.
+// One wave per SIMD cannot hide an LDS round trip behind another wave, so interleaving reads and MFMAs costs a round
+// trip per MFMA pair (microbench/slices.hip: 4650 -> 2840 cycles per slice).
+// TRSM slice CB: L'[16 w.., 16 CB..] = A[16 w.., :] L^-1[16 CB.., :]^T (K = 16 (CB + 1): L^-1 is lower); af = the
+// wave's row-block of A as MFMA A-fragments (loaded once per block), E = row-block CB of L^-1 (row stride DF_SP).
+template <int CB>
+__device__ __forceinline__ d4f ch_trsm(const double (&af)[16], const double* E, int lane) {
+  double xf[4 * (CB + 1)];
+#pragma unroll
+  for (int s = 0; s < 4 * (CB + 1); ++s) xf[s] = E[(lane & 15) * DF_SP + 4 * s + (lane >> 4)];
+  d4f acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4 * (CB + 1); s += 2) {
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s], xf[s], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s + 1], xf[s + 1], acc1, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
+// the 10 lower 16 x 16 blocks of a 64 x 64 tile, 3 / 3 / 2 / 2 per wave (-1: none)
+constexpr int kChIB[4][3] = {{0, 3, 3}, {1, 3, 2}, {1, 3, -1}, {2, 2, -1}};
+constexpr int kChJB[4][3] = {{0, 0, 3}, {0, 1, 2}, {1, 2, -1}, {0, 1, -1}};
+// UPDATE slice: D -= L'[:, 16 cb..] L'[:, 16 cb..]^T on wave W's blocks (compile-time, so fragments are picked
+// statically); Lp = L' with row stride DF_SP
+template <int W>
+__device__ __forceinline__ void ch_update(d4f (&dacc)[3], const double* Lp, int cb, int lane) {
+  constexpr auto uses = [](int r) {
+    for (int q = 0; q < 3; ++q)
+      if (kChIB[W][q] == r || kChJB[W][q] == r) return true;
+    return false;
+  };
+  double lf[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (uses(r))
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lf[r][q] = Lp[(16 * r + (lane & 15)) * DF_SP + 16 * cb + 4 * q + (lane >> 4)];
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (kChIB[W][q] >= 0)
+        dacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-lf[kChIB[W][q] < 0 ? 0 : kChIB[W][q]][st],
+                                                       lf[kChJB[W][q] < 0 ? 0 : kChJB[W][q]][st], dacc[q], 0, 0, 0);
 }
 
 __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L, int ld, double* __restrict__ rhs,
@@ -253,6 +306,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   int* counter = work;
   int* abortw = work + 1;
   int* state = work + 64;  // own cache lines
+  int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published (0..4)
   const int tid = threadIdx.x;
   if (blockIdx.x < 2) {
     // ---- workgroups 0 and 1: the critical chain, ping-pong.  Workgroup c factors the diagonal blocks b = c,
@@ -263,7 +317,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     ChainSmem& cs = *reinterpret_cast<ChainSmem*>(smem);
     Potrf64wSmem& ps = cs.p;
     const int lane = tid & 63, wv = tid >> 6;
-    int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published
     auto mark = [&](int k, int step, int field) {
       if (trace && tid == 0) trace[4 * (size_t)(ntasks + 3 * k + step) + field] = __builtin_amdgcn_s_memrealtime();
     };
@@ -278,10 +331,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       __syncthreads();
       return s_ok;
     };
-    // the 10 lower 16 x 16 blocks of a 64 x 64 tile, 3 / 3 / 2 / 2 per wave
-    constexpr int NBLK16 = 3;
-    const int blk_ib[4][NBLK16] = {{0, 3, 3}, {1, 3, 2}, {1, 3, -1}, {2, 2, -1}};
-    const int blk_jb[4][NBLK16] = {{0, 0, 3}, {0, 1, 2}, {1, 2, -1}, {0, 1, -1}};
+    constexpr int NBLK16 = 3;  // (kChIB / kChJB: this wave's lower 16 x 16 blocks)
     for (int b = blockIdx.x; b < nblk; b += 2) {
       if (b == 0) {
         potrf64w_stage<Sc1Mem>(L, ld, 0, rhs, 0, nrhs, ps);
@@ -303,7 +353,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           const Sc1Mem mD(L + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
 #pragma unroll
           for (int q = 0; q < NBLK16; ++q) {
-            const int ib = blk_ib[wv][q], jb = blk_jb[wv][q];
+            const int ib = kChIB[wv][q], jb = kChJB[wv][q];
             if (ib >= 0) {
 #pragma unroll
               for (int r = 0; r < 4; ++r)
@@ -326,6 +376,9 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         };
         if (!wait(cflag, k, 1)) return;
         eload(0);
+        double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments (Sa staged behind the barriers above)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) af[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
         bool have_next = false;
 #pragma unroll 1
         for (int cb = 0; cb < 4; ++cb) {
@@ -347,16 +400,13 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           }
           __syncthreads();
           {  // L'[16 wv.., 16 cb..] = A[16 wv.., :] L^-1[16 cb.., :]^T, K = 16 (cb + 1), two MFMA chains
-            d4f acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-            const double* Ar = cs.Sa + 16 * wv * DF_SP;
-            for (int s2 = 0; s2 < 4 * (cb + 1); s2 += 2) {
-              const int kk = 4 * s2 + (lane >> 4);
-              acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Ar[(lane & 15) * DF_SP + kk], E[(lane & 15) * DF_SP + kk], acc0,
-                                                          0, 0, 0);
-              acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Ar[(lane & 15) * DF_SP + kk + 4], E[(lane & 15) * DF_SP + kk + 4],
-                                                          acc1, 0, 0, 0);
+            d4f acc;
+            switch (cb) {
+              case 0: acc = ch_trsm<0>(af, E, lane); break;
+              case 1: acc = ch_trsm<1>(af, E, lane); break;
+              case 2: acc = ch_trsm<2>(af, E, lane); break;
+              default: acc = ch_trsm<3>(af, E, lane); break;
             }
-            const d4f acc = acc0 + acc1;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
@@ -368,17 +418,16 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           __syncthreads();
           have_next = s_next;
           if (have_next) eload(cb + 1);  // lands behind the diagonal update below
-#pragma unroll
-          for (int q = 0; q < NBLK16; ++q) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
-            const int ib = blk_ib[wv][q], jb = blk_jb[wv][q];
-            if (ib >= 0)
-              dacc[q] = mfma16_abt(dacc[q], Lp + 16 * ib * DF_SP + 16 * cb, DF_SP, Lp + 16 * jb * DF_SP + 16 * cb, DF_SP,
-                                   -1.0, lane);
+          switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
+            case 0: ch_update<0>(dacc, Lp, cb, lane); break;
+            case 1: ch_update<1>(dacc, Lp, cb, lane); break;
+            case 2: ch_update<2>(dacc, Lp, cb, lane); break;
+            default: ch_update<3>(dacc, Lp, cb, lane); break;
           }
         }
 #pragma unroll
         for (int q = 0; q < NBLK16; ++q) {
-          const int ib = blk_ib[wv][q], jb = blk_jb[wv][q];
+          const int ib = kChIB[wv][q], jb = kChJB[wv][q];
           if (ib >= 0) c16_store(ps.S + 16 * ib * P64_SP + 16 * jb, P64_SP, dacc[q], lane);
         }
         // keep L_b,k for the rhs correction at the end of POTRF(b) (X is POTRF's workspace)
@@ -450,8 +499,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     const int type = task >> 30, k = (task >> 20) & 1023, i = (task >> 10) & 1023, j = task & 1023;
     if (tid == 0) {
       bool ok;
-      if (type == 1) {
-        ok = df_wait(state, df_tri(k, k), k + 1, abortw, ctrl) && df_wait(state, df_tri(i, k), k, abortw, ctrl);
+      if (type == 1) {  // all of Linv_kk published (w_k is awaited inside the task)
+        ok = df_wait(cflag, k, 4, abortw, ctrl) && df_wait(state, df_tri(i, k), k, abortw, ctrl);
       } else if (type == 3) {  // panels k..k+3: TRSM(., k+3) done implies the earlier ones (tile order)
         ok = df_wait(state, df_tri(i, k + 3), k + 4, abortw, ctrl) &&
              df_wait(state, df_tri(j, k + 3), k + 4, abortw, ctrl) && df_wait(state, df_tri(i, j), k, abortw, ctrl);
@@ -467,7 +516,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     if (!s_ok) break;
     int done_idx, done_val = k + 1;
     if (type == 1) {
-      df_trsm(L, ld, i, k, rhs, nrhs, Linv, smem);
+      if (!df_trsm(L, ld, i, k, rhs, nrhs, Linv, smem, state, abortw, ctrl, &s_ok)) break;
       done_idx = df_tri(i, k);
     } else if (type == 3) {
       df_update4(L, ld, i, j, k, smem);
