@@ -163,13 +163,13 @@ def cpu_baseline_blas(spec, steps: int = 3):
                        f"steps ({ts:.3f} s/step)")}
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
 
 
 def pmc_traffic(kernel_prefixes):
-    """HBM bytes of one SYRK assembly phase from the committed rocprofv3 PMC passes (scripts/pmc_traffic.py:
-    FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections), summed over the launches the phase consists of (the main
-    wave, the split-K tail and the ordered reduce: the same region the HIP events time); None if absent."""
+    """HBM bytes of one phase from the committed rocprofv3 PMC passes (scripts/pmc_traffic.py: FETCH_SIZE x2 +
+    WRITE_SIZE, gfx950 corrections), summed over the launches the phase consists of (for the assembly: the main
+    wave, the split-K tail and the ordered reduce, the same region the HIP events time); None if absent."""
     try:
         doc = json.load(open(PMC_TRAFFIC))
     except (OSError, ValueError):
@@ -314,9 +314,12 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     kkt_ms = float(np.mean(ruiz_ms)) + chol + float(np.mean(solve_ms))
     flops_chol = n ** 3 / 3.0 + n * n / 2.0 + n / 6.0  # dpotrf flops; all but O(n^2) are trailing SYRK/GEMM
     frac = (lambda a: a / FP64_MFMA_PEAK_TFLOPS if a is not None else None)  # noqa: E731
+    chol_traffic, chol_src = pmc_traffic(("cvxg::k_chol_dataflow",)) if wl == "C3" else (None, None)
     trailing = {"kernel": "k_chol_dataflow (trailing SYRK/GEMM updates + 64x64 POTRF/TRSM tasks)",
                 "flops_per_launch": flops_chol, "avg_launch_ms": chol, "achieved": tf(flops_chol, chol),
-                "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(tf(flops_chol, chol))}
+                "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(tf(flops_chol, chol)),
+                "traffic": chol_traffic, "traffic_unit": "bytes/factorization (algorithmic: 8 n^2 = 134 MB, the "
+                "lower triangle read and written once)", "traffic_source": chol_src}
     comb_ach = tf(flops_syrk + flops_chol, syrk + chol)
     combined = {"what": "SURVEY.md §8d: (assembly SYRK + POTRF trailing flops) / (SYRK + Cholesky kernel time)",
                 "achieved": comb_ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(comb_ach)}
