@@ -207,7 +207,6 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
                         double* __restrict__ Linv, double* smem, const int* state, int* abortw, DevCtrl* ctrl,
                         int* s_ok) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
   double* Pi = smem;
   double* Pj = smem + NB * DF_SP;
   const Sc1Mem mA(L + (size_t)i * NB * ld + (size_t)k * NB, tile_bytes(ld));
@@ -216,22 +215,44 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
   df_stage(Pi, mA, ld);
   df_stage(Pj, Sc1Mem(Linv + (size_t)k * NB * NB, tile_bytes(NB)), NB);
   __syncthreads();
+  // Linv_kk is lower triangular: output column block c needs K < 16 (c + 1) only.  Wave (rh, cp) takes rows
+  // 32 rh.. and the column blocks {0, 3} (cp = 0) or {1, 2} (cp = 1): 40 MFMAs per wave instead of 64, balanced.
+  // (The skipped products are exact zeros: the sums are the full-K ones bit for bit.)
+  const int rh = wid >> 1, cp = wid & 1;
+  const int cb0 = cp ? 1 : 0, cb1 = cp ? 2 : 3;
+  const int lim0 = 4 * (cb0 + 1), lim1 = 4 * (cb1 + 1);
   d4f acc[2][2];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = d4f{0.0, 0.0, 0.0, 0.0};
-  df_mfma(acc, Pi, Pj, 1.0, wr, wc, lane);
+    for (int t = 0; t < 2; ++t) acc[mi][t] = d4f{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int st = 0; st < NB / 4; ++st) {
+    const int kk = 4 * st + (lane >> 4);
+    double fa[2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) fa[mi] = Pi[(rh * 32 + mi * 16 + (lane & 15)) * DF_SP + kk];
+    if (st < lim0) {
+      const double fb = Pj[(cb0 * 16 + (lane & 15)) * DF_SP + kk];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) acc[mi][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi], fb, acc[mi][0], 0, 0, 0);
+    }
+    if (st < lim1) {
+      const double fb = Pj[(cb1 * 16 + (lane & 15)) * DF_SP + kk];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) acc[mi][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi], fb, acc[mi][1], 0, 0, 0);
+    }
+  }
   __syncthreads();  // every wave is done reading Pi / Pj: reuse them for X and w_k
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < 2; ++nj)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
-        mA.st(row * ld + col, acc[mi][nj][r]);
-        Pi[row * DF_SP + col] = acc[mi][nj][r];
+        const int row = rh * 32 + mi * 16 + (lane >> 4) + 4 * r, col = (t ? cb1 : cb0) * 16 + (lane & 15);
+        mA.st(row * ld + col, acc[mi][t][r]);
+        Pi[row * DF_SP + col] = acc[mi][t][r];
       }
   if (tid == 0) *s_ok = df_wait(state, df_tri(k, k), k + 1, abortw, ctrl);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the w_k loads behind the poll
