@@ -274,7 +274,7 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
 // not emitted (workgroup 0 runs them in sequence); every transitive dependency of a chain task still precedes
 // that task's dependents in the emitted order, which keeps the launch deadlock-free.
 static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles, int near = 0,
-                                                 double boost = 0.0, int band = 0) {
+                                                 double boost = 0.0, int band = 0, bool eager = true) {
   struct Task {
     int type, i, j, k, cnt;
     double dur, bl, avail;
@@ -355,6 +355,20 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   pending.push({0.0, potrf_id[0]});
   std::vector<unsigned> order;
   order.reserve(T.size());
+  auto code = [](const Task& x) {
+    return ((unsigned)x.type << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j;
+  };
+  auto is_chain = [](const Task& x) {
+    return x.type == 0 || (x.type == 1 && x.i == x.k + 1) || (x.type == 2 && x.i == x.j && x.j == x.k + 1);
+  };
+  // the worker tasks the chain's staging of block k+2 waits on -- TRSM(k+2,k), UPDATE(k+2,k+1,k), UPDATE(k+2,k+2,k)
+  // -- are emitted as soon as their last dependency is (not at their simulated start), so a worker claims them early
+  // and starts the moment their inputs land, instead of when the queue reaches them behind trailing updates.  The
+  // order stays topological: every dependency is emitted (or a chain task) before them.
+  auto is_eager = [](const Task& x) {
+    return (x.type == 1 && x.i == x.k + 2) || (x.type == 2 && x.i == x.k + 2 && (x.j == x.i || x.j == x.i - 1));
+  };
+  std::vector<char> emitted(T.size(), 0);
   size_t nsched = 0;
   while (nsched < T.size()) {
     DI wk = wfree.top();
@@ -375,16 +389,20 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
     ready.pop();
     const Task& x = T[t];
     now = std::max(now, x.avail);  // a task moved to `ready` by a later worker is not available earlier
-    const bool chain = x.type == 0 || (x.type == 1 && x.i == x.k + 1) || (x.type == 2 && x.i == x.j && x.j == x.k + 1);
-    if (!chain)
-      order.push_back(((unsigned)x.type << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j);
+    if (!is_chain(x) && !emitted[t]) order.push_back(code(x));
     ++nsched;
     const double fin = now + x.dur;
     wfree.push({fin, wk.second});
     succ(t, sv);
     for (int s : sv) {
       T[s].avail = std::max(T[s].avail, fin);
-      if (--T[s].npred == 0) pending.push({T[s].avail, s});
+      if (--T[s].npred == 0) {
+        pending.push({T[s].avail, s});
+        if (eager && is_eager(T[s]) && !is_chain(T[s])) {
+          order.push_back(code(T[s]));
+          emitted[s] = 1;
+        }
+      }
     }
   }
   return order;
