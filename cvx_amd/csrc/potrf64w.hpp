@@ -226,7 +226,7 @@ __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int
 // behind.  On return (uniformly true / false) sm.X = L^-1 (exact zeros above the diagonal), sm.W = w = L^-1 b (also
 // stored to rhs block k); Linv[k] = L^-1 is stored row-block by row-block as it becomes final (wave 3), and *lflag
 // (when given) counts the stored row-blocks (sc1 hand-off: the stores drained first).  fix() runs on all threads
-// between the factorization and the forward solve (barrier behind it).  L_kk is not stored (potrf64_store_L).
+// between the factorization and the forward solve (barrier behind it).  L_kk is not stored (potrf64w_store_L).
 template <class M, class Fix = NoFix>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,

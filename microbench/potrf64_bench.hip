@@ -8,7 +8,7 @@
 
 #include <vector>
 
-#include "../cvx_amd/csrc/potrf64.hpp"
+#include "potrf64_ref.hpp"
 namespace cvxg {
 __device__ double* g_src;  // pristine copy of the tile (warm-I$ repetition)
 __device__ int g_reps = 1;
