@@ -186,17 +186,6 @@ __global__ __launch_bounds__(1024) void k_sum(const double* __restrict__ u, int 
   if (threadIdx.x == 0) ctrl->sc[slot] = acc;
 }
 
-__global__ __launch_bounds__(1024) void k_dot_abs(const double* __restrict__ u, const double* __restrict__ v, int n,
-                                                  DevCtrl* ctrl, int slot) {
-  __shared__ double red[16];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) acc = fma(fabs(u[i]), v ? fabs(v[i]) : 1.0, acc);
-  acc = block_sum(acc, red);
-  if (threadIdx.x == 0) ctrl->sc[slot] = acc;
-}
-void launch_dot_abs(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot) {
-  k_dot_abs<<<1, 1024, 0, s>>>(u, v, n, ctrl, slot);
-}
 // up to 4 independent |u|.|v| sums in one launch (one block each)
 __global__ __launch_bounds__(1024) void k_dots_abs(AbsDots a, DevCtrl* ctrl) {
   __shared__ double red[16];

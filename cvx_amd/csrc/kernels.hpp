@@ -35,7 +35,6 @@ void launch_gradient_finalize(hipStream_t s, const double* a0, const double* Px,
 void launch_dot(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot);
 void launch_sum(hipStream_t s, const double* u, int n, DevCtrl* ctrl, int slot);
 // sum_i |u_i| |v_i| (v NULL: sum_i |u_i|) into ctrl->sc[slot]
-void launch_dot_abs(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot);
 struct AbsDots {
   const double* u[4];
   const double* v[4];
