@@ -108,6 +108,7 @@ SIGNATURES = {
     "cvxg_affine_map": (C.c_int, [_P, _D, _D]),
     "cvxg_set_timing": (C.c_int, [_P, C.c_int]),
     "cvxg_get_phase_times": (C.c_int, [_P, _D, C.c_int]),
+    "cvxg_chol_schedule": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_uint), C.c_int]),
 }
 
 

@@ -408,6 +408,20 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   return order;
 }
 
+// The production schedule: four-panel update groups (the last two panels of a tile single) and a priority boost
+// of 100 us for the near-diagonal updates and next-row TRSMs the chain waits on (band 3).  A/B at C3 (boost 0 /
+// band 2 -> 100 / 3): Cholesky 1.553, 1.552, 1.556 -> 1.498, 1.529, 1.502 ms.
+static std::vector<unsigned> chol_schedule(int nblk, int workers) {
+  return build_chol_schedule(nblk, workers, 1, 2, 0, 100.0, 3);
+}
+
+extern "C" int cvxg_chol_schedule(int nblk, int workers, unsigned* order, int cap) {
+  if (nblk < 1 || nblk > 1023 || workers < 1 || cap < 0 || (cap > 0 && !order)) return CVXG_E_ARG;
+  const std::vector<unsigned> o = chol_schedule(nblk, workers);
+  for (size_t t = 0; t < o.size() && (int)t < cap; ++t) order[t] = o[t];
+  return (int)o.size();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Device pipeline pieces
 // ------------------------------------------------------------------------------------------------
@@ -1220,10 +1234,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   {  // dataflow Cholesky: task order for this tile count, work words
     (void)hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device);
     ctx->ncu = std::max(ctx->ncu, 1);
-    // list schedule with four-panel update groups (the last two panels of a tile single) and a priority boost of
-    // 100 us for the near-diagonal updates and next-row TRSMs the chain waits on (band 3).  A/B at C3 (boost 0 /
-    // band 2 -> 100 / 3): Cholesky 1.553, 1.552, 1.556 -> 1.498, 1.529, 1.502 ms
-    std::vector<unsigned> order = build_chol_schedule(ctx->nblk, ctx->ncu, 1, 2, 0, 100.0, 3);
+    std::vector<unsigned> order = chol_schedule(ctx->nblk, ctx->ncu);
     ctx->df_ntasks = (int)order.size();
     CHK(dalloc(ctx, &ctx->df_tasks, order.size()));
     CHK(copy_sync(ctx, ctx->df_tasks, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));

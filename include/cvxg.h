@@ -278,6 +278,12 @@ int cvxg_affine_map(cvxg_ctx* dst, const double* u, double* x);
 int cvxg_set_timing(cvxg_ctx* ctx, int enabled);
 int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count);
 
+/* The worker task order of the dataflow Cholesky for nblk diagonal blocks and `workers` simulated workgroups,
+ * exactly as cvxg_create builds it (host-only, no device needed): each entry (type << 30) | (k << 20) | (i << 10)
+ * | j with type 1 TRSM(i,k), 2 UPDATE(i,j,k), 3 UPDATE4(i,j,k..k+3); the chain tasks are not listed.  Writes at
+ * most cap entries and returns the task count (or a negative status). */
+int cvxg_chol_schedule(int nblk, int workers, unsigned* order, int cap);
+
 #ifdef __cplusplus
 }
 #endif
