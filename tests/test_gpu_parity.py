@@ -568,6 +568,35 @@ def test_symsolve_fallback_vs_oracle(mods):
     eng.close()
 
 
+def test_symsolve_fallback_multiblock_abort(mods):
+    """The same fallback chain at n = 600 (10 diagonal blocks of the dataflow Cholesky): the first pivot failure
+    comes a few blocks in (about row 280 of the equilibrated H), so both factorization attempts abort the
+    persistent launch with the chain and the workers mid-flight and must drain it (no dependency timeout), and
+    the eigen fallback's direction matches the oracle's."""
+    Z, SP, Engine, O = mods
+    spec = _indefinite_qp(Z, 600, 800, instance=63)
+    pb = _opb(O, spec)
+    eng = _engine(Engine, spec)
+    pars = SP.standardParams()
+    x, t = spec["x0"], 1e4
+    y = O.barrier_gradient(pb, t, x)
+    rec = O.NewtonStepRecord(x=x, grad=y, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
+    dref = O.newton_direction(pb, t, x, y, pars.tolEqSolve, rec)
+    assert rec.fallback == 2
+    for _ in range(2):  # twice: the aborted launches leave nothing behind for the next factorization
+        dx, _, info = eng.newton_direction(pars, t, x, grad=y)
+        assert info.fallback == 2
+        assert np.linalg.norm(dx - dref) / np.linalg.norm(dref) < 1e-8
+    # and a healthy factorization right after the aborted ones
+    d_ok, _, info_ok = eng.newton_direction(pars, 1.0, x)
+    y1 = O.barrier_gradient(pb, 1.0, x)
+    rec1 = O.NewtonStepRecord(x=x, grad=y1, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
+    d1 = O.newton_direction(pb, 1.0, x, y1, pars.tolEqSolve, rec1)
+    assert info_ok.fallback == rec1.fallback
+    assert np.linalg.norm(d_ok - d1) / np.linalg.norm(d1) < 1e-8
+    eng.close()
+
+
 def test_kktsymsolve_fallback_vs_oracle(mods):
     """KKTSystem.scala:43-66: solvePD(H) -> solvePD(H + A'A) -> kktSymSolve([H A'; A 0], (-g, r))."""
     Z, SP, Engine, O = mods
