@@ -1,5 +1,6 @@
 // Microbenchmark of the 16 x 16 elimination sweep (one wave) of the 64 x 64 diagonal-block Cholesky:
 //   v0  lanes 0-15 D rows, lanes 16-31 identity-border rows, column broadcasts by v_readlane (potrf64w.hpp)
+//   v2  as v0, two columns per step (one dependency bubble per pair; the second column updated uniformly)
 //   v1  lanes 0-15 hold a D row and its border row in two register sets, column broadcasts by DPP row_newbcast
 //       (64-bit v_mov_b64_dpp, folded into the FMAs where the compiler can), the pivot chain in VGPRs
 // Checks both against a host Cholesky (L and L^-T) and reports cycles per sweep (s_memtime, 100 sweeps).
@@ -90,6 +91,52 @@ __global__ __launch_bounds__(64) void k_sweep(const double* __restrict__ D, doub
       a[1] += 0.0 * pmin;
 #pragma unroll
       for (int c = 0; c < 16; ++c) b[c] = a[c];
+    } else if (variant == 2) {
+      // two columns per step: both columns' broadcasts issued together behind one dependency bubble; the second
+      // column's values get the first column's update uniformly (mc' = mc - lc * f), each row then applies the
+      // rank-2 update
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        a[c] = (lane < 16) ? (c <= r ? D[r * 16 + c] : 0.0) : ((lane < 32 && c == r) ? 1.0 : 0.0);
+      int firstbad = -1;
+      double piv = readlane_d(a[0], 0);
+      double rinv = rcp_nr(piv);
+      double pmin = piv;
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) {
+        double lc[16], mc[16];
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) lc[c] = readlane_d(a[j], c);
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) mc[c] = readlane_d(a[j + 1], c);  // mc[j+1]: the diagonal D_j+1,j+1
+        if (!(piv > 0.0) && firstbad < 0) firstbad = j;
+        pmin = fmin(pmin, piv);
+        const double f = lc[j + 1] * rinv;
+        const double piv1 = fma(-lc[j + 1], f, mc[j + 1]);
+        const double rinv1 = rcp_nr(piv1);
+#pragma unroll
+        for (int c = j + 2; c < 16; ++c) mc[c] = fma(-lc[c], f, mc[c]);
+        double pivn = 1.0;
+        if (j + 2 < 16) {  // next pair's pivot, uniformly: D_j+2,j+2 - lc^2 / p_j - mc'^2 / p_j+1
+          const double dn = readlane_d(a[j + 2], j + 2);
+          pivn = fma(-(mc[j + 2] * rinv1), mc[j + 2], fma(-(lc[j + 2] * rinv), lc[j + 2], dn));
+        }
+        if (!(piv1 > 0.0) && firstbad < 0) firstbad = j + 1;
+        pmin = fmin(pmin, piv1);
+        const double t1 = a[j] * rinv;
+        a[j + 1] = fma(-t1, lc[j + 1], a[j + 1]);
+        const double t2 = a[j + 1] * rinv1;
+#pragma unroll
+        for (int c = j + 2; c < 16; ++c) a[c] = fma(-t2, mc[c], fma(-t1, lc[c], a[c]));
+        a[j] *= rsqrt_nr(piv);
+        a[j + 1] *= rsqrt_nr(piv1);
+        piv = pivn;
+        rinv = rcp_nr(pivn);
+      }
+      if (firstbad >= 0) a[0] = __builtin_nan("");
+      a[1] += 0.0 * pmin;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) b[c] = a[c];
     } else {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
@@ -107,7 +154,7 @@ __global__ __launch_bounds__(64) void k_sweep(const double* __restrict__ D, doub
     __builtin_amdgcn_sched_barrier(0);
   }
   t1 = __builtin_amdgcn_s_memtime();
-  if (variant == 0) {  // v0: lanes 0-15 L rows, 16-31 L^-T rows
+  if (variant != 1) {  // v0 / v2: lanes 0-15 L rows, 16-31 L^-T rows
     if (lane < 32)
       for (int c = 0; c < 16; ++c) out[(lane < 16 ? 0 : 256) + r * 16 + c] = (lane >= 16 || c <= r) ? a[c] : 0.0;
   } else {
@@ -148,7 +195,7 @@ int main() {
   hipMalloc(&dO, 512 * 8);
   hipMalloc(&dc, 8);
   hipMemcpy(dD, D.data(), 256 * 8, hipMemcpyHostToDevice);
-  for (int v = 0; v < 2; ++v) {
+  for (int v = 0; v < 3; ++v) {
     k_sweep<<<1, 64>>>(dD, dO, v, 100, dc);
     hipDeviceSynchronize();
     std::vector<double> O(512);
