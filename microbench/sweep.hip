@@ -1,5 +1,6 @@
 // Microbenchmark of the 16 x 16 elimination sweep (one wave) of the 64 x 64 diagonal-block Cholesky:
 //   v0  lanes 0-15 D rows, lanes 16-31 identity-border rows, column broadcasts by v_readlane (potrf64w.hpp)
+//   v3  as v0, the column broadcasts through LDS (one store + broadcast loads per column)
 //   v2  as v0, two columns per step (one dependency bubble per pair; the second column updated uniformly)
 //   v1  lanes 0-15 hold a D row and its border row in two register sets, column broadcasts by DPP row_newbcast
 //       (64-bit v_mov_b64_dpp, folded into the FMAs where the compiler can), the pivot chain in VGPRs
@@ -55,6 +56,7 @@ __device__ __forceinline__ void sweep_step(double (&a)[16], double (&b)[16], dou
 
 __global__ __launch_bounds__(64) void k_sweep(const double* __restrict__ D, double* __restrict__ out, int variant,
                                               int reps, unsigned long long* cyc) {
+  __shared__ double colbuf[2][16];  // v3: the finished column, broadcast through LDS
   const int lane = threadIdx.x, r = lane & 15;
   unsigned long long t0 = 0, t1 = 0;
   double a[16], b[16];
@@ -86,6 +88,38 @@ __global__ __launch_bounds__(64) void k_sweep(const double* __restrict__ D, doub
 #pragma unroll
         for (int c = j + 1; c < 16; ++c) a[c] = fma(-t, lc[c], a[c]);
         a[j] *= sj;
+      }
+      if (firstbad >= 0) a[0] = __builtin_nan("");
+      a[1] += 0.0 * pmin;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) b[c] = a[c];
+    } else if (variant == 3) {
+      // column broadcasts through LDS: lanes 0-15 store column j after its last update, every lane reads the
+      // entries it needs back as uniform-address (broadcast) LDS loads -- one store + one read round trip per
+      // column instead of 2 (15 - j) v_readlane
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        a[c] = (lane < 16) ? (c <= r ? D[r * 16 + c] : 0.0) : ((lane < 32 && c == r) ? 1.0 : 0.0);
+      int firstbad = -1;
+      double pmin = 1e300;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        double* cb = colbuf[j & 1];
+        if (lane < 16) cb[lane] = a[j];  // column j (rows >= j are final; rows < j unused)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double lc[16];
+#pragma unroll
+        for (int c = j; c < 16; ++c) lc[c] = cb[c];
+        const double piv = lc[j];
+        if (!(piv > 0.0) && firstbad < 0) firstbad = j;
+        pmin = fmin(pmin, piv);
+        const double rj = rcp_nr(piv);
+        const double t = a[j] * rj;
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) a[c] = fma(-t, lc[c], a[c]);
+        a[j] *= rsqrt_nr(piv);
       }
       if (firstbad >= 0) a[0] = __builtin_nan("");
       a[1] += 0.0 * pmin;
@@ -195,7 +229,7 @@ int main() {
   hipMalloc(&dO, 512 * 8);
   hipMalloc(&dc, 8);
   hipMemcpy(dD, D.data(), 256 * 8, hipMemcpyHostToDevice);
-  for (int v = 0; v < 3; ++v) {
+  for (int v = 0; v < 4; ++v) {
     k_sweep<<<1, 64>>>(dD, dO, v, 100, dc);
     hipDeviceSynchronize();
     std::vector<double> O(512);
