@@ -315,11 +315,21 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     flops_chol = n ** 3 / 3.0 + n * n / 2.0 + n / 6.0  # dpotrf flops; all but O(n^2) are trailing SYRK/GEMM
     frac = (lambda a: a / FP64_MFMA_PEAK_TFLOPS if a is not None else None)  # noqa: E731
     chol_traffic, chol_src = pmc_traffic(("cvxg::k_chol_dataflow",)) if wl == "C3" else (None, None)
+    chol_sq = None
+    if wl == "C3":  # MFMA utilisation of the Cholesky from the committed SQ counter passes (scripts/pmc_sq.sh)
+        try:
+            d = json.load(open(os.path.join(ROOT, "profiles", "r02", "pmc_chol_dataflow_sq.json")))["derived"]
+            chol_sq = {"source": "profiles/r02/pmc_chol_dataflow_sq.json",
+                       "mfma_work_over_algorithmic": d["mfma_work_over_algorithmic"],
+                       "mfma_busy_vs_clock_limited_peak": d[
+                           "mfma_busy_vs_clock_limited_peak (x 0.93, the SYRK main wave's measured fraction)"]}
+        except (OSError, ValueError, KeyError):
+            chol_sq = None
     trailing = {"kernel": "k_chol_dataflow (trailing SYRK/GEMM updates + 64x64 POTRF/TRSM tasks)",
                 "flops_per_launch": flops_chol, "avg_launch_ms": chol, "achieved": tf(flops_chol, chol),
                 "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(tf(flops_chol, chol)),
                 "traffic": chol_traffic, "traffic_unit": "bytes/factorization (algorithmic: 8 n^2 = 134 MB, the "
-                "lower triangle read and written once)", "traffic_source": chol_src}
+                "lower triangle read and written once)", "traffic_source": chol_src, "pmc_sq": chol_sq}
     comb_ach = tf(flops_syrk + flops_chol, syrk + chol)
     combined = {"what": "SURVEY.md §8d: (assembly SYRK + POTRF trailing flops) / (SYRK + Cholesky kernel time)",
                 "achieved": comb_ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(comb_ach)}
