@@ -1244,7 +1244,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
       CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk)));
     }
   }
-  CHK(dalloc(ctx, &ctx->bwd_flags, ctx->nblk));
+  CHK(dalloc(ctx, &ctx->bwd_flags, bwd_work_ints(ctx->nblk)));
   CHK(dalloc(ctx, &ctx->rhs, np * MAX_RHS));
   CHK(dalloc(ctx, &ctx->sol, np * MAX_RHS));
   // SYRK tile list and wave plan (syrk_tile_plan): full-K tiles in whole waves of workgroup slots, the

@@ -3,16 +3,19 @@
 // factorization (k_dataflow.hip) stores, so every block step is a product instead of a sequential substitution.
 #include <math.h>
 
-#include "kernels.hpp"
+#include "potrf64.hpp"  // Sc1Mem
 
 namespace cvxg {
 // ------------------------------------------------------------------------------------------------
 // The whole backward substitution L' u = w in ONE launch (MatrixUtils.scala:419-430 backSolve, blocked):
 // workgroup g owns block b = nblk-1-g and accumulates  s_b = sum_{i>b} L_ib' u_i  as the u_i are published
-// (flag[i] == gen; L_ib is prefetched into registers before the wait), then  u_b = Linv_bb' (w_b - s_b)  and
-// publishes u_b.  Workgroups only wait on lower blockIdx (dispatched earlier), so the launch is deadlock-free
-// at any residency.  Thread (c, g) keeps the partial sums of column c over rows 16g..16g+15 of every tile;
-// the four row groups are added once, in a fixed order.
+// (L_ib is prefetched into registers before the wait), then  u_b = Linv_bb' (w_b - s_b)  and publishes u_b.
+// Hand-off: every entry of u_b goes out as a data-tagged 16-B granule {value, gen} (one sc1 store, observed untorn
+// on gfx950; MI355X_MICROARCH.md hand-off table: ~1.0 us for a small 1:1 hand-off against 1.7-1.9x that with a
+// separate drained flag), and the consumers poll the granules themselves -- no flag round trip.  Workgroups only
+// wait on lower blockIdx (dispatched earlier), so the launch is deadlock-free at any residency.  Thread (c, g)
+// keeps the partial sums of column c over rows 16g..16g+15 of every tile; the four row groups are added once, in
+// a fixed order.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__ L, int ld,
                                                       const double* __restrict__ Linv, const double* __restrict__ rhs,
@@ -21,8 +24,12 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
   if (ctrl->chol_info != 0) return;
   __shared__ double u[MAX_RHS][NB];
   __shared__ double part[4][MAX_RHS][NB];
-  __shared__ int s_ok;
+  __shared__ int s_bad;
   const int b = nblk - 1 - (int)blockIdx.x;
+  // the granules {u entry, gen} behind the nblk flag words (256-B aligned): entry (row, rho) at (row nrhs + rho)
+  const Sc1Mem gr(reinterpret_cast<double*>(flags + ((nblk + 63) & ~63)), (unsigned)(nblk * NB * nrhs) * 16u);
+  const double tag = __longlong_as_double((long long)gen);
+  if (threadIdx.x == 0) s_bad = 0;
   const int g = threadIdx.x >> 6, c = threadIdx.x & 63;
   double acc[MAX_RHS];
 #pragma unroll
@@ -48,18 +55,22 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
   if (b + 1 < nblk) load_tile(cur, nblk - 1);
   for (int i = nblk - 1; i > b; --i) {
     if (i - 1 > b) load_tile(nxt, i - 1);
-    if (threadIdx.x == 0) {
-      unsigned spins = 0;
-      while (__hip_atomic_load(flags + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen && ++spins < (1u << 24))
+    for (int t = threadIdx.x; t < nrhs * NB; t += 256) {  // each thread polls its own granules of u_i
+      const int rho = t / NB, cc = t % NB;
+      const int off = 2 * ((i * NB + cc) * nrhs + rho);
+      f64x2 v = gr.ld2(off);
+      for (unsigned spins = 0; __double_as_longlong(v[1]) != (long long)gen; ++spins) {
+        if (spins > (1u << 22)) {  // bounded wait: never hang the GPU on a scheduling bug
+          s_bad = 1;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
-      s_ok = spins < (1u << 24);
+        v = gr.ld2(off);
+      }
+      u[rho][cc] = v[0];
     }
     __syncthreads();
-    if (!s_ok) return;  // bounded wait: never hang the GPU on a scheduling bug
-    for (int t = threadIdx.x; t < nrhs * NB; t += 256)
-      u[t / NB][t % NB] = __hip_atomic_load(out + (size_t)(i * NB + t % NB) * nrhs + t / NB, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
+    if (s_bad) return;
     for (int rho = 0; rho < nrhs; ++rho) {
       double s = acc[rho];
 #pragma unroll
@@ -93,16 +104,17 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
   if (g == 0) {
     for (int rho = 0; rho < nrhs; ++rho) {
       const double s = ((part[0][rho][c] + part[1][rho][c]) + part[2][rho][c]) + part[3][rho][c];
-      __hip_atomic_store(out + (size_t)(b * NB + c) * nrhs + rho, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gr.st2(2 * ((b * NB + c) * nrhs + rho), f64x2{s, tag});  // the hand-off granule first
+      out[(size_t)(b * NB + c) * nrhs + rho] = s;              // the solution (read after the launch)
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __syncthreads();  // every storing wave (wave 0) has drained
-  if (threadIdx.x == 0) __hip_atomic_store(flags + b, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+size_t bwd_work_ints(int nblk) { return (size_t)((nblk + 63) & ~63) + (size_t)nblk * NB * MAX_RHS * 4; }
 
 void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,
                          int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl) {
+  // (flags: nblk words + the granules, bwd_work_ints)
   k_bwd_dataflow<<<nblk, 256, 0, s>>>(L, ld, Linv, rhs, out, nrhs, nblk, flags, gen, ctrl);
 }
 

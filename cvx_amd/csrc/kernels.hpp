@@ -106,6 +106,7 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */);
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
+size_t bwd_work_ints(int nblk);  // flag words + the data-tagged u granules of k_bwd_dataflow
 void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,
                          int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl);
 
