@@ -359,18 +359,19 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       } else {
         const int k = b - 1;
         mark(k, 1, 0);
-        if (!wait(state, df_tri(b, k), k)) return;
+        // A_b,k and D_b with every panel < k applied (state >= k), and the rhs block b with all earlier TRSM
+        // updates: one wait for both states, then every load in flight together (minus L_b,k w_k inside POTRF(b);
+        // POTRF(b-2) of this workgroup is done with ps.B)
+        if (tid == 0)
+          s_ok = df_wait(state, df_tri(b, k), k, abortw, ctrl) && df_wait(state, df_tri(b, b), k, abortw, ctrl);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        if (!s_ok) return;
         const Sc1Mem mA(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
-        df_stage(cs.Sa, mA, ld);
-        if (!wait(state, df_tri(b, b), k)) return;
-        mark(k, 1, 1);
-        {  // rhs block b with all earlier TRSM updates (state(b,b) >= k), loaded now so its latency hides behind the
-           // slices; minus L_b,k w_k inside POTRF(b).  (POTRF(b-2) of this workgroup is done with ps.B.)
-          const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-          for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
-        }
         d4f dacc[NBLK16];
         {
+          f64x2 va[NB * NB / 512];
+          df_load(va, mA, ld);
           const Sc1Mem mD(L + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
 #pragma unroll
           for (int q = 0; q < NBLK16; ++q) {
@@ -381,7 +382,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
                 dacc[q][r] = mD.ld((16 * ib + (lane >> 4) + 4 * r) * ld + 16 * jb + (lane & 15));
             }
           }
+          const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+          for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
+          df_put(cs.Sa, va);
         }
+        mark(k, 1, 1);
         const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
         double* Lp = ps.X;      // L_b,k, row stride DF_SP
         // row-block cb of L_kk^-1 (published by the other workgroup's POTRF(k) as cflag[k] reaches cb + 1) is
