@@ -130,8 +130,13 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
       }
   double* Pi = smem;
   double* Pj = (i == j) ? smem : smem + NB * DF_SP;
-  df_stage(Pi, Sc1Mem(L + (size_t)i * NB * ld + (size_t)k * NB, tile_bytes(ld)), ld);
-  if (i != j) df_stage(Pj, Sc1Mem(L + (size_t)j * NB * ld + (size_t)k * NB, tile_bytes(ld)), ld);
+  {  // both panel tiles' loads in flight together (one round trip, behind the C loads), then the LDS stores
+    f64x2 vi[NB * NB / 512], vj[NB * NB / 512];
+    df_load(vi, Sc1Mem(L + (size_t)i * NB * ld + (size_t)k * NB, tile_bytes(ld)), ld);
+    if (i != j) df_load(vj, Sc1Mem(L + (size_t)j * NB * ld + (size_t)k * NB, tile_bytes(ld)), ld);
+    df_put(Pi, vi);
+    if (i != j) df_put(Pj, vj);
+  }
   __syncthreads();
   if (active) {
     df_mfma(acc, Pi, Pj, -1.0, wr, wc, lane);
@@ -212,8 +217,13 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
   const Sc1Mem mA(L + (size_t)i * NB * ld + (size_t)k * NB, tile_bytes(ld));
   const Sc1Mem mW(rhs + (size_t)k * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
   const Sc1Mem mR(rhs + (size_t)i * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-  df_stage(Pi, mA, ld);
-  df_stage(Pj, Sc1Mem(Linv + (size_t)k * NB * NB, tile_bytes(NB)), NB);
+  {  // both operand tiles' loads in flight together, then the LDS stores
+    f64x2 va[NB * NB / 512], vl[NB * NB / 512];
+    df_load(va, mA, ld);
+    df_load(vl, Sc1Mem(Linv + (size_t)k * NB * NB, tile_bytes(NB)), NB);
+    df_put(Pi, va);
+    df_put(Pj, vl);
+  }
   __syncthreads();
   // Linv_kk is lower triangular: output column block c needs K < 16 (c + 1) only.  Wave (rh, cp) takes rows
   // 32 rh.. and the column blocks {0, 3} (cp = 0) or {1, 2} (cp = 1): 40 MFMAs per wave instead of 64, balanced.
