@@ -280,6 +280,7 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
         for _ in range(args.warmup):
             one_step()
         eng.set_timing(True)
+    reruns0 = eng.ruiz_lookahead()
     D.barrier(device)
     sync()
     t0 = time.perf_counter()
@@ -296,6 +297,8 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     elapsed = time.perf_counter() - t0
     elapsed = D.max_over_ranks(elapsed, device)
     eng.set_timing(False)
+    # timed steps whose Ruiz lookahead fell short (their Cholesky phase holds the re-run sweeps + factorization)
+    ruiz_reruns = eng.ruiz_lookahead() - reruns0
 
     x_final = eng.get_x()
     stats = np.array([rank, steps, elapsed, state["t"]], dtype=np.float64)
@@ -362,6 +365,7 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
                       "bwd_solve_residual": float(np.mean(solve_ms)), "line_search": float(np.mean(ls_ms))},
         "kkt_factor_solve_per_s": 1e3 / kkt_ms if kkt_ms > 0 else None,
         "cholesky_tflops": tf(n ** 3 / 3, chol),
+        "ruiz_lookahead_reruns": ruiz_reruns,
         "gathered_ranks": len(gathered),
     }
     return out, gathered

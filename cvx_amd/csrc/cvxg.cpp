@@ -109,6 +109,9 @@ struct cvxg_ctx {
   int* eig_info = nullptr;
   int* bwd_flags = nullptr;
   int bwd_gen = 0;
+  // Ruiz lookahead (cholesky_solve): the sweeps the next step launches first, and how often more had to follow
+  int ruiz_launch = RUIZ_MAX;
+  long long ruiz_relaunches = 0;
   int ncu = 256;
   unsigned* df_tasks = nullptr;
   int df_ntasks = 0;
@@ -415,6 +418,13 @@ static std::vector<unsigned> chol_schedule(int nblk, int workers) {
   return build_chol_schedule(nblk, workers, 1, 2, 0, 100.0, 3);
 }
 
+extern "C" int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* relaunches) {
+  if (!ctx) return CVXG_E_ARG;
+  if (relaunches) *relaunches = ctx->ruiz_relaunches;
+  if (sweeps > 0) ctx->ruiz_launch = std::min(RUIZ_MAX, sweeps);
+  return CVXG_OK;
+}
+
 extern "C" int cvxg_chol_schedule(int nblk, int workers, unsigned* order, int cap) {
   if (nblk < 1 || nblk > 1023 || workers < 1 || cap < 0 || (cap > 0 && !order)) return CVXG_E_ARG;
   const std::vector<unsigned> o = chol_schedule(nblk, workers);
@@ -475,21 +485,18 @@ static int eval_at_x(cvxg_ctx* ctx) {
   launch_gradient_finalize(s, ctx->a0, quad ? ctx->Px : (ctx->kl ? ctx->kl_negBy : nullptr), ctx->part,
                            coldot_chunks(mp), np, ctx->ctrl, ctx->y);
   if (ctx->nq > 0) launch_quad_grad(s, ctx->qPx, ctx->invd, ctx->qrows, ctx->nq, np, ctx->y);  // + (P_k x)/d_k
-  launch_dot(s, ctx->a0, ctx->x, np, ctx->ctrl, SC_A0X);
-  if (quad) launch_dot(s, ctx->x, ctx->Px, np, ctx->ctrl, SC_XPX);
-  launch_sum(s, ctx->logd, mp, ctx->ctrl, SC_SUMLOG);
-  launch_dot(s, ctx->y, nullptr, np, ctx->ctrl, SC_GG);
+  DotBatch db{};
+  db.add(DOT_FMA, ctx->a0, ctx->x, np, SC_A0X);
+  if (quad) db.add(DOT_FMA, ctx->x, ctx->Px, np, SC_XPX);
+  db.add(DOT_SUM, ctx->logd, nullptr, mp, SC_SUMLOG);
+  db.add(DOT_FMA, ctx->y, nullptr, np, SC_GG);
   if (cert) {  // error scales of f(x): |a0|.|x|, |x|.|P||x|, sum cabs/d, sum |log d|
-    AbsDots ad{};
-    auto add = [&](const double* u, const double* v, int len, int slot) {
-      ad.u[ad.count] = u, ad.v[ad.count] = v, ad.n[ad.count] = len, ad.slot[ad.count] = slot, ++ad.count;
-    };
-    add(ctx->a0, ctx->x, np, SC_A0XA);
-    if (quad) add(ctx->x, ctx->Pxa, np, SC_XPXA);
-    add(ctx->cabs, ctx->invd, mp, SC_CAINV);
-    add(ctx->logd, nullptr, mp, SC_LOGABS);
-    launch_dots_abs(s, ad, ctx->ctrl);
+    db.add(DOT_ABS, ctx->a0, ctx->x, np, SC_A0XA);
+    if (quad) db.add(DOT_ABS, ctx->x, ctx->Pxa, np, SC_XPXA);
+    db.add(DOT_ABS, ctx->cabs, ctx->invd, mp, SC_CAINV);
+    db.add(DOT_ABS, ctx->logd, nullptr, mp, SC_LOGABS);
   }
+  launch_dots(s, db, ctx->ctrl);
   if (ctx->p > 0) {
     launch_rowdot(s, ctx->Aeq, np, ctx->p, np, ctx->x, ctx->eqtmp);
     launch_axpy(s, ctx->beq, ctx->eqtmp, -1.0, ctx->p, ctx->eqd);  // b - A*x
@@ -555,16 +562,42 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr) {
   return CVXG_OK;
 }
 
-// Ruiz equilibration of H into dfin (MatrixUtils.scala:240-268).
-static void ruiz(cvxg_ctx* ctx) {
+// Ruiz equilibration of H into dfin (MatrixUtils.scala:240-268): sweeps k0 .. k1-1 (k0 = 0 starts from d = 1).
+// A sweep whose rho[k] <= 1e-6 exits at once, so launching all RUIZ_MAX sweeps is the reference's loop; the
+// final pass records the sweep count, or -1 when sweeps were left unlaunched and rho[k1] still exceeds 1e-6.
+static void ruiz_sweeps(cvxg_ctx* ctx, int k0, int k1) {
   hipStream_t s = ctx->s;
-  launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl);
-  for (int k = 0; k < RUIZ_MAX; ++k) {
+  if (k0 == 0) launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl);
+  for (int k = k0; k < k1; ++k) {
     const double* dc = (k & 1) ? ctx->ruiz1 : ctx->ruiz0;
     double* dn = (k & 1) ? ctx->ruiz0 : ctx->ruiz1;
     launch_ruiz_sweep_tri(s, ctx->H, ctx->np, ctx->n, ctx->np, dc, dn, ctx->part, ctx->ctrl, k);
   }
-  launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl);
+  launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl, k1);
+}
+static void ruiz(cvxg_ctx* ctx) { ruiz_sweeps(ctx, 0, RUIZ_MAX); }
+// The Newton step's Ruiz launches only the sweeps the previous step needed plus RUIZ_MARGIN (a sweep that exits on
+// rho <= 1e-6 still costs a launch pair, ~9 us), reads the control block, and launches RUIZ_CHUNK more at a time
+// while the loop is not done.  The sweeps that run, dfin and the sweep count are those of the full loop; a short
+// lookahead costs one more host round trip.
+constexpr int RUIZ_MARGIN = 1, RUIZ_CHUNK = 2;
+static int ruiz_lookahead(cvxg_ctx* ctx) {
+  int k1 = ctx->ruiz_launch;
+  ruiz_sweeps(ctx, 0, k1);
+  HIPC(ctx, hipGetLastError());
+  CHK(sync_ctrl(ctx));
+  while (ctx->hctrl->ruiz_sweeps < 0) {
+    ++ctx->ruiz_relaunches;
+    const int k2 = std::min(RUIZ_MAX, k1 + RUIZ_CHUNK);
+    ruiz_sweeps(ctx, k1, k2);
+    k1 = k2;
+    HIPC(ctx, hipGetLastError());
+    CHK(sync_ctrl(ctx));
+  }
+  return CVXG_OK;
+}
+static void ruiz_learn(cvxg_ctx* ctx, int sweeps) {
+  ctx->ruiz_launch = std::max(1, std::min(RUIZ_MAX, sweeps + RUIZ_MARGIN));
 }
 
 // One factorisation attempt of Q = DHD (+reg I) with the fused forward solve of nrhs right-hand sides,
@@ -632,7 +665,7 @@ static void backward_solve(cvxg_ctx* ctx, int nrhs) {
 static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
   hipStream_t s = ctx->s;
   tstart(ctx, 1);
-  ruiz(ctx);
+  CHK(ruiz_lookahead(ctx));
   tstop(ctx, 1);
   tstart(ctx, 2);
   int reg = 0;
@@ -641,6 +674,7 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
       ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, ctx->y, -1.0, ctx->n, ctx->np, 1, 0, ctx->rhs); }, &reg, &mind);
   tstop(ctx, 2);
   info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
+  if (info->ruiz_sweeps >= 0) ruiz_learn(ctx, info->ruiz_sweeps);
   info->regularized = reg;
   info->min_diag = mind;
   if (rc != CVXG_OK) return rc;
@@ -648,10 +682,11 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
   backward_solve(ctx, 1);
   launch_scale_vec(s, ctx->sol, ctx->dfin, ctx->np, ctx->dx);  // x = d :* u
   // relativeSize(H*x - b, b, tol), b = -grad  (MatrixUtils.scala:437-442, 496)
-  launch_rowdot(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->dx, ctx->vtmp);
-  launch_axpy(s, ctx->vtmp, ctx->y, 1.0, ctx->n, ctx->vtmp);
-  launch_dot(s, ctx->vtmp, nullptr, ctx->n, ctx->ctrl, SC_RES2);
-  launch_dot(s, ctx->dx, ctx->y, ctx->np, ctx->ctrl, SC_Q);
+  launch_rowdot_add(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->dx, ctx->y, ctx->vtmp);  // H x + grad = H x - b
+  DotBatch db{};
+  db.add(DOT_FMA, ctx->vtmp, nullptr, ctx->n, SC_RES2);
+  db.add(DOT_FMA, ctx->dx, ctx->y, ctx->np, SC_Q);
+  launch_dots(s, db, ctx->ctrl);
   tstop(ctx, 3);
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
@@ -1044,26 +1079,25 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
     launch_rowdot(s, ctx->Pq, ctx->np, ctx->nq * ctx->np, ctx->np, ctx->sdir, ctx->qPs);
     launch_quad_ls(s, ctx->qPx, ctx->qPs, ctx->sdir, ctx->qrows, ctx->nq, ctx->np, ctx->e, ctx->qf);
   }
-  launch_dot(s, ctx->a0, ctx->sdir, ctx->np, ctx->ctrl, SC_A0S);
   if (ctx->kl) launch_rowdot(s, ctx->KB, ctx->np, ctx->noutp, ctx->np, ctx->sdir, ctx->kl_u);  // u = B's
   if (quad) {
     if (cert) launch_rowdot_abs(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps, ctx->Psa);
     else launch_rowdot(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps);
-    launch_dot(s, ctx->sdir, ctx->Px, ctx->np, ctx->ctrl, SC_SPX);
-    launch_dot(s, ctx->sdir, ctx->Ps, ctx->np, ctx->ctrl, SC_SPS);
+  }
+  DotBatch db{};
+  db.add(DOT_FMA, ctx->a0, ctx->sdir, ctx->np, SC_A0S);
+  if (quad) {
+    db.add(DOT_FMA, ctx->sdir, ctx->Px, ctx->np, SC_SPX);
+    db.add(DOT_FMA, ctx->sdir, ctx->Ps, ctx->np, SC_SPS);
   }
   if (cert) {
-    AbsDots ad{};
-    auto add = [&](const double* u, const double* v, int slot) {
-      ad.u[ad.count] = u, ad.v[ad.count] = v, ad.n[ad.count] = ctx->np, ad.slot[ad.count] = slot, ++ad.count;
-    };
-    add(ctx->a0, ctx->sdir, SC_A0SA);
+    db.add(DOT_ABS, ctx->a0, ctx->sdir, ctx->np, SC_A0SA);
     if (quad) {
-      add(ctx->sdir, ctx->Pxa, SC_SPXA);
-      add(ctx->sdir, ctx->Psa, SC_SPSA);
+      db.add(DOT_ABS, ctx->sdir, ctx->Pxa, ctx->np, SC_SPXA);
+      db.add(DOT_ABS, ctx->sdir, ctx->Psa, ctx->np, SC_SPSA);
     }
-    launch_dots_abs(s, ad, ctx->ctrl);
   }
+  launch_dots(s, db, ctx->ctrl);
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
   const DevCtrl h = *ctx->hctrl;

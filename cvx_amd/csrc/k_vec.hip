@@ -86,16 +86,21 @@ void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int 
 }
 
 __global__ __launch_bounds__(256) void k_rowdot(const double* __restrict__ M, int ld, int rows, int cols,
-                                                const double* __restrict__ v, double* __restrict__ y) {
+                                                const double* __restrict__ v, const double* __restrict__ add,
+                                                double* __restrict__ y) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const double dot = row_dot_wave(M + (size_t)row * ld, v, cols, lane);
-  if (lane == 0) y[row] = dot;
+  if (lane == 0) y[row] = add ? dot + add[row] : dot;
 }
 
 void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y) {
-  k_rowdot<<<(rows + 3) / 4, 256, 0, s>>>(M, ld, rows, cols, v, y);
+  k_rowdot<<<(rows + 3) / 4, 256, 0, s>>>(M, ld, rows, cols, v, nullptr, y);
+}
+void launch_rowdot_add(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
+                       const double* add, double* y) {
+  k_rowdot<<<(rows + 3) / 4, 256, 0, s>>>(M, ld, rows, cols, v, add, y);
 }
 
 __global__ __launch_bounds__(256) void k_rowdot_abs(const double* __restrict__ M, int ld, int rows, int cols,
@@ -186,19 +191,31 @@ __global__ __launch_bounds__(1024) void k_sum(const double* __restrict__ u, int 
   if (threadIdx.x == 0) ctrl->sc[slot] = acc;
 }
 
-// up to 4 independent |u|.|v| sums in one launch (one block each)
-__global__ __launch_bounds__(1024) void k_dots_abs(AbsDots a, DevCtrl* ctrl) {
+// A batch of the reductions above, one block each: the per-thread loop and block_sum of each kind are those of
+// k_dot / k_sum, so a batched sum is bitwise the single-launch one (one launch instead of up to 8).
+__global__ __launch_bounds__(1024) void k_dots(DotBatch a, DevCtrl* ctrl) {
   __shared__ double red[16];
   const int b = blockIdx.x;
   const double* u = a.u[b];
   const double* v = a.v[b];
+  const int n = a.n[b];
   double acc = 0.0;
-  for (int i = threadIdx.x; i < a.n[b]; i += blockDim.x) acc = fma(fabs(u[i]), v ? fabs(v[i]) : 1.0, acc);
+  switch (a.kind[b]) {
+    case DOT_FMA:
+      for (int i = threadIdx.x; i < n; i += blockDim.x) acc = fma(u[i], v ? v[i] : u[i], acc);
+      break;
+    case DOT_SUM:
+      for (int i = threadIdx.x; i < n; i += blockDim.x) acc += u[i];
+      break;
+    default:
+      for (int i = threadIdx.x; i < n; i += blockDim.x) acc = fma(fabs(u[i]), v ? fabs(v[i]) : 1.0, acc);
+      break;
+  }
   acc = block_sum(acc, red);
   if (threadIdx.x == 0) ctrl->sc[a.slot[b]] = acc;
 }
-void launch_dots_abs(hipStream_t s, const AbsDots& a, DevCtrl* ctrl) {
-  if (a.count > 0) k_dots_abs<<<a.count, 1024, 0, s>>>(a, ctrl);
+void launch_dots(hipStream_t s, const DotBatch& a, DevCtrl* ctrl) {
+  if (a.count > 0) k_dots<<<a.count, 1024, 0, s>>>(a, ctrl);
 }
 void launch_dot(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot) {
   k_dot<<<1, 1024, 0, s>>>(u, v, n, ctrl, slot);
@@ -383,22 +400,25 @@ void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np
   k_ruiz_rows<<<(np + 63) / 64, 256, 0, s>>>(S, nbn, n, np, dcur, dnext, ctrl, k);
 }
 
+// k1 = the sweeps launched so far.  K = the first k < k1 whose rho[k] <= 1e-6 (sweeps K.. exited), else k1;
+// K == k1 < RUIZ_MAX with rho[k1] > 1e-6 means the loop is not done: ruiz_sweeps = -1 (cvxg.cpp: ruiz_lookahead).
 __global__ void k_ruiz_final(const double* __restrict__ d0, const double* __restrict__ d1, int np,
-                             double* __restrict__ dfin, DevCtrl* ctrl) {
-  int K = RUIZ_MAX;
-  for (int k = 0; k < RUIZ_MAX; ++k) {
+                             double* __restrict__ dfin, DevCtrl* ctrl, int k1) {
+  int K = k1;
+  for (int k = 0; k < k1; ++k) {
     if (!(__longlong_as_double((long long)ctrl->ruiz_rho[k]) > 1e-6)) {
       K = k;
       break;
     }
   }
+  const bool open = K == k1 && k1 < RUIZ_MAX && __longlong_as_double((long long)ctrl->ruiz_rho[k1]) > 1e-6;
   const double* src = (K & 1) ? d1 : d0;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < np) dfin[i] = src[i];
-  if (i == 0) ctrl->ruiz_sweeps = K;
+  if (i == 0) ctrl->ruiz_sweeps = open ? -1 : K;
 }
-void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl) {
-  k_ruiz_final<<<(np + 255) / 256, 256, 0, s>>>(d0, d1, np, dfin, ctrl);
+void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl, int k1) {
+  k_ruiz_final<<<(np + 255) / 256, 256, 0, s>>>(d0, d1, np, dfin, ctrl, k1);
 }
 
 // Q = (dd') o H (+ reg I), lower triangle into L; padded part: identity.   MatrixUtils.scala:267, :454

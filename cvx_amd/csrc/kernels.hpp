@@ -21,6 +21,9 @@ void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int 
                             double* cabs = nullptr);
 // y = M v (row-major, one wave per row); rows, cols multiples of 128 / any.
 void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y);
+// y = M v + add, the add fused into the row sweep (bitwise the rowdot followed by launch_axpy(y, add, 1.0))
+void launch_rowdot_add(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
+                       const double* add, double* y);
 // y = M v and yabs = |M| |v| in the same sweep
 void launch_rowdot_abs(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y,
                        double* yabs);
@@ -34,15 +37,25 @@ void launch_gradient_finalize(hipStream_t s, const double* a0, const double* Px,
 // single-block deterministic sums into ctrl->sc[slot]
 void launch_dot(hipStream_t s, const double* u, const double* v, int n, DevCtrl* ctrl, int slot);
 void launch_sum(hipStream_t s, const double* u, int n, DevCtrl* ctrl, int slot);
-// sum_i |u_i| |v_i| (v NULL: sum_i |u_i|) into ctrl->sc[slot]
-struct AbsDots {
-  const double* u[4];
-  const double* v[4];
-  int n[4];
-  int slot[4];
+// Up to DOTS_MAX independent single-block reductions in one launch (one block each), every one in exactly
+// the order of its single-launch form (bit-identical results):
+//   DOT  sum_i u_i v_i   (v NULL: u_i u_i)       = launch_dot
+//   SUM  sum_i u_i                                = launch_sum
+//   ABS  sum_i |u_i| |v_i| (v NULL: sum_i |u_i|)  -- the error scales of the certified line search
+constexpr int DOTS_MAX = 8;
+enum DotKind : int { DOT_FMA = 0, DOT_SUM = 1, DOT_ABS = 2 };
+struct DotBatch {
+  const double* u[DOTS_MAX];
+  const double* v[DOTS_MAX];
+  int n[DOTS_MAX];
+  int slot[DOTS_MAX];
+  int kind[DOTS_MAX];
   int count;
+  void add(int k, const double* uu, const double* vv, int len, int sl) {
+    u[count] = uu, v[count] = vv, n[count] = len, slot[count] = sl, kind[count] = k, ++count;
+  }
 };
-void launch_dots_abs(hipStream_t s, const AbsDots& a, DevCtrl* ctrl);
+void launch_dots(hipStream_t s, const DotBatch& a, DevCtrl* ctrl);
 // out = u + v*alpha (alpha read from device scalar pointer or host value)
 void launch_axpy(hipStream_t s, const double* u, const double* v, double alpha, int n, double* out);
 void launch_scale_vec(hipStream_t s, const double* u, const double* d, int n, double* out);  // out = d*u
@@ -52,7 +65,7 @@ void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl);
 // The same sweep from the lower triangle only (64 x 64 tiles -> partials S[nbn][nbn*64] -> fixed-order row sums).
 void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np, const double* dcur, double* dnext,
                            double* S, DevCtrl* ctrl, int k);
-void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl);
+void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl, int k1);
 // L[i][j] = d_i d_j H_ij (+reg on the diagonal), lower triangle; padded diagonal = 1.
 void launch_form_q(hipStream_t s, const double* H, double* L, int ld, int n, int np, const double* d,
                    const DevCtrl* ctrl);

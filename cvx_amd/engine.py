@@ -246,6 +246,13 @@ class Engine:
     def set_timing(self, on: bool):
         self._check(self.lib.cvxg_set_timing(self.h, 1 if on else 0))
 
+    def ruiz_lookahead(self, sweeps: int = 0) -> int:
+        """cvxg_set_ruiz_lookahead: the Ruiz sweeps the next Newton step launches (0 keeps the setting); returns how
+        often a lookahead has fallen short on this context (the remaining sweeps and the factorization re-ran)."""
+        n = C.c_longlong()
+        self._check(self.lib.cvxg_set_ruiz_lookahead(self.h, int(sweeps), C.byref(n)))
+        return n.value
+
     def phase_times(self) -> np.ndarray:
         ms = np.zeros(8)
         self._check(self.lib.cvxg_get_phase_times(self.h, _dp(ms), 8))

@@ -278,6 +278,12 @@ int cvxg_affine_map(cvxg_ctx* dst, const double* u, double* x);
 int cvxg_set_timing(cvxg_ctx* ctx, int enabled);
 int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count);
 
+/* The Newton step's Ruiz lookahead (cholesky_solve, MatrixUtils.scala:240-268 as restated in k_vec.hip): the next
+ * step first launches `sweeps` Ruiz sweeps (the last step's count + 1 by default, RUIZ_MAX = 20 on a fresh
+ * context), reads whether the loop is done, and launches 2 more at a time until it is, so results equal the full
+ * loop's.  sweeps <= 0 leaves the setting; *relaunches (if given) receives how many extra batches were launched. */
+int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* relaunches);
+
 /* The worker task order of the dataflow Cholesky for nblk diagonal blocks and `workers` simulated workgroups,
  * exactly as cvxg_create builds it (host-only, no device needed): each entry (type << 30) | (k << 20) | (i << 10)
  * | j with type 1 TRSM(i,k), 2 UPDATE(i,j,k), 3 UPDATE4(i,j,k..k+3); the chain tasks are not listed.  Writes at

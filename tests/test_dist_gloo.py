@@ -67,6 +67,9 @@ class OracleEngine:
     def phase_times(self):
         return np.zeros(8)
 
+    def ruiz_lookahead(self, sweeps=0):
+        return 0
+
     def close(self):
         pass
 

@@ -1137,3 +1137,28 @@ def test_batch_barrier_solve_matches_single_contexts(mods):
     assert _lib.lib().cvxg_batch_newton_step(2, hs, C.byref(ps), None, None) == _lib.CVXG_E_ARG
     for e in engs:
         e.close()
+
+
+@pytest.mark.parametrize("n,m", [(384, 700), (1024, 2048)])
+def test_ruiz_lookahead_equals_full_loop(mods, n, m):
+    """The Newton step first launches only the Ruiz sweeps the previous step needed + 1 (cvxg.cpp: ruiz_lookahead)
+    and launches more while the loop is not done.  Every lookahead -- all 20 sweeps, one sweep, exactly the count,
+    one short -- gives bitwise the same dx and sweep count (MatrixUtils.scala:240-268), and only the short ones
+    launch more."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp(n, m, instance=23)
+    eng = _engine(Engine, spec)
+    pars = SP.standardParams()
+    x = spec["x0"]
+    for t in (1.0, 1e4):
+        eng.ruiz_lookahead(20)
+        dx_full, _, info = eng.newton_direction(pars, t, x)
+        k = info.ruiz_sweeps
+        assert 1 <= k <= 20
+        for look, reruns in ((1, k > 1), (k, False), (max(k - 1, 1), k > 1), (20, False)):
+            before = eng.ruiz_lookahead(look)
+            dx, _, inf2 = eng.newton_direction(pars, t, x)
+            assert np.array_equal(dx, dx_full), f"t={t} lookahead {look}"
+            assert inf2.ruiz_sweeps == k and inf2.regularized == info.regularized
+            assert (eng.ruiz_lookahead() - before > 0) == reruns
+    eng.close()
