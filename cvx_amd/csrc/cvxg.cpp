@@ -601,9 +601,11 @@ static void ruiz_learn(cvxg_ctx* ctx, int sweeps) {
 }
 
 // One factorisation attempt of Q = DHD (+reg I) with the fused forward solve of nrhs right-hand sides,
-// which `fill_rhs` writes into ctx->rhs first.  Returns chol_info / min_diag via hctrl.
-template <class F>
-static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs) {
+// which `fill_rhs` writes into ctx->rhs first.  `after` enqueues the work that consumes the factor (the back
+// substitution) before the one host read of the attempt, which returns chol_info / min_diag via hctrl; a caller
+// discards that work when the attempt fails.
+template <class F, class G>
+static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G after) {
   hipStream_t s = ctx->s;
   launch_ctrl_set(s, ctx->ctrl, 1, reg);
   launch_ctrl_reset_chol(s, ctx->ctrl);
@@ -612,6 +614,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs) {
   // the whole factorization as one persistent launch over the 64 x 64 tile DAG (k_dataflow.hip)
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
                        ctx->df_ntasks, ctx->ncu, ctx->df_trace);
+  after();
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
   if (ctx->hctrl->df_status != 0)
@@ -640,15 +643,15 @@ static double min_diag_of(const DevCtrl& h) {
 
 // regularizedCholesky (MatrixUtils.scala:452-461): chol(Q); on failure or min diag(L) <= 1e-7 use
 // chol(Q + 1e-10 I), whose failure propagates (CVXG_E_NOT_PD).
-template <class F>
-static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regularized, double* mind) {
-  CHK(factor_attempt(ctx, 0.0, nrhs, fill_rhs));
+template <class F, class G>
+static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regularized, double* mind, G after) {
+  CHK(factor_attempt(ctx, 0.0, nrhs, fill_rhs, after));
   *regularized = 0;
   if (ctx->hctrl->chol_info == 0 && min_diag_of(*ctx->hctrl) > 1e-7) {
     *mind = min_diag_of(*ctx->hctrl);
     return CVXG_OK;
   }
-  CHK(factor_attempt(ctx, 1e-10, nrhs, fill_rhs));
+  CHK(factor_attempt(ctx, 1e-10, nrhs, fill_rhs, after));
   *regularized = 1;
   *mind = min_diag_of(*ctx->hctrl);
   if (ctx->hctrl->chol_info != 0)
@@ -670,26 +673,29 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
   tstart(ctx, 2);
   int reg = 0;
   double mind = 0.0;
+  // the back substitution and residual go out behind each factorization attempt, before its host read (one
+  // round trip per step instead of two); a failed attempt's results are overwritten by the retry's
+  auto solve_and_residual = [&]() {
+    tstop(ctx, 2);
+    tstart(ctx, 3);
+    backward_solve(ctx, 1);
+    launch_scale_vec(s, ctx->sol, ctx->dfin, ctx->np, ctx->dx);  // x = d :* u
+    // relativeSize(H*x - b, b, tol), b = -grad  (MatrixUtils.scala:437-442, 496)
+    launch_rowdot_add(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->dx, ctx->y, ctx->vtmp);  // H x + grad = H x - b
+    DotBatch db{};
+    db.add(DOT_FMA, ctx->vtmp, nullptr, ctx->n, SC_RES2);
+    db.add(DOT_FMA, ctx->dx, ctx->y, ctx->np, SC_Q);
+    launch_dots(s, db, ctx->ctrl);
+    tstop(ctx, 3);
+  };
   int rc = regularized_cholesky(
-      ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, ctx->y, -1.0, ctx->n, ctx->np, 1, 0, ctx->rhs); }, &reg, &mind);
-  tstop(ctx, 2);
+      ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, ctx->y, -1.0, ctx->n, ctx->np, 1, 0, ctx->rhs); }, &reg, &mind,
+      solve_and_residual);
   info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
   if (info->ruiz_sweeps >= 0) ruiz_learn(ctx, info->ruiz_sweeps);
   info->regularized = reg;
   info->min_diag = mind;
   if (rc != CVXG_OK) return rc;
-  tstart(ctx, 3);
-  backward_solve(ctx, 1);
-  launch_scale_vec(s, ctx->sol, ctx->dfin, ctx->np, ctx->dx);  // x = d :* u
-  // relativeSize(H*x - b, b, tol), b = -grad  (MatrixUtils.scala:437-442, 496)
-  launch_rowdot_add(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->dx, ctx->y, ctx->vtmp);  // H x + grad = H x - b
-  DotBatch db{};
-  db.add(DOT_FMA, ctx->vtmp, nullptr, ctx->n, SC_RES2);
-  db.add(DOT_FMA, ctx->dx, ctx->y, ctx->np, SC_Q);
-  launch_dots(s, db, ctx->ctrl);
-  tstop(ctx, 3);
-  HIPC(ctx, hipGetLastError());
-  CHK(sync_ctrl(ctx));
   const double nb = ctx->normGrad;
   const double f = nb < tol ? tol : tol + nb;
   const double rel = sqrt(ctx->hctrl->sc[SC_RES2]) / f;
@@ -836,7 +842,7 @@ static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, doubl
         launch_kkt_prep(s, ctx->Aeq, np, p, n, np, ctx->dfin, ctx->kB, ctx->rhs, nr);  // B = A diag(d), B'
         launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, nr, p, ctx->rhs);            // D q
       },
-      &reg, &mind);
+      &reg, &mind, [] {});
   tstop(ctx, 2);
   info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
   info->regularized = reg;
@@ -871,7 +877,7 @@ static int kkt_solve_pd_wide(cvxg_ctx* ctx, const double* qv, const double* bv, 
   int reg = 0;
   double mind = 0.0;
   int rc = regularized_cholesky(
-      ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, 1, 0, ctx->rhs); }, &reg, &mind);
+      ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, 1, 0, ctx->rhs); }, &reg, &mind, [] {});
   tstop(ctx, 2);
   info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
   info->regularized = reg;
