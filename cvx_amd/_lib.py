@@ -79,6 +79,7 @@ SIGNATURES = {
     "cvxg_version": (C.c_char_p, []),
     "cvxg_set_objective": (C.c_int, [_P, _D, C.c_int, _D, C.c_double]),
     "cvxg_set_objective_kl": (C.c_int, [_P, _D, C.c_int, C.c_int, C.c_int, _D, C.c_double]),
+    "cvxg_set_objective_kl_primal": (C.c_int, [_P, C.c_int]),
     "cvxg_set_ineq": (C.c_int, [_P, _D, C.c_int, C.c_int, _D, _D]),
     "cvxg_set_eq": (C.c_int, [_P, _D, C.c_int, C.c_int, _D]),
     "cvxg_set_quad": (C.c_int, [_P, C.c_int, _I, _D, C.c_int]),

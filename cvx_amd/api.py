@@ -196,6 +196,27 @@ class DualKLObjectiveFunction(ObjectiveFunction):
         return (self.B * self._y(z)[None, :]) @ self.B.T
 
 
+class KLPrimalObjectiveFunction(ObjectiveFunction):
+    """Dist_KL.objectiveFunction(n) (Dist_KL.scala:223-239): the KL distance x . log(n x) from the uniform distribution
+    on n outcomes; gradient (1 + log x) + log n, Hessian diag(1/x).  On the engine through
+    cvxg_set_objective_kl_primal (barrier solver)."""
+
+    def __init__(self, n: int):
+        super().__init__(n)
+        self.n = n
+
+    def valueAt(self, x):
+        x = np.asarray(x, dtype=np.float64)
+        assert x.shape[0] == self.n, f"Dimension mismatch x.length = {x.shape[0]} dim(d_KL) = {self.n}"
+        return float(x @ np.log(x * float(self.n)))
+
+    def gradientAt(self, x):
+        return (1.0 + np.log(x)) + np.log(self.n)
+
+    def hessianAt(self, x):
+        return np.diag(1.0 / np.asarray(x, dtype=np.float64))
+
+
 class LinearConstraint:
     """Affine inequality r + a'x <= ub (LinearConstraint.scala:7-32)."""
 
@@ -428,8 +449,10 @@ class GpuBarrierSolver:
 
     def __init__(self, objF: ObjectiveFunction, cnts: ConstraintSet, eqs: Optional[EqualityConstraint],
                  pars: SolverParams, device: int = 0):
-        if not isinstance(objF, (QuadraticObjectiveFunction, LinearObjectiveFunction, DualKLObjectiveFunction)):
-            raise TypeError("GPU barrier engine: objective must be Quadratic-, Linear- or DualKLObjectiveFunction")
+        if not isinstance(objF, (QuadraticObjectiveFunction, LinearObjectiveFunction, DualKLObjectiveFunction,
+                                 KLPrimalObjectiveFunction)):
+            raise TypeError("GPU barrier engine: objective must be Quadratic-, Linear-, DualKL- or "
+                            "KLPrimalObjectiveFunction")
         if cnts.feasiblePoint is None:
             raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
         p = 0 if eqs is None else eqs.A.shape[0]
@@ -441,6 +464,8 @@ class GpuBarrierSolver:
         self.engine = Engine(cnts.dim, A.shape[0], p, device)
         if isinstance(objF, DualKLObjectiveFunction):
             self.engine.set_objective_kl(objF.B, objF.w, objF.R)
+        elif isinstance(objF, KLPrimalObjectiveFunction):
+            self.engine.set_objective_kl_primal(objF.n)
         else:
             self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
         self.engine.set_ineq(A, r, ub)
@@ -604,8 +629,8 @@ class OptimizationProblem:
 
 class Dist_KL(OptimizationProblem):
     """Dist_KL (Dist_KL.scala:68-177) with Duality (Duality.scala): argmin_Q dist_KL(Q, uniform) s.t. HQ <= u,
-    AQ = r, solved through the dual barrier problem on the MI355X engine.  The direct (primal) solve has a
-    non-quadratic objective and stays outside this engine."""
+    AQ = r.  Both solves run on the MI355X engine: the direct one (solve: the barrier solver over the KL primal
+    objective with the equalities, Dist_KL.scala:309-312) and the dual one (solveDual)."""
 
     E = 2.7182811828459045  # Dist_KL.scala:114 (reference constant, not exp(1))
 
@@ -628,18 +653,9 @@ class Dist_KL(OptimizationProblem):
         super().__init__(id, None, None)
 
     @staticmethod
-    def objectiveFunction(n: int) -> ObjectiveFunction:
-        """Dist_KL.objectiveFunction (Dist_KL.scala:223-239): x . log(n x); its primal solve is not on the engine."""
-        class _KL(ObjectiveFunction):
-            def valueAt(self, x):
-                return float(x @ np.log(x * float(n)))
-
-            def gradientAt(self, x):
-                return 1.0 + np.log(x) + np.log(n)
-
-            def hessianAt(self, x):
-                return np.diag(1.0 / x)
-        return _KL(n)
+    def objectiveFunction(n: int) -> "KLPrimalObjectiveFunction":
+        """Dist_KL.objectiveFunction (Dist_KL.scala:223-239): x . log(n x), on the engine's KL primal objective."""
+        return KLPrimalObjectiveFunction(n)
 
     @staticmethod
     def equalityConstraint(n: int, A=None, r=None) -> EqualityConstraint:
@@ -674,6 +690,8 @@ class Dist_KL(OptimizationProblem):
         prob = Dist_KL(id, n, H, u, A, r, device)
         prob.ineqsWithFeasiblePoint = ineqs.withFeasiblePoint(eqs, pars)  # phase I
         prob.solverType = solverType
+        prob.eqs, prob.pars = eqs, pars
+        prob.objectiveFunction = Dist_KL.objectiveFunction(n)
         return prob
 
     def primalOptimum(self, z):
@@ -705,7 +723,15 @@ class Dist_KL(OptimizationProblem):
         return solD
 
     def solve(self, debugLevel: int = 0) -> Solution:
-        raise TypeError("Dist_KL direct solve: the primal KL objective is not on the GPU engine; use solveDual")
+        """The direct solve (Dist_KL.scala:309-312): BarrierSolver(objF, ineqsWithFeasiblePoint, Some(eqs)) on the
+        engine's KL primal objective.  "PD" builds the reference's PrimalDualSolver with equalities (solve_withEQs),
+        which this engine does not run (include/cvxg.h)."""
+        if self.solverType == "PD":
+            raise TypeError("GPU primal-dual engine: equality constraints are not supported (solve_withEQs)")
+        if self.solver is None:
+            self.solver = BarrierSolver.apply(self.objectiveFunction, self.ineqsWithFeasiblePoint, self.eqs, self.pars,
+                                              self.device)
+        return self.solver.solve(debugLevel)
 
 
 def problem_from_spec(spec: dict):
@@ -728,7 +754,7 @@ def problem_from_spec(spec: dict):
 
 __all__ = ["SolverParams", "Solution", "OptimizationState", "CvxUtils", "FeasibilityReport",
            "InfeasibleProblemException", "barrier_t_loop", "ObjectiveFunction", "QuadraticObjectiveFunction", "LinearObjectiveFunction",
-           "DualKLObjectiveFunction", "Dist_KL",
+           "DualKLObjectiveFunction", "KLPrimalObjectiveFunction", "Dist_KL",
            "LinearConstraint", "QuadraticConstraint", "Constraints", "EqualityConstraint", "ConstraintSet", "GpuBarrierSolver", "BarrierSolver",
            "GpuPrimalDualSolver", "PrimalDualSolver",
            "OptimizationProblem", "problem_from_spec", "CvxgError", "NotStrictlyFeasible"]

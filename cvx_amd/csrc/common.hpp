@@ -27,7 +27,7 @@ struct DevCtrl {
   unsigned long long min_diag;    // bits of min diag(L) (positive doubles order like uint64)
   unsigned long long pd_s0;       // bits of the primal-dual step bound s0 (PrimalDualSolver.scala:331-338)
   unsigned long long ruiz_rho[RUIZ_MAX + 2];
-  double sc[32];                  // reduced scalars, see SC_* below
+  double sc[40];                  // reduced scalars, see SC_* below
 };
 
 enum {
@@ -56,8 +56,12 @@ enum {
   SC_TR_A0X,    // a0 . xt
   SC_TR_XPX,    // xt . P xt
   SC_TR_SUMLOG, // sum_i log d_i(xt)
+  SC_KLP,       // KL primal objective x . log(n x) at x (Dist_KL.scala:223-227)
+  SC_KLPA,      // its error scale sum_j |x_j log(n x_j)| + |x_j|
+  SC_TR_KLP,    // the KL primal objective at a fresh trial point xt
   SC_COUNT
 };
+static_assert(SC_COUNT <= 40, "DevCtrl::sc too small");
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

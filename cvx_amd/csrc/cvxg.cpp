@@ -48,6 +48,11 @@ struct cvxg_ctx {
   double kl_R = 0.0;
   double *KB = nullptr, *kl_v = nullptr, *kl_y = nullptr, *kl_u = nullptr, *kl_negBy = nullptr;
   double *kl_part = nullptr, *kl_ls = nullptr;
+  // KL primal objective (cvxg_set_objective_kl_primal): f0 = x . log(n x), its gradient and diag(1/x) Hessian
+  int klp = 0;
+  double klp_n = 0.0;
+  double *klp_lx = nullptr, *klp_g0 = nullptr, *klp_hd = nullptr, *klp_ab = nullptr, *klp_lxt = nullptr;
+  double *klp_part = nullptr, *klp_ls = nullptr;
   double* a0 = nullptr;
   double r0 = 0.0;
   double *A = nullptr, *r = nullptr, *ub = nullptr;
@@ -440,6 +445,7 @@ extern "C" int cvxg_chol_schedule(int nblk, int workers, unsigned* order, int ca
 // KL dual  w.z + R.exp(-B'z)  (Dist_KL.scala:146-147 negated by Duality.scala:76)
 static double objective_from_ctrl(const cvxg_ctx* ctx, const DevCtrl& h) {
   if (ctx->kl) return h.sc[SC_A0X] + h.sc[SC_KLSUM];
+  if (ctx->klp) return h.sc[SC_KLP];  // x dot log(x*n)  (Dist_KL.scala:226)
   return ctx->r0 + h.sc[SC_A0X] + (ctx->hasP ? h.sc[SC_XPX] / 2 : 0.0);
 }
 
@@ -481,18 +487,27 @@ static int eval_at_x(cvxg_ctx* ctx) {
     launch_axpy(s, ctx->kl_negBy, ctx->kl_negBy, -2.0, np, ctx->kl_negBy);  // -B y
     launch_sum(s, ctx->kl_y, ctx->noutp, ctx->ctrl, SC_KLSUM);
   }
+  if (ctx->klp)  // log(n x), the gradient (1 + log x) + log n, diag(1/x) and the value terms' error scale
+    launch_klp_eval(s, ctx->x, ctx->n, np, ctx->klp_n, ctx->klp_lx, ctx->klp_g0, ctx->klp_hd, ctx->klp_ab);
   launch_coldot_partials(s, ctx->A, np, mp, np, ctx->invd, ctx->part);
-  launch_gradient_finalize(s, ctx->a0, quad ? ctx->Px : (ctx->kl ? ctx->kl_negBy : nullptr), ctx->part,
-                           coldot_chunks(mp), np, ctx->ctrl, ctx->y);
+  // objF.gradientAt(x) * t: (a + P x) t, the KL dual's (w - B y) t, or the KL primal's (0 + g0) t = g0 t (a0 = 0)
+  launch_gradient_finalize(s, ctx->a0, quad ? ctx->Px : (ctx->kl ? ctx->kl_negBy : (ctx->klp ? ctx->klp_g0 : nullptr)),
+                           ctx->part, coldot_chunks(mp), np, ctx->ctrl, ctx->y);
   if (ctx->nq > 0) launch_quad_grad(s, ctx->qPx, ctx->invd, ctx->qrows, ctx->nq, np, ctx->y);  // + (P_k x)/d_k
   DotBatch db{};
   db.add(DOT_FMA, ctx->a0, ctx->x, np, SC_A0X);
   if (quad) db.add(DOT_FMA, ctx->x, ctx->Px, np, SC_XPX);
+  if (ctx->klp) db.add(DOT_FMA, ctx->x, ctx->klp_lx, np, SC_KLP);
   db.add(DOT_SUM, ctx->logd, nullptr, mp, SC_SUMLOG);
   db.add(DOT_FMA, ctx->y, nullptr, np, SC_GG);
-  if (cert) {  // error scales of f(x): |a0|.|x|, |x|.|P||x|, sum cabs/d, sum |log d|
+  if (cert) {  // error scales of f(x): |a0|.|x|, |x|.|P||x| (or the KL primal terms), sum cabs/d, sum |log d|
+    if (db.full()) {
+      launch_dots(s, db, ctx->ctrl);
+      db.count = 0;
+    }
     db.add(DOT_ABS, ctx->a0, ctx->x, np, SC_A0XA);
     if (quad) db.add(DOT_ABS, ctx->x, ctx->Pxa, np, SC_XPXA);
+    if (ctx->klp) db.add(DOT_SUM, ctx->klp_ab, nullptr, np, SC_KLPA);
     db.add(DOT_ABS, ctx->cabs, ctx->invd, mp, SC_CAINV);
     db.add(DOT_ABS, ctx->logd, nullptr, mp, SC_LOGABS);
   }
@@ -546,13 +561,14 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr) {
     w = ctx->wd;
     rows = ctx->mdp;
   }
+  const double* Pd = ctx->klp ? ctx->klp_hd : nullptr;  // the KL primal's diag(1/x) * t
   if (ctx->ntiles_main > 0)
     launch_syrk_assemble(ctx->s, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
-                         TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->part);
+                         TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->part, Pd);
   if (ctx->ntiles > ctx->ntiles_main)
     launch_syrk_assemble(ctx->s, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
                          TileList{ctx->tiles + ctx->ntiles_main, ctx->ntiles - ctx->ntiles_main}, ctx->nsplit,
-                         ctx->part);
+                         ctx->part, Pd);
   if (ctx->have_sparse)
     launch_sparse_hess(ctx->s, ctx->sp_ptr, ctx->sp_pq, ctx->sp_row, ctx->sp_coef, wsrc, ctx->sp_T, ctx->H, ctx->np);
   if (ctx->nq > 0)  // + hessianAt/d = P_k / d_k  (BarrierSolver.scala:314)
@@ -862,13 +878,14 @@ static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, doubl
 static int kkt_solve_pd_wide(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
   hipStream_t s = ctx->s;
   const int n = ctx->n, np = ctx->np, p = ctx->p, nr = p + 1;
-  if (!ctx->blas) {
-    if (lib_handle_create(s, &ctx->blas) != 0) return set_err(ctx, CVXG_E_HIP, "rocBLAS handle creation failed");
-    CHK(dalloc(ctx, &ctx->kY, (size_t)np * nr));
-    CHK(dalloc(ctx, &ctx->kR, (size_t)p * nr));
-    CHK(dalloc(ctx, &ctx->kS, (size_t)p * p));
-    CHK(dalloc(ctx, &ctx->kzp, (size_t)p));
-    CHK(dalloc(ctx, &ctx->kinfo, 1));
+  if (!ctx->blas || !ctx->kY || !ctx->kR || !ctx->kS || !ctx->kzp || !ctx->kinfo) {  // lazily, each piece once
+    if (!ctx->kY) CHK(dalloc(ctx, &ctx->kY, (size_t)np * nr));
+    if (!ctx->kR) CHK(dalloc(ctx, &ctx->kR, (size_t)p * nr));
+    if (!ctx->kS) CHK(dalloc(ctx, &ctx->kS, (size_t)p * p));
+    if (!ctx->kzp) CHK(dalloc(ctx, &ctx->kzp, (size_t)p));
+    if (!ctx->kinfo) CHK(dalloc(ctx, &ctx->kinfo, 1));
+    if (!ctx->blas && lib_handle_create(s, &ctx->blas) != 0)
+      return set_err(ctx, CVXG_E_HIP, "rocBLAS handle creation failed");
   }
   tstart(ctx, 1);
   ruiz(ctx);
@@ -972,7 +989,8 @@ struct TrialBatch {
   double logs[LS_TRIALS];
   double lerr[LS_TRIALS];  // certified mode: bound of the log-sum error (inf: not certifiable)
   double labs[LS_TRIALS];  // certified mode: sum |log d_i|
-  double kl[LS_TRIALS];    // KL dual: sum_j R exp(-(B'(x + t_k s))_j)
+  double kl[LS_TRIALS];    // KL dual: sum_j R exp(-(B'(x + t_k s))_j); KL primal: sum_j xt_j log(n xt_j)
+  double kla[LS_TRIALS];   // KL primal: the error scale of kl (certified mode)
   int viol[LS_TRIALS], npos[LS_TRIALS], sure[LS_TRIALS], amb[LS_TRIALS];
 };
 
@@ -981,13 +999,25 @@ static constexpr double U53 = 1.1102230246251565e-16;  // unit roundoff 2^-53
 // margin and room for the few roundings around the dot (r +, x + s t, ub -)
 static double ls_gamma(const cvxg_ctx* ctx) { return 4.0 * (ctx->np + 16) * U53; }
 
+// The objective's own per-trial terms when it is not linear / quadratic in the step: the KL dual's R.exp(-B'(z + t s))
+// or the KL primal's (x + s t).log(n (x + s t)) with its error scale; copied into b->kl / b->kla on the stream.
+static int ls_objective_trials(cvxg_ctx* ctx, double tbase, double beta, TrialBatch* b) {
+  if (ctx->kl) {
+    launch_ls_kl(ctx->s, ctx->kl_v, ctx->kl_u, ctx->nout, ctx->kl_R, tbase, beta, ctx->kl_part, ctx->kl_ls);
+    HIPC(ctx, hipMemcpyAsync(b->kl, ctx->kl_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
+  } else if (ctx->klp) {
+    launch_ls_klp(ctx->s, ctx->x, ctx->sdir, ctx->n, ctx->klp_n, tbase, beta, ctx->klp_part, ctx->klp_ls);
+    HIPC(ctx, hipMemcpyAsync(b->kl, ctx->klp_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
+    HIPC(ctx, hipMemcpyAsync(b->kla, ctx->klp_ls + LS_TRIALS, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost,
+                             ctx->s));
+  }
+  return CVXG_OK;
+}
+
 static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch* b) {
   if (ctx->m == 0) {  // no inequality constraints: every trial is in C and contributes no log terms
-    if (ctx->kl) {
-      launch_ls_kl(ctx->s, ctx->kl_v, ctx->kl_u, ctx->nout, ctx->kl_R, tbase, beta, ctx->kl_part, ctx->kl_ls);
-      HIPC(ctx, hipMemcpyAsync(b->kl, ctx->kl_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
-      HIPC(ctx, hipStreamSynchronize(ctx->s));
-    }
+    CHK(ls_objective_trials(ctx, tbase, beta, b));
+    HIPC(ctx, hipStreamSynchronize(ctx->s));
     b->k0 = k0;
     for (int k = 0; k < LS_TRIALS; ++k) {
       b->logs[k] = b->lerr[k] = b->labs[k] = 0.0;
@@ -995,10 +1025,7 @@ static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch
     }
     return CVXG_OK;
   }
-  if (ctx->kl) {
-    launch_ls_kl(ctx->s, ctx->kl_v, ctx->kl_u, ctx->nout, ctx->kl_R, tbase, beta, ctx->kl_part, ctx->kl_ls);
-    HIPC(ctx, hipMemcpyAsync(b->kl, ctx->kl_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
-  }
+  CHK(ls_objective_trials(ctx, tbase, beta, b));
   const int nb = ls_blocks(ctx->m);
   const bool cert = ls_certified(ctx);
   launch_ls_trials(ctx->s, ctx->c, ctx->e, ctx->ub, ctx->m, tbase, beta, ctx->ls_plog, ctx->ls_pcnt,
@@ -1046,10 +1073,14 @@ static int trial_fresh(cvxg_ctx* ctx, double tt, FreshTrial* out) {
     launch_rowdot(s, ctx->P, np, np, np, ctx->xtr, ctx->Pxtr);
     launch_dot(s, ctx->xtr, ctx->Pxtr, np, ctx->ctrl, SC_TR_XPX);
   }
+  if (ctx->klp) {  // Dist_KL.objectiveFunction(n).valueAt(xt) = xt dot log(xt*n)
+    launch_klp_eval(s, ctx->xtr, ctx->n, np, ctx->klp_n, ctx->klp_lxt, nullptr, nullptr, nullptr);
+    launch_dot(s, ctx->xtr, ctx->klp_lxt, np, ctx->ctrl, SC_TR_KLP);
+  }
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
   const DevCtrl& h = *ctx->hctrl;
-  const double f0 = ctx->r0 + h.sc[SC_TR_A0X] + (quad ? h.sc[SC_TR_XPX] / 2 : 0.0);
+  const double f0 = ctx->klp ? h.sc[SC_TR_KLP] : ctx->r0 + h.sc[SC_TR_A0X] + (quad ? h.sc[SC_TR_XPX] / 2 : 0.0);
   out->fv = ctx->t * f0 - h.sc[SC_TR_SUMLOG];
   out->viol = h.not_strict;
   out->npos = h.infeasible;
@@ -1108,21 +1139,25 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
   CHK(sync_ctrl(ctx));
   const DevCtrl h = *ctx->hctrl;
   const double tb = ctx->t, f = ctx->f_at_x;
-  auto f0_at = [&](double tt, double klsum) {  // r + a.(x+st) + (x+st)'P(x+st)/2, or w.(z+st) + R.exp(-B'(z+st))
+  // r + a.(x+st) + (x+st)'P(x+st)/2, or w.(z+st) + R.exp(-B'(z+st)), or the KL primal (x+st).log(n (x+st))
+  auto f0_at = [&](double tt, double klsum) {
     if (ctx->kl) return (h.sc[SC_A0X] + tt * h.sc[SC_A0S]) + klsum;
+    if (ctx->klp) return klsum;
     double v = ctx->r0 + (h.sc[SC_A0X] + tt * h.sc[SC_A0S]);
     if (quad) v += (h.sc[SC_XPX] + 2 * tt * h.sc[SC_SPX] + tt * tt * h.sc[SC_SPS]) / 2;
     return v;
   };
   // error bounds (certified mode) of the objective part at x + s tt and of the barrier value f at x
   const double gam = ls_gamma(ctx);
-  auto ef0_at = [&](double tt) {
+  // (klabs: the KL primal's error scale at the trial point; the KL dual's terms are not certified)
+  auto ef0_at = [&](double tt, double klabs) {
+    if (ctx->klp) return gam * klabs;
     double v = fabs(ctx->r0) + h.sc[SC_A0XA] + tt * h.sc[SC_A0SA];
     if (quad) v += (h.sc[SC_XPXA] + 2 * tt * h.sc[SC_SPXA] + tt * tt * h.sc[SC_SPSA]) / 2;
     return gam * v;
   };
-  const double ef_x = tb * ef0_at(0.0) + 2.0 * gam * h.sc[SC_CAINV] + (ctx->mp + 8) * U53 * h.sc[SC_LOGABS] +
-                      8 * U53 * fabs(f);
+  const double ef_x = tb * ef0_at(0.0, h.sc[SC_KLPA]) + 2.0 * gam * h.sc[SC_CAINV] +
+                      (ctx->mp + 8) * U53 * h.sc[SC_LOGABS] + 8 * U53 * fabs(f);
   TrialBatch b;
   double tcur = 1.0;
   double tbatch = 1.0;  // t at the start of the next batch (products of beta, UnconstrainedSolver.scala:93)
@@ -1171,9 +1206,15 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
     int npos = b.npos[j];
     double fv = tb * f0_at(tcur, b.kl[j]) - b.logs[j];
     const double thr = f + alpha * tcur * q;
+    if (cert && fresh_it == it) {
+      // this trial's feasibility was decided fresh: its d > 0 test and its value are the fresh evaluation's too (the
+      // batch log sum skips rows whose own d <= 0 with no error bound, so it cannot stand in for barrierFunction here)
+      npos = fr.npos;
+      fv = fr.fv;
+    }
     if (cert) {
-      if (fresh_it == it) npos = fr.npos;  // this trial's feasibility was decided fresh: its d > 0 test too
-      const double efv = tb * ef0_at(tcur) + b.lerr[j] + (ctx->mp + 8) * U53 * b.labs[j] + 8 * U53 * fabs(fv);
+      const double efv =
+          tb * ef0_at(tcur, b.kla[j]) + b.lerr[j] + (ctx->mp + 8) * U53 * b.labs[j] + 8 * U53 * fabs(fv);
       const double ethr = ef_x + 8 * U53 * (fabs(f) + fabs(alpha * tcur * q));
       if (!(fabs(fv - thr) > efv + ethr)) ++*ties;  // a tie: decided by the batch value (see above)
     }
@@ -1342,7 +1383,8 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->pd_w, ctx->pd_rhs, ctx->pd_d1, ctx->pd_R0, ctx->pd_R1, ctx->pd_tmp, ctx->pd_part_rows,
                   ctx->pd_part_cols, ctx->pd_out, ctx->qrows, ctx->qslot, ctx->Pq, ctx->qPx, ctx->qPs,
                   ctx->qextra, ctx->qf, ctx->aff_F, ctx->aff_z0, ctx->ls_paux, ctx->cabs, ctx->eabs, ctx->Pxa,
-                  ctx->Psa, ctx->xtr, ctx->Pxtr, ctx->c_tr, ctx->d_tr, ctx->invd_tr, ctx->w_tr, ctx->logd_tr};
+                  ctx->Psa, ctx->xtr, ctx->Pxtr, ctx->c_tr, ctx->d_tr, ctx->invd_tr, ctx->w_tr, ctx->logd_tr,
+                  ctx->klp_lx, ctx->klp_g0, ctx->klp_hd, ctx->klp_ab, ctx->klp_lxt, ctx->klp_part, ctx->klp_ls};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->kY, (void*)ctx->kR, (void*)ctx->kS, (void*)ctx->kzp, (void*)ctx->kinfo})
@@ -1374,6 +1416,7 @@ int cvxg_set_objective(cvxg_ctx* ctx, const double* P, int ldP, const double* a,
   CHK(upload_vec(ctx, ctx->a0, a, n, np));
   ctx->r0 = r;
   ctx->kl = 0;
+  ctx->klp = 0;
   ctx->have_obj = 1;
   ctx->x_eval_valid = 0;
   return CVXG_OK;
@@ -1412,9 +1455,31 @@ int cvxg_set_objective_kl(cvxg_ctx* ctx, const double* B, int ldB, int row_major
   CHK(upload_vec(ctx, ctx->a0, w, n, np));
   ctx->r0 = 0.0;
   ctx->kl = 1;
+  ctx->klp = 0;
   ctx->nout = nout;
   ctx->noutp = noutp;
   ctx->kl_R = R;
+  ctx->have_obj = 1;
+  ctx->x_eval_valid = 0;
+  return CVXG_OK;
+}
+
+int cvxg_set_objective_kl_primal(cvxg_ctx* ctx, int nout) {
+  if (!ctx || nout <= 0) return CVXG_E_ARG;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  const int np = ctx->np;
+  if (!ctx->klp_lx) {
+    for (double** v : {&ctx->klp_lx, &ctx->klp_g0, &ctx->klp_hd, &ctx->klp_ab, &ctx->klp_lxt}) CHK(dalloc(ctx, v, np));
+    CHK(dalloc(ctx, &ctx->klp_part, (size_t)ls_klp_blocks(ctx->n) * 2 * LS_TRIALS));
+    CHK(dalloc(ctx, &ctx->klp_ls, 2 * LS_TRIALS));
+  }
+  HIPC(ctx, hipMemsetAsync(ctx->a0, 0, (size_t)np * sizeof(double), ctx->s));  // no linear term: g = (0 + g0) t
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  ctx->klp_n = (double)nout;  // Dist_KL: n.toDouble in x*n, log(n) in the gradient
+  ctx->r0 = 0.0;
+  ctx->hasP = 0;
+  ctx->kl = 0;
+  ctx->klp = 1;
   ctx->have_obj = 1;
   ctx->x_eval_valid = 0;
   return CVXG_OK;
@@ -1865,9 +1930,15 @@ extern "C++" {
 template <class F>
 static int batch_run(int count, cvxg_ctx* const* ctxs, int* status, F one) {
   if (count < 0 || (count > 0 && !ctxs)) return CVXG_E_ARG;
+  bool bad = false;
   for (int i = 0; i < count; ++i)
-    for (int j = 0; j < i; ++j)
-      if (!ctxs[i] || ctxs[i] == ctxs[j]) return CVXG_E_ARG;  // one thread per distinct context
+    for (int j = 0; j <= i; ++j)
+      if (!ctxs[i] || (j < i && ctxs[i] == ctxs[j])) bad = true;  // one thread per distinct context
+  if (bad) {  // nothing ran: every status says so (a caller reading status[] alone must not see success)
+    if (status)
+      for (int i = 0; i < count; ++i) status[i] = CVXG_E_ARG;
+    return CVXG_E_ARG;
+  }
   std::vector<int> rc(count, CVXG_OK);
   std::vector<std::thread> th;
   th.reserve(count);
@@ -1922,7 +1993,8 @@ static int pd_check(cvxg_ctx* ctx) {
     return set_err(ctx, CVXG_E_UNSUPPORTED,
                    "PrimalDualSolver.solve_withEQs is not built (its KKT right-hand side has the opposite sign of "
                    "the no-equality system, PrimalDualSolver.scala:284)");
-  if (ctx->kl) return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: quadratic or linear objective only");
+  if (ctx->kl || ctx->klp)
+    return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: quadratic or linear objective only");
   if (ctx->nq > 0) return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: linear constraints only");
   if (ctx->m == 0) return set_err(ctx, CVXG_E_ARG, "primal-dual solver needs inequality constraints");
   if (ctx->lam) return CVXG_OK;
@@ -2222,7 +2294,7 @@ int cvxg_affine_from(cvxg_ctx* dst, cvxg_ctx* src, const double* z0, const doubl
   if (ldF < src->n) return set_err(dst, CVXG_E_DIM, "cvxg_affine_from: ldF < n");
   if (!src->have_obj || !src->have_ineq || (src->p > 0 && !src->have_eq))
     return set_err(dst, CVXG_E_ARG, "cvxg_affine_from: the source problem is not complete");
-  if (src->kl) return set_err(dst, CVXG_E_UNSUPPORTED, "cvxg_affine_from: KL dual objective");
+  if (src->kl || src->klp) return set_err(dst, CVXG_E_UNSUPPORTED, "cvxg_affine_from: KL objective");
   HIPC(dst, hipSetDevice(src->dev));
   HIPC(dst, hipStreamSynchronize(src->s));
   const int n = src->n, k = dst->n, m = src->m, p = src->p, nq = src->nq;

@@ -601,6 +601,77 @@ void launch_ls_kl(hipStream_t s, const double* v, const double* u, int nout, dou
   k_sum_chunks<<<1, LS_TRIALS, 0, s>>>(part, nb, LS_TRIALS, out);
 }
 
+// KL primal objective Dist_KL.objectiveFunction(n) (Dist_KL.scala:223-239) at x, per coordinate j < n:
+//   lx_j = log(x_j * n)                      (valueAt = x dot log(x*n.toDouble): the dot is taken over x and lx)
+//   g0_j = (1 + log(x_j)) + log(n)            (gradientAt, left to right)
+//   hd_j = 1 / x_j                            (hessianAt = diag(1/x))
+//   ab_j = |x_j lx_j| + |x_j|                 (error scale of the value term, certified line search)
+// zeros on the padding.
+__global__ void k_klp_eval(const double* __restrict__ x, int n, int np, double nd, double* __restrict__ lx,
+                           double* __restrict__ g0, double* __restrict__ hd, double* __restrict__ ab) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= np) return;
+  double l = 0.0, g = 0.0, h = 0.0, a = 0.0;
+  if (j < n) {
+    const double xj = x[j];
+    l = log(xj * nd);
+    g = (1.0 + log(xj)) + log(nd);
+    h = 1.0 / xj;
+    a = fabs(xj * l) + fabs(xj);
+  }
+  lx[j] = l;
+  if (g0) g0[j] = g;
+  if (hd) hd[j] = h;
+  if (ab) ab[j] = a;
+}
+void launch_klp_eval(hipStream_t s, const double* x, int n, int np, double nd, double* lx, double* g0, double* hd,
+                     double* ab) {
+  k_klp_eval<<<(np + 255) / 256, 256, 0, s>>>(x, n, np, nd, lx, g0, hd, ab);
+}
+
+// KL primal objective at the LS_TRIALS trial points xt = x + s*t_k (t_k = tbase beta^k by repeated products, as the
+// host's backtracking; x + s*t with two roundings, as Breeze's x + s*t): per trial {sum_j xt_j log(xt_j n),
+// sum_j |xt_j log(xt_j n)| + |xt_j|}; per-block partials, then a fixed-order sum over the blocks.  A trial outside
+// the domain (some xt_j <= 0) gives a NaN / -inf sum; the backtracking into C has rejected it before Armijo reads it.
+__global__ __launch_bounds__(256) void k_ls_klp(const double* __restrict__ x, const double* __restrict__ sdir, int n,
+                                                double nd, double tbase, double beta, double* __restrict__ part) {
+  __shared__ double sred[2][4][LS_TRIALS];
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool valid = j < n;
+  const double xj = valid ? x[j] : 0.0, sj = valid ? sdir[j] : 0.0;
+  double t = tbase;
+  for (int k = 0; k < LS_TRIALS; ++k) {
+    double v = 0.0, a = 0.0;
+    if (valid) {
+      const double st = sj * t;
+      const double xt = xj + st;
+      const double l = log(xt * nd);
+      v = xt * l;
+      a = fabs(v) + fabs(xt);
+    }
+    const double sv = wave_sum(v), sa = wave_sum(a);
+    if (lane == 0) {
+      sred[0][wid][k] = sv;
+      sred[1][wid][k] = sa;
+    }
+    t *= beta;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * LS_TRIALS) {
+    const int q = threadIdx.x / LS_TRIALS, k = threadIdx.x % LS_TRIALS;
+    part[(size_t)blockIdx.x * 2 * LS_TRIALS + q * LS_TRIALS + k] =
+        ((sred[q][0][k] + sred[q][1][k]) + sred[q][2][k]) + sred[q][3][k];
+  }
+}
+int ls_klp_blocks(int n) { return (n + 255) / 256; }
+void launch_ls_klp(hipStream_t s, const double* x, const double* sdir, int n, double nd, double tbase, double beta,
+                   double* part, double* out) {
+  const int nb = ls_klp_blocks(n);
+  k_ls_klp<<<nb, 256, 0, s>>>(x, sdir, n, nd, tbase, beta, part);
+  k_sum_chunks<<<1, 2 * LS_TRIALS, 0, s>>>(part, nb, 2 * LS_TRIALS, out);
+}
+
 // KL dual at z (v = B'z given): y_j = R exp(-v_j) for j < nout (Dist_KL.scala:163, 170), 0 on the padding
 __global__ void k_kl_eval(const double* __restrict__ v, int nout, int noutp, double R, double* __restrict__ y) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -786,14 +857,16 @@ void launch_kkt_prep_cm(hipStream_t s, const double* Aeq, int ld, int p, int n, 
 // S = (R + R')/2 (KKTSystem.scala:139) and z = -(b + R[:, p]) (:141) from R = B X (p x (p+1), column-major)
 __global__ void k_kkt_sym(const double* __restrict__ R, int p, const double* __restrict__ b, double* __restrict__ S,
                           double* __restrict__ z) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p * p) return;
-  const int r = i % p, c = i / p;
-  S[i] = (R[(size_t)c * p + r] + R[(size_t)r * p + c]) * 0.5;
-  if (c == 0) z[r] = -(b[r] + R[(size_t)p * p + r]);
+  const size_t pp = (size_t)p * p;  // p < n <= 65472: p*p exceeds int range
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= pp) return;
+  const size_t r = i % p, c = i / p;
+  S[i] = (R[c * p + r] + R[r * p + c]) * 0.5;
+  if (c == 0) z[r] = -(b[r] + R[pp + r]);
 }
 void launch_kkt_sym(hipStream_t s, const double* R, int p, const double* b, double* S, double* z) {
-  k_kkt_sym<<<(p * p + 255) / 256, 256, 0, s>>>(R, p, b, S, z);
+  const size_t pp = (size_t)p * p;
+  k_kkt_sym<<<(unsigned)((pp + 255) / 256), 256, 0, s>>>(R, p, b, S, z);
 }
 
 // out = u + alpha*v elementwise with a strided source column: out_i = u_i + alpha * v[i*vs + vc]

@@ -1,5 +1,6 @@
 // kernels.hpp — host-side launch wrappers for the HIP kernels of the barrier engine.
 #pragma once
+#include <assert.h>
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
@@ -52,8 +53,10 @@ struct DotBatch {
   int kind[DOTS_MAX];
   int count;
   void add(int k, const double* uu, const double* vv, int len, int sl) {
+    assert(count < DOTS_MAX && "DotBatch full: launch it and start a new batch");
     u[count] = uu, v[count] = vv, n[count] = len, slot[count] = sl, kind[count] = k, ++count;
   }
+  bool full() const { return count >= DOTS_MAX; }
 };
 void launch_dots(hipStream_t s, const DotBatch& a, DevCtrl* ctrl);
 // out = u + v*alpha (alpha read from device scalar pointer or host value)
@@ -108,8 +111,10 @@ void launch_pd_trials(hipStream_t s, const double* c, const double* e, const dou
 
 // ---- MFMA SYRK (k_syrk.hip) -----------------------------------------------------------------------
 // H = t*P + A' diag(w) A over the lower tile list; split-K when nsplit > 1 (partials + ordered reduce).
+// Pd (optional, with P NULL): a diagonal objective Hessian, H_jj += t Pd_j (the KL primal objective's diag(1/x)).
 void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double* w, int mp, const double* P,
-                          const DevCtrl* ctrl, double* H, int ldh, TileList tiles, int nsplit, double* partials);
+                          const DevCtrl* ctrl, double* H, int ldh, TileList tiles, int nsplit, double* partials,
+                          const double* Pd = nullptr);
 
 // ---- Cholesky (k_chol.hip) ------------------------------------------------------------------------
 // k_dataflow.hip: the whole factorization (potrf + trsm + updates + fused forward solve) as one persistent
@@ -138,6 +143,15 @@ int ls_blocks(int m);
 void launch_kl_eval(hipStream_t s, const double* v, int nout, int noutp, double R, double* y);
 void launch_ls_kl(hipStream_t s, const double* v, const double* u, int nout, double R, double tbase, double beta,
                   double* part, double* out);
+
+// KL primal objective (Dist_KL.scala:223-239): lx = log(n x), g0 = gradient, hd = diag of the Hessian, ab = error
+// scale of the value terms (each output may be NULL but lx)
+void launch_klp_eval(hipStream_t s, const double* x, int n, int np, double nd, double* lx, double* g0, double* hd,
+                     double* ab);
+// per trial k: out[k] = sum_j xt log(n xt), out[LS_TRIALS + k] = its error scale, xt = x + s t_k
+int ls_klp_blocks(int n);
+void launch_ls_klp(hipStream_t s, const double* x, const double* sdir, int n, double nd, double tbase, double beta,
+                   double* part, double* out);
 
 // ---- KKT Schur complement (p > 0) ------------------------------------------------------------------
 void launch_kkt_schur(hipStream_t s, const double* X, int nrhs, const double* B, int ldb, int p, int n,

@@ -101,6 +101,11 @@ class Engine:
         self._check(self.lib.cvxg_set_objective_kl(self.h, _dp(B), B.shape[1], 1, B.shape[1], _dp(w), float(R)))
         self._keep_obj = (B, w)
 
+    def set_objective_kl_primal(self, nout: int):
+        """Dist_KL.objectiveFunction(nout): x . log(nout x) (cvxg_set_objective_kl_primal)."""
+        self._check(self.lib.cvxg_set_objective_kl_primal(self.h, int(nout)))
+        self._keep_obj = None
+
     def set_ineq(self, A, r, ub):
         A, r, ub = _f64(A), _f64(r), _f64(ub)
         self._check(self.lib.cvxg_set_ineq(self.h, _dp(A), A.shape[1] if A.ndim == 2 else self.n, 1, _dp(r), _dp(ub)))
@@ -120,6 +125,8 @@ class Engine:
     def load_problem(self, spec: dict):
         if spec.get("kl_B") is not None:
             self.set_objective_kl(spec["kl_B"], spec["a0"], float(np.asarray(spec["kl_R"]).ravel()[0]))
+        elif spec.get("klp_n") is not None:
+            self.set_objective_kl_primal(int(np.asarray(spec["klp_n"]).ravel()[0]))
         else:
             self.set_objective(spec["a0"], spec.get("r0", 0.0), spec.get("P"))
         self.set_ineq(spec["A"], spec["r"], spec["ub"])
@@ -268,7 +275,9 @@ def batch_barrier_solve(engines, pars, termination: int = 0):
     sols = (L.cvxg_solution * k)()
     st = (C.c_int * k)()
     ps = params_struct(pars)
-    lib.cvxg_batch_barrier_solve(k, hs, C.byref(ps), int(termination), sols, st)
+    rc = lib.cvxg_batch_barrier_solve(k, hs, C.byref(ps), int(termination), sols, st)
+    if rc == L.CVXG_E_ARG:  # rejected before any instance ran (NULL or repeated context)
+        raise CvxgError(rc, "cvxg_batch_barrier_solve: NULL or repeated context")
     return list(sols), list(st)
 
 
@@ -280,7 +289,9 @@ def batch_newton_step(engines, pars):
     infos = (L.cvxg_step_info * k)()
     st = (C.c_int * k)()
     ps = params_struct(pars)
-    lib.cvxg_batch_newton_step(k, hs, C.byref(ps), infos, st)
+    rc = lib.cvxg_batch_newton_step(k, hs, C.byref(ps), infos, st)
+    if rc == L.CVXG_E_ARG:
+        raise CvxgError(rc, "cvxg_batch_newton_step: NULL or repeated context")
     return list(infos), list(st)
 
 

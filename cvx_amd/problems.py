@@ -103,6 +103,37 @@ def kl_dual_spec(nout: int, k: int, instance: int = 0) -> Dict[str, np.ndarray]:
                 kl_R=np.array([1.0 / (nout * 2.7182811828459045)]))
 
 
+def kl_primal_spec(n: int, kind: str = "kl_1") -> Dict[str, np.ndarray]:
+    """The direct (primal) KL problems of OptimizationProblems.scala on Dist_KL.objectiveFunction(n) (x . log(n x),
+    Dist_KL.scala:223-239), n even and > 9:
+    * kl_1 (:167-210): rows x_j >= 0 (allCoordinatesPositive) then P(A) >= 0.36 and P(B) <= 0.1 (expectation_lt_r),
+      equality sum(x) = 1 (Constraints.sumToOne); A = {0, 1, 2}, B = {n/2, .., n-1};
+    * kl_2 (:271-320): the positivity rows, equalities 1'x = 1, P(A) = 0.36, P(B) = 0.1 (probEq.addEqualities(e1)
+      .addEqualities(e2)).
+    x0 is strictly feasible for the inequalities (P(A) = 0.39, P(B) = 0.09 for kl_1; the known optimum, which has
+    every x_j > 0, for kl_2); x_opt = kl1_ / kl2_analyticSolution (:136-141, 249-251, n > 15)."""
+    assert n > 9 and n % 2 == 0
+    j = np.arange(n)
+    I_A = (j < 3).astype(float)
+    I_B = (j >= n // 2).astype(float)
+    A, r, ub = _positivity(n)
+    x_opt = np.where(j < 3, 0.12, np.where(j >= n // 2, 0.2 / n, 1.08 / (n - 6)))
+    if kind == "kl_1":
+        A = np.vstack([A, -I_A, I_B])
+        r = np.zeros(n + 2)
+        ub = np.concatenate([ub, [-0.36, 0.1]])
+        Aeq, beq = _sum_to_one(n)
+        x0 = np.where(j < 3, 0.13, np.where(j >= n // 2, 0.18 / n, 0.52 / (n // 2 - 3)))
+    elif kind == "kl_2":
+        Aeq = np.vstack([np.ones(n), I_A, I_B])
+        beq = np.array([1.0, 0.36, 0.1])
+        x0 = x_opt.copy()
+    else:
+        raise ValueError(kind)
+    return dict(id=f"{kind}(n={n})", a0=np.zeros(n), r0=0.0, P=None, A=A, r=r, ub=ub, Aeq=Aeq, beq=beq, x0=x0,
+                klp_n=n, x_opt=x_opt, x_where_defined=np.full(n, 1.0 / n))
+
+
 def _positivity(n: int):
     """Constraints.allCoordinatesPositive (Constraints.scala:26-69): -x_j <= 0, j = 0..n-1."""
     return -np.eye(n), np.zeros(n), np.zeros(n)

@@ -121,6 +121,13 @@ int cvxg_set_objective(cvxg_ctx* ctx, const double* P, int ldP, const double* a,
 int cvxg_set_objective_kl(cvxg_ctx* ctx, const double* B, int ldB, int row_major, int nout, const double* w,
                           double R);
 
+/* Dist_KL.objectiveFunction(n) (Dist_KL.scala:223-239), the KL distance from the uniform distribution on nout outcomes
+ * (nout = the context's n for Dist_KL's own problems):
+ *   valueAt(x) = x . log(x * nout),  gradientAt(x)_j = (1 + log x_j) + log nout,  hessianAt(x) = diag(1 / x).
+ * Defined for x > 0 (Dist_KL's allCoordinatesPositive rows keep the iterates there).  The barrier path only: the
+ * primal-dual solver and cvxg_affine_from return CVXG_E_UNSUPPORTED for it. */
+int cvxg_set_objective_kl_primal(cvxg_ctx* ctx, int nout);
+
 /* The LinearConstraint list r_i + a_i.x <= ub_i (LinearConstraint.scala:7-32), A row i = a_i in LIST
  * order (fold and forall order matter: BarrierSolver.scala:280-315, ConstraintSet.scala:34-38). */
 int cvxg_set_ineq(cvxg_ctx* ctx, const double* A, int ldA, int row_major, const double* r,

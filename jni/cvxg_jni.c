@@ -364,8 +364,9 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_batchBarrierSolve(JNIEnv* env, jc
   jsize k = (*env)->GetArrayLength(env, handles);
   jlong* hv = (jlong*)malloc((size_t)(k > 0 ? k : 1) * sizeof(jlong));
   cvxg_ctx** cv = (cvxg_ctx**)malloc((size_t)(k > 0 ? k : 1) * sizeof(cvxg_ctx*));
-  cvxg_solution* sv = (cvxg_solution*)malloc((size_t)(k > 0 ? k : 1) * sizeof(cvxg_solution));
-  jint* st = (jint*)malloc((size_t)(k > 0 ? k : 1) * sizeof(jint));
+  /* zeroed: an argument error (CVXG_E_ARG) returns before any instance writes its slot */
+  cvxg_solution* sv = (cvxg_solution*)calloc((size_t)(k > 0 ? k : 1), sizeof(cvxg_solution));
+  jint* st = (jint*)calloc((size_t)(k > 0 ? k : 1), sizeof(jint));
   double* o = (double*)malloc((size_t)(k > 0 ? 9 * k : 1) * sizeof(double));
   if (!hv || !cv || !sv || !st || !o) {
     free(hv), free(cv), free(sv), free(st), free(o);

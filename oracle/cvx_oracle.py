@@ -119,6 +119,9 @@ class Problem:
     # r + a'x + x'P_k x / 2 <= ub with P_k = qP[k]
     qrows: Optional[np.ndarray] = None
     qP: Optional[np.ndarray] = None
+    # KL primal objective Dist_KL.objectiveFunction(klp_n) (Dist_KL.scala:223-239): f(x) = x . log(x klp_n),
+    # gradient 1 + log x + log klp_n, Hessian diag(1/x); a0 / r0 / P unused (a0 = 0 only sizes the problem)
+    klp_n: Optional[int] = None
 
     def quad_index(self, i: int) -> int:
         if self.qrows is None:
@@ -148,6 +151,8 @@ def objective_value(pb: Problem, x: np.ndarray) -> float:
         return objective_value(pb.pb, pb.x_of(x))
     if pb.kl_B is not None:
         return float(np.dot(pb.a0, x)) + float(np.dot(pb.kl_R, np.exp(-(pb.kl_B.T @ x))))
+    if pb.klp_n is not None:  # Dist_KL.scala:226 — x dot log(x*n.toDouble)
+        return float(np.dot(x, np.log(x * float(pb.klp_n))))
     v = pb.r0 + float(np.dot(pb.a0, x))
     if pb.P is not None:
         v = v + float(np.dot(x, pb.P @ x)) / 2
@@ -159,6 +164,8 @@ def objective_gradient(pb: Problem, x: np.ndarray) -> np.ndarray:
     KL dual: -gradientDualObjFAt(z) = vec_w - B*(vec_R :* exp(-B'z)) (Dist_KL.scala:152-153)."""
     if pb.kl_B is not None:
         return pb.a0 - pb.kl_B @ kl_y(pb, x)
+    if pb.klp_n is not None:  # Dist_KL.scala:228-229 — DenseVector.tabulate(n)(j => 1+log(x(j))+log(n))
+        return (1.0 + np.log(x)) + math.log(pb.klp_n)
     if pb.P is None:
         return pb.a0.copy()
     return pb.a0 + pb.P @ x
@@ -171,6 +178,8 @@ def objective_hessian(pb: Problem, x: Optional[np.ndarray] = None) -> np.ndarray
         y = kl_y(pb, x)
         Bdy = pb.kl_B * y[None, :]
         return -(-(Bdy @ pb.kl_B.T))
+    if pb.klp_n is not None:  # Dist_KL.scala:231-236 — diag(1.0/x(j))
+        return np.diag(1.0 / x)
     if pb.P is None:
         return np.zeros((pb.n, pb.n))
     return pb.P

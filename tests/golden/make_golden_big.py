@@ -17,6 +17,10 @@ The line-search decisions (accepted step, both backtracking counters) are the re
 (UnconstrainedSolver.scala:83-113, oracle.unconstrained_line_search) run on that direction from the
 recorded (iteration, frozen trust radius).
 
+Late in the path (t >= 1e6) H is ill-conditioned, so the test holds those steps to backward-error, decrement-side and
+line-search-replay criteria instead of the 1e-8 direction bar.  C2 is also solved to the standard termination: its
+final x, per-centering step counts and active sets (separated threshold and Constraint.isActive's 1e-12) are stored.
+
 Run:  python tests/golden/make_golden_big.py [C2] [C3]   (C3 takes several minutes and ~6 GB of RAM)
 """
 from __future__ import annotations
@@ -37,9 +41,14 @@ from oracle import cvx_oracle as O  # noqa: E402
 
 CONFIGS = {
     # name: (n, m, instance, recorded (t, iteration-within-centering) pairs, form of the recorded directions)
-    "C2": (1024, 2048, 0, [(1.0, 0), (1.0, 1), (1e2, 0), (1e4, 0), (1e4, 1)], "fold"),
-    "C3": (4096, 8192, 0, [(1.0, 0), (1e2, 0), (1e4, 0), (1e4, 1)], "blas"),
+    "C2": (1024, 2048, 0, [(1.0, 0), (1.0, 1), (1e2, 0), (1e4, 0), (1e4, 1),
+                           (1e6, 0), (1e6, 1), (1e8, 0), (1e8, 1), (1e11, 0), (1e11, 1)], "fold"),
+    "C3": (4096, 8192, 0, [(1.0, 0), (1e2, 0), (1e4, 0), (1e4, 1), (1e6, 0), (1e6, 1), (1e8, 0), (1e8, 1)], "blas"),
 }
+# configurations whose whole barrier solve is run to the standard termination (gap < tolSolver): the final x, the
+# per-centering Newton step counts and the active sets at the separated threshold and at Constraint.isActive's 1e-12
+FULL = {"C2"}
+ACTIVE_SEPARATED = 1e-6
 
 
 def fingerprint(spec):
@@ -57,19 +66,28 @@ def make(name):
     pars = O.standard_params()
     sha, psum, a0sum = fingerprint(spec)
     t_last = max(t for t, _ in want)
+    full = name in FULL
     x = spec["x0"].copy()
     t = 1.0
     states = []  # (t, it_n, radius, x, grad)
-    while t <= t_last:
-        max_steps = max(k for tt, k in want if tt == t) + 1 if t == t_last else None
+    per_centering = []  # Newton steps of each centering (full solves)
+    gap = float("inf")
+    # the reference's t-loop (BarrierSolver.scala:70-117): until gap = m/t < tolSolver (full) or past t_last
+    while (gap >= pars.tolSolver) if full else (t <= t_last):
+        max_steps = max(k for tt, k in want if tt == t) + 1 if (t == t_last and not full) else None
         sol = O.unconstrained_solve(pb, t, x, pars, record=True, max_steps=max_steps, hess="blas", fast_subst=True)
         for rc in sol.records:
-            if (t, rc.it_n) in want:
+            if (t, rc.it_n) in want and rc.newton_decrement > pars.tolSolver:
                 states.append((t, rc.it_n, rc.radius, rc.x.copy(), rc.grad.copy()))
         print(f"{name}: t={t:g} {sol.newton_steps} steps ({time.time() - t0:.0f} s)", flush=True)
+        per_centering.append(sol.newton_steps)
         x = sol.x
+        gap = m / t
         t *= 10.0
-    assert len(states) == len(want), (len(states), want)
+    x_final = x.copy()
+    missing = [w for w in want if w not in [(s_[0], s_[1]) for s_ in states]]
+    if missing:  # a centering that ends before its second step (or a final decrement below tol) has nothing there
+        print(f"{name}: not recorded (no such moving step): {missing}", flush=True)
     out = {k: [] for k in ("t", "it_n", "radius", "x", "grad", "f", "dx", "q", "step", "kc", "ka", "ruiz", "reg",
                            "rel_err")}
     for (t, it_n, radius, x, g) in states:
@@ -91,6 +109,19 @@ def make(name):
         print(f"{name}: t={t:g} it={it_n} q={q:.6e} step={st:g} kc={k1} ka={it - k1} ruiz={rec.ruiz_sweeps} "
               f"reg={rec.regularized}", flush=True)
     arrays = {k: np.array(v) for k, v in out.items()}
+    if full:  # the whole solve: final x, step counts per centering, active sets (Constraint.isActive, :26)
+        x = x_final
+        g = pb.r + pb.A @ x
+        marg = np.abs(g - pb.ub)
+        act_sep = np.nonzero(marg < ACTIVE_SEPARATED)[0]
+        act_12 = np.nonzero(marg < 1e-12)[0]
+        # separation of the threshold: no margin within a factor 100 of it
+        near = np.sum((marg > ACTIVE_SEPARATED / 100) & (marg < ACTIVE_SEPARATED * 100))
+        print(f"{name}: final gap {gap:.3e}, {sum(per_centering)} Newton steps {per_centering}, active "
+              f"{len(act_sep)} (< {ACTIVE_SEPARATED:g}; {near} margins within 100x), {len(act_12)} (< 1e-12)")
+        arrays.update(x_final=x, gap=np.array(gap), per_centering=np.array(per_centering),
+                      active_sep=act_sep, active_1e12=act_12, active_threshold=np.array(ACTIVE_SEPARATED),
+                      active_near=np.array(near))
     arrays.update(n=np.array(n), m=np.array(m), instance=np.array(inst), sha256=np.array(sha), P_sum=np.array(psum),
                   a0_sum=np.array(a0sum), hess_form=np.array(form))
     path = os.path.join(HERE, "big", f"{name}_n{n}_m{m}.npz")

@@ -124,3 +124,43 @@ def test_jni_glue_binds_every_scala_native_and_every_step_entry():
               "constraintValues", "activeSet", "setQuad", "batchBarrierSolve"):
         assert s in c_names
     assert "GetPrimitiveArrayCritical" not in c_src  # no critical region spans a GPU call
+
+
+# Scala / Breeze names the glue uses that are not defined in the reference's own sources
+_SCALA_LIB = {"Array", "ArrayBuffer", "AssertionError", "DenseMatrix", "DenseVector", "Divergence",
+              "IllegalArgumentException", "Iterations", "MaxValue", "NotConvergedException", "RuntimeException", "Some",
+              "_1", "collection", "cols", "data", "fill", "forall", "foreach", "getOrElse", "gpu", "isDefined",
+              "isInstanceOf", "length", "linalg", "loadLibrary", "majorStride", "map", "mutable", "nonEmpty", "toArray",
+              "toInt", "zipWithIndex"}
+_SCALA_KW = {"if", "else", "for", "while", "match", "case", "new", "def", "val", "var", "return", "override", "yield",
+             "until", "with", "extends"}
+REF_SCALA = "/root/reference/src/main/scala/cvx"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SCALA), reason="reference sources not present (GPU box)")
+def test_scala_glue_calls_only_defined_names():
+    """Every name the Scala blocks of INTEGRATION.md call or select (f(..), x.f, new C) is defined in those blocks
+    (def / val / object / class / parameter / pattern) or in the reference's own sources (src/main/scala/cvx), or is a
+    Scala / Breeze library name.  Catches glue that calls helpers nobody defines (a maintainer pasting it would not
+    compile).  Names only: scoping and types are not checked."""
+    import glob
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    code = "\n".join(re.findall(r"```scala\n(.*?)```", doc, re.S))
+    code = re.sub(r"/\*.*?\*/", "", code, flags=re.S)
+    code = re.sub(r"//[^\n]*", "", code)
+    code = re.sub(r'"[^"\n]*"', '""', code)
+    defined = set(re.findall(r"\b(?:def|val|var|object|class|trait)\s+(\w+)", code))
+    defined |= set(re.findall(r"[(,]\s*(\w+)\s*:", code))       # parameters
+    defined |= set(re.findall(r"\b(\w+)\s*=>", code))           # lambda parameters
+    for pat in re.findall(r"\(([^()]*(?:\([^()]*\)[^()]*)*)\)\s*<-", code):  # for-comprehension patterns
+        defined |= set(re.findall(r"\w+", pat))
+    defined |= set(re.findall(r"\b(\w+)\s*<-", code))
+    ref = "".join(open(f).read() for f in glob.glob(os.path.join(REF_SCALA, "*.scala")))
+    ref_defined = set(re.findall(r"\b(?:def|val|var|object|class|trait)\s+(\w+)", ref))
+    ref_defined |= set(re.findall(r"[(,]\s*(\w+)\s*:", ref))    # constructor / case-class parameters
+    used = set(re.findall(r"\b([A-Za-z_]\w*)\s*\(", code)) | set(re.findall(r"\.([A-Za-z_]\w*)", code))
+    used |= set(re.findall(r"\bnew\s+(\w+)", code))
+    unknown = sorted(u for u in used if u not in defined | ref_defined | _SCALA_LIB | _SCALA_KW)
+    assert not unknown, unknown
+    # the onDevice factory carries what its reduced override needs
+    assert re.search(r"def onDevice\([^)]*device: Int\)", code, re.S)

@@ -684,6 +684,98 @@ def test_kl2A_dual_solve_on_gpu(mods):
     assert sol.nu is not None and sol.nu.shape == (3,)
 
 
+# ---- Dist_KL direct (primal) solve: the KL primal objective on the device ---------------------------------------
+
+def _klp_opb(O, spec):
+    return O.Problem(a0=spec["a0"], r0=0.0, P=None, A=spec["A"], r=spec["r"], ub=spec["ub"], Aeq=spec["Aeq"],
+                     beq=spec["beq"], klp_n=int(spec["klp_n"]))
+
+
+@pytest.mark.parametrize("kind,n", [("kl_1", 300), ("kl_1", 2048), ("kl_2", 2048)])
+def test_kl_primal_barrier_oracles_and_direction(mods, kind, n):
+    """Dist_KL.objectiveFunction (Dist_KL.scala:223-239: x . log(n x), (1 + log x) + log n, diag(1/x)) inside the
+    barrier value, gradient and Hessian (BarrierSolver.scala:280-315) against the oracle (1e-12), and the KKT Newton
+    direction (KKTSystem.solve with sum(x) = 1 and the expectation equalities) within 1e-8 of the oracle's at
+    t = 1, 1e2, 1e4."""
+    Z, SP, Engine, O = mods
+    spec = Z.kl_primal_spec(n, kind)
+    pb = _klp_opb(O, spec)
+    eng = Engine(n, spec["A"].shape[0], spec["Aeq"].shape[0])
+    eng.load_problem(spec)
+    pars = SP.standardParams()
+    x = spec["x0"]
+    for t in (1.0, 1e2, 1e4):
+        f, g, Hs = eng.barrier_eval(t, x, want_grad=True, want_hess=True)
+        fr, gr, Hr = O.barrier_value(pb, t, x), O.barrier_gradient(pb, t, x), O.barrier_hessian(pb, t, x, literal=False)
+        assert abs(f - fr) <= 1e-12 * max(1.0, abs(fr)), (t, f, fr)
+        assert np.linalg.norm(g - gr) <= 1e-12 * np.linalg.norm(gr), t
+        assert np.linalg.norm(Hs - Hr) <= 1e-12 * np.linalg.norm(Hr), t
+        assert np.array_equal(Hs, Hs.T)
+        dx, w, info = eng.newton_direction(pars, t, x)
+        assert info.fallback == 0
+        dref, wref = O.kkt_solve(Hr, pb.Aeq, gr, pb.beq - pb.Aeq @ x, pars.tolEqSolve)
+        assert np.linalg.norm(dx - dref) <= 1e-8 * np.linalg.norm(dref), t
+        assert np.linalg.norm(w - wref) <= 1e-7 * np.linalg.norm(wref), t
+    eng.close()
+
+
+@pytest.mark.parametrize("kind", ["kl_1", "kl_2"])
+def test_kl_primal_barrier_solve_vs_oracle(mods, kind):
+    """The whole equality-constrained barrier solve (EqualityConstrainedSolver, BarrierSolver.solveWithEQs) of kl_1 /
+    kl_2 at n = 40 from the same strictly feasible start: final x within 1e-6 of the oracle's trajectory, gaps below
+    tol, Newton step counts as the oracle's."""
+    Z, SP, Engine, O = mods
+    spec = Z.kl_primal_spec(40, kind)
+    pars = SP.standardParams()
+    eng = Engine(40, spec["A"].shape[0], spec["Aeq"].shape[0])
+    eng.load_problem(spec)
+    eng.set_x(spec["x0"])
+    sol = eng.barrier_solve(pars, termination=0)
+    x = eng.get_x()
+    eng.close()
+    ref = O.barrier_solve(_klp_opb(O, spec), spec["x0"], pars)
+    assert np.linalg.norm(x - ref.x) <= 1e-6 * np.linalg.norm(ref.x)
+    assert sol.duality_gap < pars.tolSolver and sol.equality_gap < pars.tolSolver
+    print(f"{kind}: engine {sol.newton_steps} Newton steps, oracle {ref.newton_steps}")
+    assert abs(sol.newton_steps - ref.newton_steps) <= max(2, int(0.05 * ref.newton_steps))
+
+
+def test_kl_primal_direct_solves_known_answers(mods):
+    """What MinimizationTests.runProblems does with every KL problem (MinimizationTests.scala:23,35): the direct solve
+    first.  kl_1 and kl_2 (OptimizationProblems.scala:167-210, 271-320) at n = 2048 through
+    OptimizationProblem.withoutFeasiblePoint (phase I, then the barrier solver over Dist_KL.objectiveFunction) hit
+    kl1_ / kl2_analyticSolution (reference tolerance 1e-2); kl_1A built by Dist_KL.apply solves directly (solve) and
+    through the dual (solveDual) to the same distribution."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import (ConstraintSet, Constraints, Dist_KL, EqualityConstraint, LinearConstraint,
+                             OptimizationProblem)
+    n = 2048
+    pars = SP.standardParams()
+    objF = Dist_KL.objectiveFunction(n)
+    for kind in ("kl_1", "kl_2"):
+        spec = Z.kl_primal_spec(n, kind)
+        cnts = [LinearConstraint(f"row{i}", n, spec["ub"][i], spec["r"][i], spec["A"][i])
+                for i in range(spec["A"].shape[0])]
+        ineqs = ConstraintSet(n, cnts, np.full(n, 1.0 / n))
+        prob = OptimizationProblem.withoutFeasiblePoint(kind, objF, ineqs, EqualityConstraint(spec["Aeq"], spec["beq"]),
+                                                        "BR", pars)
+        sol = prob.solve()
+        err = np.max(np.abs(sol.x - spec["x_opt"]))
+        print(f"{kind}(n={n}) direct: max |x - x_opt| = {err:.2e}, {sol.newtonSteps} Newton steps, gap "
+              f"{sol.dualityGap:.1e}")
+        assert err < 1e-2 and sol.dualityGap < pars.tolSolver and sol.equalityGap < pars.tolSolver
+        assert err < 1e-5  # the engine's own bar (gap 1e-8)
+        prob.solver.engine.close()
+    H, u = O.kl1A_data(n)
+    kl1A = Dist_KL.apply("dist_KL_1A", n, H, u, None, None, "BR", pars)
+    sol_d = kl1A.solve()
+    sol_dual = kl1A.solveDual("BR", pars)
+    assert np.max(np.abs(sol_d.x - sol_dual.x)) < 1e-5
+    assert np.max(np.abs(sol_d.x - O.kl1_analytic_solution(n))) < 1e-5
+    assert abs(objF.valueAt(sol_d.x) - objF.valueAt(sol_dual.x)) < 1e-7
+    kl1A.solver.engine.close()
+
+
 # ---- PrimalDualSolver (solverType "PD") on the device -----------------------------------------------------------
 
 @pytest.mark.parametrize("kind,n,m", [("qp", 40, 96), ("qp", 300, 500), ("bounds", 60, 40)])
@@ -1135,6 +1227,57 @@ def test_batch_barrier_solve_matches_single_contexts(mods):
     hs = (C.c_void_p * 2)(engs[0].h.value, engs[0].h.value)
     ps = params_struct(pars)
     assert _lib.lib().cvxg_batch_newton_step(2, hs, C.byref(ps), None, None) == _lib.CVXG_E_ARG
+    for e in engs:
+        e.close()
+
+
+def test_batch_full_size_contexts_share_one_gpu(mods):
+    """Config C5's batch path at its real size on one GPU: two C3 contexts (n=4096, m=8192) and two n=600 contexts
+    (10 Cholesky blocks) share cuda:0, so multi-block persistent k_chol_dataflow / k_bwd_dataflow launches of different
+    contexts overlap on one device.  cvxg_batch_newton_step (two steps from x0 at t = 1) and then
+    cvxg_batch_barrier_solve (the whole t-loop) give every instance bitwise the x, step records, step counts and gaps
+    of its own single-context run: one independent solve per instance (BarrierSolver.scala:70-117)."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.engine import batch_barrier_solve, batch_newton_step
+    pars = SP.standardParams()
+    pars.maxIter = 30  # at most 30 Newton steps per centering keeps the 13 centerings of each C3 solve within seconds
+    specs = [Z.random_qp(4096, 8192, instance=i) for i in (0, 1)] + [Z.random_qp(600, 1200, instance=70 + i)
+                                                                     for i in (0, 1)]
+    fields = ("step", "backtracks_c", "backtracks_armijo", "q", "f", "ruiz_sweeps", "regularized", "min_diag")
+    ref = []
+    for spec in specs:
+        e = _engine(Engine, spec)
+        e.set_x(spec["x0"])
+        e.centering_begin(1.0)
+        steps = [tuple(getattr(e.newton_step(pars), f) for f in fields) for _ in range(2)]
+        x2 = e.get_x()
+        e.set_x(spec["x0"])
+        s = e.barrier_solve(pars, 0)
+        ref.append((steps, x2, e.get_x(), s.newton_steps, s.outer_iters, s.duality_gap))
+        e.close()
+    engs = [_engine(Engine, spec) for spec in specs]
+    for e, spec in zip(engs, specs):
+        e.set_x(spec["x0"])
+        e.centering_begin(1.0)
+    got_steps = [[], [], [], []]
+    for _ in range(2):
+        infos, st = batch_newton_step(engs, pars)
+        assert st == [0, 0, 0, 0]
+        for i, inf in enumerate(infos):
+            got_steps[i].append(tuple(getattr(inf, f) for f in fields))
+    for i, e in enumerate(engs):
+        assert got_steps[i] == ref[i][0], i
+        assert np.array_equal(e.get_x(), ref[i][1]), i
+    for e, spec in zip(engs, specs):
+        e.set_x(spec["x0"])
+    sols, st = batch_barrier_solve(engs, pars, 0)
+    assert st == [0, 0, 0, 0]
+    for i, (e, s) in enumerate(zip(engs, sols)):
+        _, _, x, steps, outer, gap = ref[i]
+        assert np.array_equal(e.get_x(), x), i
+        assert (s.newton_steps, s.outer_iters, s.duality_gap) == (steps, outer, gap), i
+        assert s.duality_gap < pars.tolSolver
+        print(f"instance {i} (n={specs[i]['a0'].shape[0]}): {steps} Newton steps, {outer} centerings, gap {gap:.2e}")
     for e in engs:
         e.close()
 
