@@ -110,8 +110,8 @@ def kl_primal_spec(n: int, kind: str = "kl_1") -> Dict[str, np.ndarray]:
       equality sum(x) = 1 (Constraints.sumToOne); A = {0, 1, 2}, B = {n/2, .., n-1};
     * kl_2 (:271-320): the positivity rows, equalities 1'x = 1, P(A) = 0.36, P(B) = 0.1 (probEq.addEqualities(e1)
       .addEqualities(e2)).
-    x0 is strictly feasible for the inequalities (P(A) = 0.39, P(B) = 0.09 for kl_1; the known optimum, which has
-    every x_j > 0, for kl_2); x_opt = kl1_ / kl2_analyticSolution (:136-141, 249-251, n > 15)."""
+    x0 is strictly feasible for the inequalities (P(A) = 0.39, P(B) = 0.09 for kl_1; a positive perturbation of the
+    known optimum with sum 1 for kl_2); x_opt = kl1_ / kl2_analyticSolution (:136-141, 249-251, n > 15)."""
     assert n > 9 and n % 2 == 0
     j = np.arange(n)
     I_A = (j < 3).astype(float)
@@ -127,7 +127,10 @@ def kl_primal_spec(n: int, kind: str = "kl_1") -> Dict[str, np.ndarray]:
     elif kind == "kl_2":
         Aeq = np.vstack([np.ones(n), I_A, I_B])
         beq = np.array([1.0, 0.36, 0.1])
-        x0 = x_opt.copy()
+        # the known optimum is the whole central path (its gradient lies in the row space of Aeq), so start off it:
+        # a positive perturbation that keeps sum(x) = 1 but not the expectation equalities
+        x0 = x_opt * (1.0 + 0.25 * np.sin(1.7 * j + 0.3))
+        x0 = x0 / np.sum(x0)
     else:
         raise ValueError(kind)
     return dict(id=f"{kind}(n={n})", a0=np.zeros(n), r0=0.0, P=None, A=A, r=r, ub=ub, Aeq=Aeq, beq=beq, x0=x0,

@@ -1243,13 +1243,16 @@ def test_batch_full_size_contexts_share_one_gpu(mods):
     pars.maxIter = 30  # at most 30 Newton steps per centering keeps the 13 centerings of each C3 solve within seconds
     specs = [Z.random_qp(4096, 8192, instance=i) for i in (0, 1)] + [Z.random_qp(600, 1200, instance=70 + i)
                                                                      for i in (0, 1)]
-    fields = ("step", "backtracks_c", "backtracks_armijo", "q", "f", "ruiz_sweeps", "regularized", "min_diag")
+    fields = ("step", "backtracks_c", "backtracks_armijo", "q", "f", "ruiz_sweeps", "regularized", "min_diag", "iter")
     ref = []
     for spec in specs:
         e = _engine(Engine, spec)
         e.set_x(spec["x0"])
         e.centering_begin(1.0)
-        steps = [tuple(getattr(e.newton_step(pars), f) for f in fields) for _ in range(2)]
+        steps = []
+        for _ in range(2):
+            info = e.newton_step(pars)
+            steps.append(tuple(getattr(info, f) for f in fields))
         x2 = e.get_x()
         e.set_x(spec["x0"])
         s = e.barrier_solve(pars, 0)
