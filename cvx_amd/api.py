@@ -403,6 +403,48 @@ class ConstraintSet:
         x_feas, s_feas = w[:n], float(w[n])
         return FeasibilityReport(x_feas, [s_feas], s_feas < 0.0, cs, 0.0)
 
+    def phase_I_Analysis_SOI(self, eqs: Optional[EqualityConstraint], pars: SolverParams) -> FeasibilityReport:
+        """phase_I_Analysis_SOI (ConstraintSet.scala:503-535), the sum-of-infeasibilities method on the engine:
+        u = (x, s_1..s_p), objective sum(s) (phase_I_SOI_ObjectiveFunction, :233-248), rows (a_j, -e_j) with r_j, ub_j
+        (Constraint.phase_I_SOI, Constraint.scala:101-123; a quadratic member's P padded with zeros for s) followed by
+        the rows -s_j <= 0 (:147-158, sparse rows on the engine), feasible point (x0, max(0.5, 1 + g_j(x0) - ub_j))
+        (:262-269), equalities [A | 0] (EqualityConstraint.phase_I_SOI_EqualityConstraint, :50-55); solved by
+        BarrierSolver.solve, the standard termination (:481-490, 512).  The report keeps the reference's
+        isStrictlySatisfied expression, (0 until n).forall(j => s_feas(j) < 0) && eqError < tolSolver."""
+        A, r, ub = self.packed()
+        p, n = A.shape
+        x0 = self.pointWhereDefined
+        A1 = np.zeros((2 * p, n + p))
+        A1[:p, :n] = A
+        A1[np.arange(p), n + np.arange(p)] = -1.0
+        A1[p + np.arange(p), n + np.arange(p)] = -1.0
+        a0 = np.concatenate([np.zeros(n), np.ones(p)])
+        s0 = np.array([max(0.5, 1 + self.constraints[j].valueAt(x0) - self.constraints[j].ub) for j in range(p)])
+        u0 = np.concatenate([x0, s0])
+        qrows, qP = self.quadratic()
+        neq = 0 if eqs is None else eqs.A.shape[0]
+        eng = Engine(n + p, 2 * p, neq)
+        try:
+            eng.set_objective(a0, 0.0, None)
+            eng.set_ineq(A1, np.concatenate([r, np.zeros(p)]), np.concatenate([ub, np.zeros(p)]))
+            if qrows is not None:
+                qP1 = np.zeros((len(qrows), n + p, n + p))
+                qP1[:, :n, :n] = qP
+                eng.set_quad(qrows, qP1)
+            if neq:
+                eng.set_eq(np.hstack([eqs.A, np.zeros((neq, p))]), eqs.b)
+            sol = barrier_t_loop(eng, lambda u: float(np.sum(u[n:])), 2 * p, neq > 0,
+                                 CvxUtils.standardTerminationCriterion(pars), pars, u0)
+        finally:
+            eng.close()
+        w = sol.x
+        x_feas, s_feas = w[:n], w[n:]
+        eq_err = None if eqs is None else eqs.errorAt(x_feas)
+        strict = all(s_feas[j] < 0 for j in range(n)) and (0.0 if eq_err is None else eq_err) < pars.tolSolver
+        report = FeasibilityReport(x_feas, s_feas, strict, self, eq_err)
+        report.solution = sol
+        return report
+
     def withFeasiblePoint(self, eqs: Optional[EqualityConstraint], pars: SolverParams) -> "ConstraintSet":
         """ConstraintSet.scala:556-575: phase I, InfeasibleProblemException unless the report is feasible at
         pars.tolSolver."""
@@ -568,8 +610,8 @@ class BarrierSolver:
 class GpuPrimalDualSolver:
     """PrimalDualSolver (PrimalDualSolver.scala:18-460) on the MI355X engine: each iteration's KKT matrix, its
     SymmetricLinearSystem solve, dlambda and the residual line-search trials run on the device
-    (cvxg_pd_solve).  Quadratic or linear objective, LinearConstraint list, no equality constraints (the
-    reference's solve_withEQs is not built, see include/cvxg.h)."""
+    (cvxg_pd_solve).  Quadratic or linear objective, LinearConstraint and QuadraticConstraint members, no equality
+    constraints (the reference's solve_withEQs is not built, see include/cvxg.h)."""
 
     def __init__(self, objF: ObjectiveFunction, cnts: ConstraintSet, eqs: Optional[EqualityConstraint],
                  pars: SolverParams, device: int = 0):
@@ -577,8 +619,6 @@ class GpuPrimalDualSolver:
             raise TypeError("GPU primal-dual engine: objective must be Quadratic- or LinearObjectiveFunction")
         if eqs is not None:
             raise TypeError("GPU primal-dual engine: equality constraints are not supported (solve_withEQs)")
-        if cnts.quadratic()[0] is not None:
-            raise TypeError("GPU primal-dual engine: LinearConstraint only")
         if cnts.feasiblePoint is None:
             raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
         self.objF, self.cnts, self.eqs, self.pars = objF, cnts, eqs, pars
@@ -589,6 +629,9 @@ class GpuPrimalDualSolver:
         self.engine = Engine(cnts.dim, A.shape[0], 0, device)
         self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
         self.engine.set_ineq(A, r, ub)
+        qrows, qP = cnts.quadratic()
+        if qrows is not None:  # kktMatrix_noEqs adds grad2_gi * lambda_i (PrimalDualSolver.scala:224-238)
+            self.engine.set_quad(qrows, qP)
 
     def solve(self, debugLevel: int = 0) -> Solution:
         """PrimalDualSolver.solve (:628-633): standard criterion gap < tol and |r_dual| < tol."""

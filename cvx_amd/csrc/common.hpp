@@ -59,6 +59,8 @@ enum {
   SC_KLP,       // KL primal objective x . log(n x) at x (Dist_KL.scala:223-227)
   SC_KLPA,      // its error scale sum_j |x_j log(n x_j)| + |x_j|
   SC_TR_KLP,    // the KL primal objective at a fresh trial point xt
+  SC_KLA,       // KL dual: sum_j y_j (|B'||z|)_j, the error scale of its exponents at z
+  SC_TR_KLSUM,  // KL dual: sum_j R exp(-(B'zt)_j) at a fresh trial point zt
   SC_COUNT
 };
 static_assert(SC_COUNT <= 40, "DevCtrl::sc too small");

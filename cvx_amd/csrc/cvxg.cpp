@@ -48,6 +48,8 @@ struct cvxg_ctx {
   double kl_R = 0.0;
   double *KB = nullptr, *kl_v = nullptr, *kl_y = nullptr, *kl_u = nullptr, *kl_negBy = nullptr;
   double *kl_part = nullptr, *kl_ls = nullptr;
+  // certified line search of the KL dual: |B'||z|, |B'||s|; a fresh trial point's B'zt and y
+  double *kl_vabs = nullptr, *kl_uabs = nullptr, *kl_vtr = nullptr, *kl_ytr = nullptr;
   // KL primal objective (cvxg_set_objective_kl_primal): f0 = x . log(n x), its gradient and diag(1/x) Hessian
   int klp = 0;
   double klp_n = 0.0;
@@ -103,9 +105,13 @@ struct cvxg_ctx {
   std::vector<char> is_quad;     // per constraint row
   int *qrows = nullptr, *qslot = nullptr;  // device: row of constraint k, its row in As
   double *Pq = nullptr, *qPx = nullptr, *qPs = nullptr, *qextra = nullptr, *qf = nullptr;
+  // certified line search of quadratic rows: |P_k||x|, |P_k||s| (stacked), the band's t^2 term per row, and a fresh
+  // trial point's P_k xt and xt'P_k xt / 2
+  double *qPxa = nullptr, *qPsa = nullptr, *qfabs = nullptr, *qPx_tr = nullptr, *qextra_tr = nullptr;
   // primal-dual solver state (PrimalDualSolver.scala; allocated on first use)
   double *lam = nullptr, *dlam = nullptr, *pd_rc = nullptr, *pd_w = nullptr;  // mp
-  double *pd_rhs = nullptr, *pd_d1 = nullptr, *pd_R0 = nullptr, *pd_R1 = nullptr, *pd_tmp = nullptr;  // np
+  double *pd_rhs = nullptr, *pd_d1 = nullptr, *pd_R0 = nullptr, *pd_R1 = nullptr, *pd_R2 = nullptr;  // np
+  double* pd_tmp = nullptr;
   double *pd_part_rows = nullptr, *pd_part_cols = nullptr, *pd_out = nullptr, *pd_hout = nullptr;
   // symSolve / kktSymSolve fallback buffers (allocated on first use; ldm = round_up(n + p, 128))
   int eig_ldm = 0;
@@ -451,19 +457,22 @@ static double objective_from_ctrl(const cvxg_ctx* ctx, const DevCtrl& h) {
 
 // c = g(x), d, 1/d, 1/d^2, log d at ctx->x; QuadraticConstraint rows add x'P_k x / 2 (P_k x kept in qPx for the
 // gradient, the Hessian rows and the line search).
-// Certified line-search decisions cover linear constraints with a linear / quadratic objective (the configs of
-// BASELINE.json); QuadraticConstraint rows and the KL dual keep the plain trial arithmetic.
-static bool ls_certified(const cvxg_ctx* ctx) { return ctx->m > 0 && ctx->nq == 0 && !ctx->kl; }
+// Certified line-search decisions (line_search): every configuration with inequality constraints -- linear and
+// QuadraticConstraint rows, quadratic / linear / KL objectives.
+static bool ls_certified(const cvxg_ctx* ctx) { return ctx->m > 0; }
 
 static void constraint_eval_all(cvxg_ctx* ctx) {
   const int np = ctx->np;
+  const bool cert = ls_certified(ctx);
   if (ctx->nq > 0) {
-    launch_rowdot(ctx->s, ctx->Pq, np, ctx->nq * np, np, ctx->x, ctx->qPx);
+    if (cert) launch_rowdot_abs(ctx->s, ctx->Pq, np, ctx->nq * np, np, ctx->x, ctx->qPx, ctx->qPxa);
+    else launch_rowdot(ctx->s, ctx->Pq, np, ctx->nq * np, np, ctx->x, ctx->qPx);
     launch_quad_xpx(ctx->s, ctx->qPx, ctx->x, ctx->qrows, ctx->nq, np, ctx->qextra);
   }
   launch_constraint_eval(ctx->s, ctx->A, np, ctx->mp, np, ctx->x, ctx->r, ctx->ub, ctx->c, ctx->d, ctx->invd, ctx->w,
-                         ctx->logd, ctx->ctrl, ctx->nq > 0 ? ctx->qextra : nullptr,
-                         ls_certified(ctx) ? ctx->cabs : nullptr);
+                         ctx->logd, ctx->ctrl, ctx->nq > 0 ? ctx->qextra : nullptr, cert ? ctx->cabs : nullptr);
+  if (cert && ctx->nq > 0)  // + |x|'|P_k||x| / 2 on the quadratic rows
+    launch_quad_absdot(ctx->s, ctx->qPxa, ctx->x, ctx->qrows, ctx->nq, np, 0.5, 1, ctx->cabs);
 }
 
 // Barrier value / gradient pieces at the current x and ctrl->t (BarrierSolver.scala:280-301):
@@ -480,7 +489,8 @@ static int eval_at_x(cvxg_ctx* ctx) {
     else launch_rowdot(s, ctx->P, np, np, np, ctx->x, ctx->Px);
   }
   if (ctx->kl) {  // v = B'z, y = R exp(-v), -B y (the KL dual gradient is w - B y), sum_j y_j
-    launch_rowdot(s, ctx->KB, np, ctx->noutp, np, ctx->x, ctx->kl_v);
+    if (cert) launch_rowdot_abs(s, ctx->KB, np, ctx->noutp, np, ctx->x, ctx->kl_v, ctx->kl_vabs);
+    else launch_rowdot(s, ctx->KB, np, ctx->noutp, np, ctx->x, ctx->kl_v);
     launch_kl_eval(s, ctx->kl_v, ctx->nout, ctx->noutp, ctx->kl_R, ctx->kl_y);
     launch_coldot_partials(s, ctx->KB, np, ctx->noutp, np, ctx->kl_y, ctx->kl_part);
     launch_sum_chunks(s, ctx->kl_part, coldot_chunks(ctx->noutp), np, ctx->kl_negBy);
@@ -508,6 +518,7 @@ static int eval_at_x(cvxg_ctx* ctx) {
     db.add(DOT_ABS, ctx->a0, ctx->x, np, SC_A0XA);
     if (quad) db.add(DOT_ABS, ctx->x, ctx->Pxa, np, SC_XPXA);
     if (ctx->klp) db.add(DOT_SUM, ctx->klp_ab, nullptr, np, SC_KLPA);
+    if (ctx->kl) db.add(DOT_ABS, ctx->kl_y, ctx->kl_vabs, ctx->noutp, SC_KLA);
     db.add(DOT_ABS, ctx->cabs, ctx->invd, mp, SC_CAINV);
     db.add(DOT_ABS, ctx->logd, nullptr, mp, SC_LOGABS);
   }
@@ -533,9 +544,10 @@ static int eval_at_x(cvxg_ctx* ctx) {
 
 static double objective_at_x(cvxg_ctx* ctx) { return objective_from_ctrl(ctx, *ctx->hctrl); }
 
-// H = t P + A' diag(wts) A (+ the sparse rows' entries); wts = ctx->w = 1/d^2 for the barrier Hessian, or the
-// primal-dual KKT weights lambda/d (then ctrl->t = 1).
-static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr) {
+// H = t P + A' diag(wts) A (+ the sparse rows' entries) + sum_k qw_k P_k over the QuadraticConstraint rows; wts =
+// ctx->w = 1/d^2 and qw = 1/d for the barrier Hessian (BarrierSolver.scala:314), or the primal-dual KKT weights
+// lambda/d and qw = lambda (kktMatrix_noEqs, PrimalDualSolver.scala:226-238; then ctrl->t = 1).
+static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr, const double* qw = nullptr) {
   tstart(ctx, 5);
   const double* wsrc = wts ? wts : ctx->w;
   // full tiles in whole waves of workgroup slots, then the leftover tiles split along K across all slots
@@ -571,8 +583,8 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr) {
                          ctx->part, Pd);
   if (ctx->have_sparse)
     launch_sparse_hess(ctx->s, ctx->sp_ptr, ctx->sp_pq, ctx->sp_row, ctx->sp_coef, wsrc, ctx->sp_T, ctx->H, ctx->np);
-  if (ctx->nq > 0)  // + hessianAt/d = P_k / d_k  (BarrierSolver.scala:314)
-    launch_quad_hess(ctx->s, ctx->Pq, ctx->invd, ctx->qrows, ctx->nq, ctx->np, ctx->H);
+  if (ctx->nq > 0)  // + hessianAt/d = P_k / d_k  (BarrierSolver.scala:314), or grad2_gi * l_i (PrimalDualSolver.scala:236)
+    launch_quad_hess(ctx->s, ctx->Pq, qw ? qw : ctx->invd, ctx->qrows, ctx->nq, ctx->np, ctx->H);
   tstop(ctx, 5);
   HIPC(ctx, hipGetLastError());
   return CVXG_OK;
@@ -1003,8 +1015,12 @@ static double ls_gamma(const cvxg_ctx* ctx) { return 4.0 * (ctx->np + 16) * U53;
 // or the KL primal's (x + s t).log(n (x + s t)) with its error scale; copied into b->kl / b->kla on the stream.
 static int ls_objective_trials(cvxg_ctx* ctx, double tbase, double beta, TrialBatch* b) {
   if (ctx->kl) {
-    launch_ls_kl(ctx->s, ctx->kl_v, ctx->kl_u, ctx->nout, ctx->kl_R, tbase, beta, ctx->kl_part, ctx->kl_ls);
+    const bool cert = ls_certified(ctx);
+    launch_ls_kl(ctx->s, ctx->kl_v, ctx->kl_u, ctx->nout, ctx->kl_R, tbase, beta, ctx->kl_part, ctx->kl_ls,
+                 cert ? ctx->kl_vabs : nullptr, cert ? ctx->kl_uabs : nullptr, ls_gamma(ctx));
     HIPC(ctx, hipMemcpyAsync(b->kl, ctx->kl_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
+    HIPC(ctx, hipMemcpyAsync(b->kla, ctx->kl_ls + LS_TRIALS, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost,
+                             ctx->s));
   } else if (ctx->klp) {
     launch_ls_klp(ctx->s, ctx->x, ctx->sdir, ctx->n, ctx->klp_n, tbase, beta, ctx->klp_part, ctx->klp_ls);
     HIPC(ctx, hipMemcpyAsync(b->kl, ctx->klp_ls, LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
@@ -1030,7 +1046,7 @@ static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch
   const bool cert = ls_certified(ctx);
   launch_ls_trials(ctx->s, ctx->c, ctx->e, ctx->ub, ctx->m, tbase, beta, ctx->ls_plog, ctx->ls_pcnt,
                    ctx->nq > 0 ? ctx->qf : nullptr, cert ? ctx->cabs : nullptr, ctx->eabs, ls_gamma(ctx),
-                   ctx->ls_paux);
+                   ctx->ls_paux, (cert && ctx->nq > 0) ? ctx->qfabs : nullptr);
   launch_ls_finalize(ctx->s, ctx->ls_plog, ctx->ls_pcnt, ctx->ls_paux, nb, ctx->ls_log, ctx->ls_cnt);
   HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipMemcpyAsync(ctx->hls, ctx->ls_log, 3 * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
@@ -1064,8 +1080,12 @@ static int trial_fresh(cvxg_ctx* ctx, double tt, FreshTrial* out) {
   const int np = ctx->np, mp = ctx->mp;
   launch_axpy(s, ctx->x, ctx->sdir, tt, np, ctx->xtr);  // x + s*t (contraction off: two roundings, as Breeze)
   launch_ctrl_reset_eval(s, ctx->ctrl);
+  if (ctx->nq > 0) {  // QuadraticConstraint.valueAt(xt): r + a.xt + xt.(P xt)/2
+    launch_rowdot(s, ctx->Pq, np, ctx->nq * np, np, ctx->xtr, ctx->qPx_tr);
+    launch_quad_xpx(s, ctx->qPx_tr, ctx->xtr, ctx->qrows, ctx->nq, np, ctx->qextra_tr);
+  }
   launch_constraint_eval(s, ctx->A, np, mp, np, ctx->xtr, ctx->r, ctx->ub, ctx->c_tr, ctx->d_tr, ctx->invd_tr, ctx->w_tr,
-                         ctx->logd_tr, ctx->ctrl, nullptr, nullptr);
+                         ctx->logd_tr, ctx->ctrl, ctx->nq > 0 ? ctx->qextra_tr : nullptr, nullptr);
   launch_sum(s, ctx->logd_tr, mp, ctx->ctrl, SC_TR_SUMLOG);
   launch_dot(s, ctx->a0, ctx->xtr, np, ctx->ctrl, SC_TR_A0X);
   const bool quad = ctx->hasP && !ctx->kl;
@@ -1077,10 +1097,17 @@ static int trial_fresh(cvxg_ctx* ctx, double tt, FreshTrial* out) {
     launch_klp_eval(s, ctx->xtr, ctx->n, np, ctx->klp_n, ctx->klp_lxt, nullptr, nullptr, nullptr);
     launch_dot(s, ctx->xtr, ctx->klp_lxt, np, ctx->ctrl, SC_TR_KLP);
   }
+  if (ctx->kl) {  // -dualObjFAt(zt) = w.zt + R.exp(-B'zt)  (Dist_KL.scala:146-147, Duality.scala:76)
+    launch_rowdot(s, ctx->KB, np, ctx->noutp, np, ctx->xtr, ctx->kl_vtr);
+    launch_kl_eval(s, ctx->kl_vtr, ctx->nout, ctx->noutp, ctx->kl_R, ctx->kl_ytr);
+    launch_sum(s, ctx->kl_ytr, ctx->noutp, ctx->ctrl, SC_TR_KLSUM);
+  }
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
   const DevCtrl& h = *ctx->hctrl;
-  const double f0 = ctx->klp ? h.sc[SC_TR_KLP] : ctx->r0 + h.sc[SC_TR_A0X] + (quad ? h.sc[SC_TR_XPX] / 2 : 0.0);
+  const double f0 = ctx->klp  ? h.sc[SC_TR_KLP]
+                    : ctx->kl ? h.sc[SC_TR_A0X] + h.sc[SC_TR_KLSUM]
+                              : ctx->r0 + h.sc[SC_TR_A0X] + (quad ? h.sc[SC_TR_XPX] / 2 : 0.0);
   out->fv = ctx->t * f0 - h.sc[SC_TR_SUMLOG];
   out->viol = h.not_strict;
   out->npos = h.infeasible;
@@ -1113,10 +1140,18 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
     else launch_rowdot(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e);
   }
   if (ctx->nq > 0) {  // e_k = G_k.s and f_k = s'P_k s: g_k(x + t s) = g_k + t e_k + t^2 f_k / 2
-    launch_rowdot(s, ctx->Pq, ctx->np, ctx->nq * ctx->np, ctx->np, ctx->sdir, ctx->qPs);
+    if (cert) launch_rowdot_abs(s, ctx->Pq, ctx->np, ctx->nq * ctx->np, ctx->np, ctx->sdir, ctx->qPs, ctx->qPsa);
+    else launch_rowdot(s, ctx->Pq, ctx->np, ctx->nq * ctx->np, ctx->np, ctx->sdir, ctx->qPs);
     launch_quad_ls(s, ctx->qPx, ctx->qPs, ctx->sdir, ctx->qrows, ctx->nq, ctx->np, ctx->e, ctx->qf);
+    if (cert) {  // eabs += |s|'|P_k||x|, fabs = |s|'|P_k||s|
+      launch_quad_absdot(s, ctx->qPxa, ctx->sdir, ctx->qrows, ctx->nq, ctx->np, 1.0, 1, ctx->eabs);
+      launch_quad_absdot(s, ctx->qPsa, ctx->sdir, ctx->qrows, ctx->nq, ctx->np, 1.0, 0, ctx->qfabs);
+    }
   }
-  if (ctx->kl) launch_rowdot(s, ctx->KB, ctx->np, ctx->noutp, ctx->np, ctx->sdir, ctx->kl_u);  // u = B's
+  if (ctx->kl) {  // u = B's (and |B'||s|)
+    if (cert) launch_rowdot_abs(s, ctx->KB, ctx->np, ctx->noutp, ctx->np, ctx->sdir, ctx->kl_u, ctx->kl_uabs);
+    else launch_rowdot(s, ctx->KB, ctx->np, ctx->noutp, ctx->np, ctx->sdir, ctx->kl_u);
+  }
   if (quad) {
     if (cert) launch_rowdot_abs(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps, ctx->Psa);
     else launch_rowdot(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps);
@@ -1149,15 +1184,18 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
   };
   // error bounds (certified mode) of the objective part at x + s tt and of the barrier value f at x
   const double gam = ls_gamma(ctx);
-  // (klabs: the KL primal's error scale at the trial point; the KL dual's terms are not certified)
-  auto ef0_at = [&](double tt, double klabs) {
-    if (ctx->klp) return gam * klabs;
+  // error bound of f0 at x + s tt; klerr: the KL objectives' own term (the KL primal's error scale at the trial point,
+  // or the KL dual's exponent error already scaled, k_ls_kl)
+  auto ef0_at = [&](double tt, double klerr) {
+    if (ctx->klp) return gam * klerr;
+    if (ctx->kl) return gam * (h.sc[SC_A0XA] + tt * h.sc[SC_A0SA]) + klerr;
     double v = fabs(ctx->r0) + h.sc[SC_A0XA] + tt * h.sc[SC_A0SA];
     if (quad) v += (h.sc[SC_XPXA] + 2 * tt * h.sc[SC_SPXA] + tt * tt * h.sc[SC_SPSA]) / 2;
     return gam * v;
   };
-  const double ef_x = tb * ef0_at(0.0, h.sc[SC_KLPA]) + 2.0 * gam * h.sc[SC_CAINV] +
-                      (ctx->mp + 8) * U53 * h.sc[SC_LOGABS] + 8 * U53 * fabs(f);
+  const double klerr_x = ctx->klp ? h.sc[SC_KLPA] : gam * h.sc[SC_KLA] + 4 * U53 * h.sc[SC_KLSUM];
+  const double ef_x = tb * ef0_at(0.0, klerr_x) + 2.0 * gam * h.sc[SC_CAINV] + (ctx->mp + 8) * U53 * h.sc[SC_LOGABS] +
+                      8 * U53 * fabs(f);
   TrialBatch b;
   double tcur = 1.0;
   double tbatch = 1.0;  // t at the start of the next batch (products of beta, UnconstrainedSolver.scala:93)
@@ -1380,11 +1418,13 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,
                   ctx->kl_negBy, ctx->kl_part, ctx->kl_ls, ctx->As, ctx->wd, ctx->didx, ctx->sp_ptr,
                   ctx->sp_pq, ctx->sp_row, ctx->sp_coef, ctx->kl_spart, ctx->lam, ctx->dlam, ctx->pd_rc,
-                  ctx->pd_w, ctx->pd_rhs, ctx->pd_d1, ctx->pd_R0, ctx->pd_R1, ctx->pd_tmp, ctx->pd_part_rows,
+                  ctx->pd_w, ctx->pd_rhs, ctx->pd_d1, ctx->pd_R0, ctx->pd_R1, ctx->pd_R2, ctx->pd_tmp, ctx->pd_part_rows,
                   ctx->pd_part_cols, ctx->pd_out, ctx->qrows, ctx->qslot, ctx->Pq, ctx->qPx, ctx->qPs,
                   ctx->qextra, ctx->qf, ctx->aff_F, ctx->aff_z0, ctx->ls_paux, ctx->cabs, ctx->eabs, ctx->Pxa,
                   ctx->Psa, ctx->xtr, ctx->Pxtr, ctx->c_tr, ctx->d_tr, ctx->invd_tr, ctx->w_tr, ctx->logd_tr,
-                  ctx->klp_lx, ctx->klp_g0, ctx->klp_hd, ctx->klp_ab, ctx->klp_lxt, ctx->klp_part, ctx->klp_ls};
+                  ctx->klp_lx, ctx->klp_g0, ctx->klp_hd, ctx->klp_ab, ctx->klp_lxt, ctx->klp_part, ctx->klp_ls,
+                  ctx->kl_vabs, ctx->kl_uabs, ctx->kl_vtr, ctx->kl_ytr, ctx->qPxa, ctx->qPsa, ctx->qfabs, ctx->qPx_tr,
+                  ctx->qextra_tr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->kY, (void*)ctx->kR, (void*)ctx->kS, (void*)ctx->kzp, (void*)ctx->kinfo})
@@ -1430,14 +1470,16 @@ int cvxg_set_objective_kl(cvxg_ctx* ctx, const double* B, int ldB, int row_major
   if (ldB < (row_major ? nout : n)) return set_err(ctx, CVXG_E_DIM, "ldB too small");
   const int noutp = round_up(nout, MPAD);
   if (noutp != ctx->noutp) {
-    for (double** v : {&ctx->KB, &ctx->kl_v, &ctx->kl_y, &ctx->kl_u, &ctx->kl_negBy, &ctx->kl_part, &ctx->kl_ls})
+    for (double** v : {&ctx->KB, &ctx->kl_v, &ctx->kl_y, &ctx->kl_u, &ctx->kl_negBy, &ctx->kl_part, &ctx->kl_ls,
+                       &ctx->kl_vabs, &ctx->kl_uabs, &ctx->kl_vtr, &ctx->kl_ytr})
       if (*v) (void)hipFree(*v), *v = nullptr;
     CHK(dalloc(ctx, &ctx->KB, (size_t)noutp * np));
-    for (double** v : {&ctx->kl_v, &ctx->kl_y, &ctx->kl_u}) CHK(dalloc(ctx, v, noutp));
+    for (double** v : {&ctx->kl_v, &ctx->kl_y, &ctx->kl_u, &ctx->kl_vabs, &ctx->kl_uabs, &ctx->kl_vtr, &ctx->kl_ytr})
+      CHK(dalloc(ctx, v, noutp));
     CHK(dalloc(ctx, &ctx->kl_negBy, np));
     CHK(dalloc(ctx, &ctx->kl_part, std::max((size_t)coldot_chunks(noutp) * np,
-                                            (size_t)((noutp + 255) / 256) * LS_TRIALS)));
-    CHK(dalloc(ctx, &ctx->kl_ls, LS_TRIALS));
+                                            (size_t)ls_kl_blocks(noutp) * 2 * LS_TRIALS)));
+    CHK(dalloc(ctx, &ctx->kl_ls, 2 * LS_TRIALS));
   }
   // KB = B' (nout x n): B row-major (ldB) is B' column-major with the same ld, and vice versa
   CHK(upload_mat(ctx, ctx->KB, np, noutp, B, nout, n, ldB, row_major ? 0 : 1));
@@ -1610,7 +1652,8 @@ int cvxg_set_quad(cvxg_ctx* ctx, int q, const int* rows, const double* P, int ld
     if (rs[k] < 0 || rs[k] >= m) return set_err(ctx, CVXG_E_DIM, "quadratic constraint row %d out of range", rs[k]);
     if (k > 0 && rs[k] <= rs[k - 1]) return set_err(ctx, CVXG_E_ARG, "quadratic constraint rows must ascend");
   }
-  for (double** v : {&ctx->Pq, &ctx->qPx, &ctx->qPs, &ctx->qextra, &ctx->qf})
+  for (double** v : {&ctx->Pq, &ctx->qPx, &ctx->qPs, &ctx->qextra, &ctx->qf, &ctx->qPxa, &ctx->qPsa, &ctx->qfabs,
+                     &ctx->qPx_tr, &ctx->qextra_tr})
     if (*v) (void)hipFree(*v), *v = nullptr;
   if (ctx->qrows) (void)hipFree(ctx->qrows), ctx->qrows = nullptr;
   ctx->nq = q;
@@ -1627,6 +1670,9 @@ int cvxg_set_quad(cvxg_ctx* ctx, int q, const int* rows, const double* P, int ld
     CHK(dalloc(ctx, &ctx->qPs, (size_t)q * np));
     CHK(dalloc(ctx, &ctx->qextra, ctx->mp));  // zero on the linear rows
     CHK(dalloc(ctx, &ctx->qf, ctx->mp));
+    for (double** v : {&ctx->qPxa, &ctx->qPsa, &ctx->qPx_tr}) CHK(dalloc(ctx, v, (size_t)q * np));
+    CHK(dalloc(ctx, &ctx->qextra_tr, ctx->mp));
+    CHK(dalloc(ctx, &ctx->qfabs, ctx->mp));
   }
   // re-split the rows (quadratic rows are dense SYRK rows with a changing gradient): A back from the device
   std::vector<double> hA((size_t)ctx->mp * np);
@@ -1995,12 +2041,12 @@ static int pd_check(cvxg_ctx* ctx) {
                    "the no-equality system, PrimalDualSolver.scala:284)");
   if (ctx->kl || ctx->klp)
     return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: quadratic or linear objective only");
-  if (ctx->nq > 0) return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: linear constraints only");
   if (ctx->m == 0) return set_err(ctx, CVXG_E_ARG, "primal-dual solver needs inequality constraints");
   if (ctx->lam) return CVXG_OK;
   const size_t np = ctx->np, mp = ctx->mp;
   for (double** v : {&ctx->lam, &ctx->dlam, &ctx->pd_rc, &ctx->pd_w}) CHK(dalloc(ctx, v, mp));
-  for (double** v : {&ctx->pd_rhs, &ctx->pd_d1, &ctx->pd_R0, &ctx->pd_R1, &ctx->pd_tmp}) CHK(dalloc(ctx, v, np));
+  for (double** v : {&ctx->pd_rhs, &ctx->pd_d1, &ctx->pd_R0, &ctx->pd_R1, &ctx->pd_R2, &ctx->pd_tmp})
+    CHK(dalloc(ctx, v, np));
   CHK(dalloc(ctx, &ctx->pd_part_rows, (size_t)pd_row_blocks(ctx->m) * 2 * LS_TRIALS));
   CHK(dalloc(ctx, &ctx->pd_part_cols, (size_t)((ctx->n + 255) / 256) * LS_TRIALS));
   CHK(dalloc(ctx, &ctx->pd_out, 3 * LS_TRIALS));
@@ -2008,10 +2054,12 @@ static int pd_check(cvxg_ctx* ctx) {
   return CVXG_OK;
 }
 
-// grad f(x) + A' v into out (the dual residual, :63-71); Px must hold P x (eval_at_x)
+// grad f(x) + Dg' v into out (the dual residual, :63-71): A' v, plus sum_k (P_k x) v_k over the QuadraticConstraint
+// rows (their gradients a_k + P_k x; qPx from eval_at_x).  Px must hold P x.
 static void pd_dual_residual(cvxg_ctx* ctx, const double* v, const double* a0, const double* Pv, double* out) {
   launch_coldot_partials(ctx->s, ctx->A, ctx->np, ctx->mp, ctx->np, v, ctx->part);
   launch_pd_finalize(ctx->s, a0, Pv, ctx->part, coldot_chunks(ctx->mp), ctx->np, out);
+  if (ctx->nq > 0) launch_quad_grad(ctx->s, ctx->qPx, v, ctx->qrows, ctx->nq, ctx->np, out);
 }
 
 // Search direction at (t, ctx->x, ctx->lam) into ctx->dx / ctx->dlam (PrimalDualSolver.scala:421-425).
@@ -2023,7 +2071,7 @@ static int pd_direction_dev(cvxg_ctx* ctx, const cvxg_params* pars, double t, cv
   launch_pd_rhs(s, ctx->y, t, n, np, ctx->pd_rhs);                       // rhs1 = -y / t        (:162-176)
   launch_pd_weights(s, ctx->lam, ctx->d, ctx->m, ctx->mp, ctx->pd_w);    // lambda_i / d_i      (:226-238)
   launch_ctrl_set(s, ctx->ctrl, 0, 1.0);                                 // hpd starts at objF.hessianAt(x)
-  CHK(assemble_hessian(ctx, ctx->pd_w));
+  CHK(assemble_hessian(ctx, ctx->pd_w, ctx->lam));
   launch_ctrl_set(s, ctx->ctrl, 0, t);
   ctx->x_eval_valid = 0;  // y is reused below as the rhs of the shared choleskySolve
   // SymmetricLinearSystem: d1 = Ruiz(H), Q = (d1 d1') o H, s = d1 o r (SymmetricLinearSystem.scala:20-23).  Q is
@@ -2056,8 +2104,13 @@ static int pd_direction_dev(cvxg_ctx* ctx, const cvxg_params* pars, double t, cv
     HIPC(ctx, hipMemcpyAsync(ctx->dx, ctx->eig_x, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
   }
   launch_scale_vec(s, ctx->dx, ctx->pd_d1, np, ctx->dx);  // x = d :* u  (:54)
-  // deltaLambda (:184-209) with the step bound s0 and the central residual at (x, lambda)
+  // deltaLambda (:184-209) with the step bound s0 and the central residual at (x, lambda); w = Dg dx (for a
+  // QuadraticConstraint row (a + P x).dx, with f = dx'P dx kept for the line-search trials)
   launch_rowdot(s, ctx->A, np, ctx->mp, np, ctx->dx, ctx->e);
+  if (ctx->nq > 0) {
+    launch_rowdot(s, ctx->Pq, np, ctx->nq * np, np, ctx->dx, ctx->qPs);
+    launch_quad_ls(s, ctx->qPx, ctx->qPs, ctx->dx, ctx->qrows, ctx->nq, np, ctx->e, ctx->qf);
+  }
   launch_pd_reset_s0(s, ctx->ctrl);
   launch_pd_dlambda(s, ctx->c, ctx->ub, ctx->lam, ctx->e, t, ctx->m, ctx->mp, ctx->dlam, ctx->pd_rc, ctx->ctrl);
   HIPC(ctx, hipGetLastError());
@@ -2073,6 +2126,11 @@ static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg
   pd_dual_residual(ctx, ctx->lam, ctx->a0, Px, ctx->pd_R0);                      // r_dual(x, lambda)
   if (ctx->hasP) launch_rowdot(s, ctx->P, np, np, np, ctx->dx, ctx->pd_tmp);     // P dx
   pd_dual_residual(ctx, ctx->dlam, nullptr, ctx->hasP ? ctx->pd_tmp : nullptr, ctx->pd_R1);
+  if (ctx->nq > 0) {  // Dg(x + s dx)'(l + s dl): + s sum_k (P_k dx) l_k, + s^2 sum_k (P_k dx) dl_k
+    launch_quad_grad(s, ctx->qPs, ctx->lam, ctx->qrows, ctx->nq, np, ctx->pd_R1);
+    HIPC(ctx, hipMemsetAsync(ctx->pd_R2, 0, (size_t)np * sizeof(double), s));
+    launch_quad_grad(s, ctx->qPs, ctx->dlam, ctx->qrows, ctx->nq, np, ctx->pd_R2);
+  }
   launch_dot(s, ctx->pd_R0, nullptr, np, ctx->ctrl, SC_RES2);
   launch_dot(s, ctx->pd_rc, nullptr, ctx->mp, ctx->ctrl, SC_RES2B);
   HIPC(ctx, hipGetLastError());
@@ -2090,7 +2148,8 @@ static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg
   double sK = 0.0;
   while (K < 0) {
     launch_pd_trials(s, ctx->c, ctx->e, ctx->ub, ctx->lam, ctx->dlam, ctx->m, ctx->pd_R0, ctx->pd_R1, ctx->n, sbase,
-                     beta, t, ctx->pd_part_rows, ctx->pd_part_cols, ctx->pd_out);
+                     beta, t, ctx->pd_part_rows, ctx->pd_part_cols, ctx->pd_out, ctx->nq > 0 ? ctx->qf : nullptr,
+                     ctx->nq > 0 ? ctx->pd_R2 : nullptr);
     HIPC(ctx, hipGetLastError());
     CHK(copy_sync(ctx, ctx->pd_hout, ctx->pd_out, 3 * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost));
     double sk = sbase;

@@ -104,12 +104,13 @@ void launch_pd_finalize(hipStream_t s, const double* a0, const double* Pv, const
 
 // Line-search trials (:344-368) along s_k = s_base beta^k (repeated products): per trial, over the constraint
 // rows, the number failing g_i(x + s dx) (1 + 3e-16) < ub_i (Constraint.scala:23) and the sum of squares of the
-// central residual -(l + s dl)(g - ub) - 1/t; g(x + s dx) = c + s (A dx) since g is affine.  Per-block
-// partials, [block][trial][2] as doubles, summed in a fixed order by k_sum_chunks.
+// central residual -(l + s dl)(g - ub) - 1/t; g(x + s dx) = c + s (G dx) (+ s^2 dx'P dx / 2 for a QuadraticConstraint
+// row, f != NULL).  Per-block partials, [block][trial][2] as doubles, summed in a fixed order by k_sum_chunks.
 __global__ __launch_bounds__(256) void k_pd_trials_rows(const double* __restrict__ c, const double* __restrict__ e,
                                                         const double* __restrict__ ub, const double* __restrict__ lam,
                                                         const double* __restrict__ dlam, int m, double sbase,
-                                                        double beta, double t, double* __restrict__ part) {
+                                                        double beta, double t, double* __restrict__ part,
+                                                        const double* __restrict__ f) {
   __shared__ double scent[4][LS_TRIALS];
   __shared__ int sviol[4][LS_TRIALS];
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -117,9 +118,10 @@ __global__ __launch_bounds__(256) void k_pd_trials_rows(const double* __restrict
   const bool valid = i < m;
   const double ci = valid ? c[i] : 0.0, ei = valid ? e[i] : 0.0, ubi = valid ? ub[i] : 1.0;
   const double li = valid ? lam[i] : 0.0, dli = valid ? dlam[i] : 0.0;
+  const double fi = (valid && f) ? f[i] : 0.0;
   double s = sbase;
   for (int k = 0; k < LS_TRIALS; ++k) {
-    const double g = ci + s * ei;
+    const double g = f ? (ci + s * ei) + (s * s * fi) / 2 : ci + s * ei;
     const bool viol = valid && !(g * (1 + 3e-16) < ubi);
     const double r = -(li + s * dli) * (g - ubi) - 1.0 / t;
     const double sc = wave_sum(valid ? r * r : 0.0);
@@ -137,17 +139,19 @@ __global__ __launch_bounds__(256) void k_pd_trials_rows(const double* __restrict
     part[((size_t)blockIdx.x * LS_TRIALS + k) * 2 + 1] = (double)(sviol[0][k] + sviol[1][k] + sviol[2][k] + sviol[3][k]);
   }
 }
-// ... and over the variables, the dual residual grad f(x_s) + A' l_s = R0 + s R1 (both affine in s).
+// ... and over the variables, the dual residual grad f(x_s) + Dg(x_s)' l_s = R0 + s R1 (+ s^2 R2 with
+// QuadraticConstraint rows, whose gradients a + P x_s move with the step).
 __global__ __launch_bounds__(256) void k_pd_trials_cols(const double* __restrict__ R0, const double* __restrict__ R1,
-                                                        int n, double sbase, double beta, double* __restrict__ part) {
+                                                        int n, double sbase, double beta, double* __restrict__ part,
+                                                        const double* __restrict__ R2) {
   __shared__ double sd[4][LS_TRIALS];
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool valid = j < n;
-  const double r0 = valid ? R0[j] : 0.0, r1 = valid ? R1[j] : 0.0;
+  const double r0 = valid ? R0[j] : 0.0, r1 = valid ? R1[j] : 0.0, r2 = (valid && R2) ? R2[j] : 0.0;
   double s = sbase;
   for (int k = 0; k < LS_TRIALS; ++k) {
-    const double v = r0 + s * r1;
+    const double v = R2 ? (r0 + s * r1) + (s * s) * r2 : r0 + s * r1;
     const double sv = wave_sum(v * v);
     if (lane == 0) sd[wid][k] = sv;
     s *= beta;
@@ -162,10 +166,10 @@ int pd_row_blocks(int m) { return m > 0 ? (m + 255) / 256 : 1; }
 // out[0 .. 2 LS_TRIALS): (central sum of squares, violations) per trial; out[2 LS_TRIALS ..): dual sum of squares
 void launch_pd_trials(hipStream_t s, const double* c, const double* e, const double* ub, const double* lam,
                       const double* dlam, int m, const double* R0, const double* R1, int n, double sbase, double beta,
-                      double t, double* part_rows, double* part_cols, double* out) {
+                      double t, double* part_rows, double* part_cols, double* out, const double* f, const double* R2) {
   const int br = pd_row_blocks(m), bc = (n + 255) / 256;
-  k_pd_trials_rows<<<br, 256, 0, s>>>(c, e, ub, lam, dlam, m, sbase, beta, t, part_rows);
-  k_pd_trials_cols<<<bc, 256, 0, s>>>(R0, R1, n, sbase, beta, part_cols);
+  k_pd_trials_rows<<<br, 256, 0, s>>>(c, e, ub, lam, dlam, m, sbase, beta, t, part_rows, f);
+  k_pd_trials_cols<<<bc, 256, 0, s>>>(R0, R1, n, sbase, beta, part_cols, R2);
   launch_sum_chunks(s, part_rows, br, 2 * LS_TRIALS, out);
   launch_sum_chunks(s, part_cols, bc, LS_TRIALS, out + 2 * LS_TRIALS);
 }

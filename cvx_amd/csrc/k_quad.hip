@@ -90,4 +90,21 @@ void launch_quad_ls(hipStream_t s, const double* qPx, const double* qPs, const d
   k_quad_ls<<<(nq + 3) / 4, 256, 0, s>>>(qPx, qPs, sdir, qrows, nq, np, e, f);
 }
 
+// Error scales of the certified line search for QuadraticConstraint rows (k_ls_trials): out[row_k] (+)= scale *
+// |v|.M_k for the stacked |P_k| products M (|P_k||x| or |P_k||s|), one wave per constraint.
+__global__ __launch_bounds__(256) void k_quad_absdot(const double* __restrict__ M, const double* __restrict__ v,
+                                                     const int* __restrict__ qrows, int nq, int np, double scale,
+                                                     int accumulate, double* __restrict__ out) {
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (k >= nq) return;
+  double s = 0.0;
+  for (int j = lane; j < np; j += 64) s = fma(fabs(v[j]), M[(size_t)k * np + j], s);
+  s = wave_sum(s) * scale;
+  if (lane == 0) out[qrows[k]] = accumulate ? out[qrows[k]] + s : s;
+}
+void launch_quad_absdot(hipStream_t s, const double* M, const double* v, const int* qrows, int nq, int np, double scale,
+                        int accumulate, double* out) {
+  k_quad_absdot<<<(nq + 3) / 4, 256, 0, s>>>(M, v, qrows, nq, np, scale, accumulate, out);
+}
+
 }  // namespace cvxg

@@ -481,7 +481,9 @@ int ls_blocks(int m) { return (m + 255) / 256; }
 
 // Certified decisions (cabs != nullptr): the trial value c_i + t e_i and the reference's fresh evaluation
 // r_i + a_i.(x + s t) both lie within B_i(t) = gamma (cabs_i + t eabs_i) of the exact g_i(x + s t), with cabs_i = |r_i|
-// + |a_i|.|x|, eabs_i = |a_i|.|s| and gamma = 4 (n + 16) u.  A constraint whose feasibility margin is inside that
+// + |a_i|.|x|, eabs_i = |a_i|.|s| and gamma = 4 (n + 16) u.  A QuadraticConstraint row (g = c + t e + t^2 f / 2 with
+// e = (a + P x).s, f = s'P s) adds |x|'|P||x|/2 to cabs, |s|'|P||x| to eabs and the band term t^2 fabs / 2 with
+// fabs = |s|'|P||s| (the expansion of |x + s t|'|P||x + s t| / 2).  A constraint whose feasibility margin is inside that
 // band counts as ambiguous (the host then evaluates that trial fresh); per trial the kernel also sums the first-
 // order bound of the log-sum error, sum_i (B_i + 4u(|g_i| + |ub_i|)) / d_i, and sum_i |log d_i| (+inf when some
 // B_i is not small against d_i).
@@ -490,7 +492,7 @@ __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c,
                                                    double* __restrict__ part_log, int* __restrict__ part_cnt,
                                                    const double* __restrict__ f, const double* __restrict__ cabs,
                                                    const double* __restrict__ eabs, double gamma,
-                                                   double* __restrict__ part_aux) {
+                                                   double* __restrict__ part_aux, const double* __restrict__ fabsq) {
   // blockIdx.y = group of LS_GROUP consecutive trials (more workgroups than ceil(m/256) alone)
   constexpr int LS_GROUP = 8;
   constexpr double U = 1.1102230246251565e-16;  // 2^-53
@@ -504,6 +506,7 @@ __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c,
   const double fi = (valid && f) ? f[i] : 0.0;  // s'P s of a QuadraticConstraint row (0: linear)
   const bool cert = cabs != nullptr;
   const double ca = (valid && cert) ? cabs[i] : 0.0, ea = (valid && cert) ? eabs[i] : 0.0;
+  const double fa = (valid && cert && fabsq) ? fabsq[i] : 0.0;
   double t = tbase;
   for (int q = 0; q < k0; ++q) t *= beta;  // the same product chain as trial by trial
   for (int kk = 0; kk < LS_GROUP; ++kk) {
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c,
     bool sure = false, amb = false;
     double lerr = 0.0, labs = 0.0;
     if (valid && cert) {
-      const double band = gamma * (ca + t * ea);
+      const double band = fabsq ? gamma * ((ca + t * ea) + (t * t * fa) / 2) : gamma * (ca + t * ea);
       const double bt = band * (1 + 3e-16) + 4 * U * (fabs(g) + fabs(ubi));
       const double margin = gs - ubi;  // >= 0: violated
       sure = margin > bt;
@@ -567,38 +570,50 @@ __global__ __launch_bounds__(256) void k_ls_trials(const double* __restrict__ c,
 
 void launch_ls_trials(hipStream_t s, const double* c, const double* e, const double* ub, int m, double tbase,
                       double beta, double* part_log, int* part_cnt, const double* f, const double* cabs,
-                      const double* eabs, double gamma, double* part_aux) {
+                      const double* eabs, double gamma, double* part_aux, const double* fabsq) {
   k_ls_trials<<<dim3(ls_blocks(m), LS_TRIALS / 8), 256, 0, s>>>(c, e, ub, m, tbase, beta, part_log, part_cnt, f, cabs,
-                                                                eabs, gamma, part_aux);
+                                                                eabs, gamma, part_aux, fabsq);
 }
 
 // KL dual objective along the trial steps: per trial k, sum_j R exp(-(v_j + t_k u_j)) (v = B'z, u = B's),
 // the vec_R dot exp(-B'(z + s t)) term of Dist_KL.dualObjFAt (Dist_KL.scala:146-147); t_k by repeated products.
+// With vabs / uabs (= |B'||z|, |B'||s|; certified mode) also its error scale against any evaluation order of
+// B'(z + s t): sum_j y_j (gamma (vabs_j + t_k uabs_j) + 4u) (the exponent's error propagated through exp).
 __global__ __launch_bounds__(256) void k_ls_kl(const double* __restrict__ v, const double* __restrict__ u, int nout,
-                                               double R, double tbase, double beta, double* __restrict__ part) {
-  __shared__ double sred[4][LS_TRIALS];
+                                               double R, double tbase, double beta, double* __restrict__ part,
+                                               const double* __restrict__ vabs, const double* __restrict__ uabs,
+                                               double gamma) {
+  constexpr double U = 1.1102230246251565e-16;  // 2^-53
+  __shared__ double sred[2][4][LS_TRIALS];
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool valid = j < nout;
   const double vj = valid ? v[j] : 0.0, uj = valid ? u[j] : 0.0;
+  const double va = (valid && vabs) ? vabs[j] : 0.0, ua = (valid && uabs) ? uabs[j] : 0.0;
   double t = tbase;
   for (int k = 0; k < LS_TRIALS; ++k) {
     const double y = valid ? R * exp(-(vj + t * uj)) : 0.0;
-    const double sw = wave_sum(y);
-    if (lane == 0) sred[wid][k] = sw;
+    const double ye = vabs ? y * (gamma * (va + t * ua) + 4 * U) : 0.0;
+    const double sw = wave_sum(y), se = wave_sum(ye);
+    if (lane == 0) {
+      sred[0][wid][k] = sw;
+      sred[1][wid][k] = se;
+    }
     t *= beta;
   }
   __syncthreads();
-  if (threadIdx.x < LS_TRIALS) {
-    const int k = threadIdx.x;
-    part[(size_t)blockIdx.x * LS_TRIALS + k] = ((sred[0][k] + sred[1][k]) + sred[2][k]) + sred[3][k];
+  if (threadIdx.x < 2 * LS_TRIALS) {
+    const int q = threadIdx.x / LS_TRIALS, k = threadIdx.x % LS_TRIALS;
+    part[(size_t)blockIdx.x * 2 * LS_TRIALS + q * LS_TRIALS + k] =
+        ((sred[q][0][k] + sred[q][1][k]) + sred[q][2][k]) + sred[q][3][k];
   }
 }
+int ls_kl_blocks(int nout) { return (nout + 255) / 256; }
 void launch_ls_kl(hipStream_t s, const double* v, const double* u, int nout, double R, double tbase, double beta,
-                  double* part, double* out) {
-  const int nb = (nout + 255) / 256;
-  k_ls_kl<<<nb, 256, 0, s>>>(v, u, nout, R, tbase, beta, part);
-  k_sum_chunks<<<1, LS_TRIALS, 0, s>>>(part, nb, LS_TRIALS, out);
+                  double* part, double* out, const double* vabs, const double* uabs, double gamma) {
+  const int nb = ls_kl_blocks(nout);
+  k_ls_kl<<<nb, 256, 0, s>>>(v, u, nout, R, tbase, beta, part, vabs, uabs, gamma);
+  k_sum_chunks<<<1, 2 * LS_TRIALS, 0, s>>>(part, nb, 2 * LS_TRIALS, out);
 }
 
 // KL primal objective Dist_KL.objectiveFunction(n) (Dist_KL.scala:223-239) at x, per coordinate j < n:

@@ -92,6 +92,9 @@ void launch_quad_hess(hipStream_t s, const double* Pq, const double* invd, const
                       double* H);
 void launch_quad_ls(hipStream_t s, const double* qPx, const double* qPs, const double* sdir, const int* qrows, int nq,
                     int np, double* e, double* f);
+// out[row_k] (+)= scale * |v|.M_k (M: the stacked |P_k| v products of k_rowdot_abs)
+void launch_quad_absdot(hipStream_t s, const double* M, const double* v, const int* qrows, int nq, int np, double scale,
+                        int accumulate, double* out);
 
 // ---- primal-dual iteration pieces (k_pd.hip) ---------------------------------------------------------
 void launch_pd_rhs(hipStream_t s, const double* y, double t, int n, int np, double* rhs);
@@ -105,9 +108,12 @@ void launch_pd_finalize(hipStream_t s, const double* a0, const double* Pv, const
 int pd_row_blocks(int m);
 void launch_pd_lambda0(hipStream_t s, const double* invd, int m, int mp, double* lam);
 void launch_pd_reset_s0(hipStream_t s, DevCtrl* ctrl);
+// f (QuadraticConstraint rows: dx'P dx per row, 0 on linear rows) and R2 (the s^2 term of the dual residual) may be
+// NULL when every constraint is linear.
 void launch_pd_trials(hipStream_t s, const double* c, const double* e, const double* ub, const double* lam,
                       const double* dlam, int m, const double* R0, const double* R1, int n, double sbase, double beta,
-                      double t, double* part_rows, double* part_cols, double* out);
+                      double t, double* part_rows, double* part_cols, double* out, const double* f = nullptr,
+                      const double* R2 = nullptr);
 
 // ---- MFMA SYRK (k_syrk.hip) -----------------------------------------------------------------------
 // H = t*P + A' diag(w) A over the lower tile list; split-K when nsplit > 1 (partials + ordered reduce).
@@ -133,16 +139,19 @@ void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* L
 // (#violations of g*(1+3e-16)<ub, #(ub-g<=0), sum log(ub-g)).
 // With cabs / eabs (|r| + |a|.|x|, |a|.|s|) the trials also report sure / ambiguous violation counts and the log-sum
 // error bound (certified decisions, see k_vec.hip); part_aux: 2 doubles per (block, trial).
+// fabsq (certified mode, QuadraticConstraint rows): |s|'|P||s| per row (0 on linear rows), the t^2 term of the band.
 void launch_ls_trials(hipStream_t s, const double* c, const double* e, const double* ub, int m, double tbase,
                       double beta, double* part_log, int* part_cnt, const double* f, const double* cabs,
-                      const double* eabs, double gamma, double* part_aux);
+                      const double* eabs, double gamma, double* part_aux, const double* fabsq = nullptr);
 void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_cnt, const double* part_aux,
                         int nblocks, double* out_log, int* out_cnt);
 int ls_blocks(int m);
 // KL dual objective (Dist_KL.scala:146-170): y = R exp(-v) (masked padding); trial sums of R exp(-(v + t_k u))
 void launch_kl_eval(hipStream_t s, const double* v, int nout, int noutp, double R, double* y);
+// out[k] = the trial sums, out[LS_TRIALS + k] = their error scales (vabs / uabs NULL: zeros)
+int ls_kl_blocks(int nout);
 void launch_ls_kl(hipStream_t s, const double* v, const double* u, int nout, double R, double tbase, double beta,
-                  double* part, double* out);
+                  double* part, double* out, const double* vabs, const double* uabs, double gamma);
 
 // KL primal objective (Dist_KL.scala:223-239): lx = log(n x), g0 = gradient, hd = diag of the Hessian, ab = error
 // scale of the value terms (each output may be NULL but lx)

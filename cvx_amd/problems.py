@@ -137,6 +137,52 @@ def kl_primal_spec(n: int, kind: str = "kl_1") -> Dict[str, np.ndarray]:
                 klp_n=n, x_opt=x_opt, x_where_defined=np.full(n, 1.0 / n))
 
 
+def random_constraint_set(x0: np.ndarray, p: int, q: int, instance: int = 0, neq: int = 0) -> Dict[str, np.ndarray]:
+    """ConstraintSets.randomConstraintSet (ConstraintSets.scala:67-89), seeded: p linear rows a'(x - x0) <= e, a ~
+    U[-1,1]^n, e = 0.1 + 0.1 U (Constraints.randomLinearIneqConstraint / linearIneqConstraint, Constraints.scala:158-171:
+    r = -a.x0), then q quadratic rows ||R(x - x0)||^2 / 2 <= e, R ~ U[-1,1]^(n x n), e = 0.2 (1 + U)
+    (randomQuadraticIneqConstraint / quadraticIneqConstraint, :177-200: P = R'R, a = -R'R x0, r = ||R x0||^2 / 2);
+    pointWhereDefined u = 0.  neq > 0 adds Constraints.randomEqualityConstraint(x0, neq) (:207-214): A ~ U[-1,1],
+    b = A x0.  The objective is left to the caller (a0 = 0)."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 7919 + instance))
+    x0 = np.asarray(x0, dtype=np.float64)
+    n = x0.shape[0]
+    A, r, ub, qP = [], [], [], []
+    for _ in range(p):
+        e = 0.1 + 0.1 * rng.uniform()
+        a = rng.uniform(-1.0, 1.0, n)
+        A.append(a), r.append(-(a @ x0)), ub.append(e)
+    for _ in range(q):
+        e = 0.2 * (1 + rng.uniform())
+        R = rng.uniform(-1.0, 1.0, (n, n))
+        Rx0 = R @ x0
+        nr = np.linalg.norm(Rx0)
+        A.append(-(R.T @ Rx0)), r.append(nr * nr / 2), ub.append(e)
+        qP.append(R.T @ R)
+    spec = dict(id=f"randomConstraintSet(n={n},p={p},q={q},instance={instance})", a0=np.zeros(n), r0=0.0, P=None,
+                A=np.array(A), r=np.array(r), ub=np.array(ub), Aeq=None, beq=None,
+                qrows=np.arange(p, p + q, dtype=np.int32) if q else None, qP=np.array(qP) if q else None,
+                x_where_defined=np.zeros(n), x_feasible=x0.copy())
+    if neq:
+        Aeq = rng.uniform(-1.0, 1.0, (neq, n))
+        spec.update(Aeq=Aeq, beq=Aeq @ x0)
+    return spec
+
+
+def prob_ab(n: int, pA: float, sgnA: float, pB: float, sgnB: float) -> Dict[str, np.ndarray]:
+    """ConstraintSets.probAB (ConstraintSets.scala:39-60) with A = {0, 1, 2}, B = {n/2, .., n-1} (FeasibilityTests.
+    runAll, FeasibilityTests.scala:117-124): rows sgnB P(B) <= sgnB pB, sgnA P(A) <= sgnA pA (expectation_lt_r), then
+    allCoordinatesPositive; pointWhereDefined 1/n; the equality sum(x) = 1 (Constraints.sumToOne)."""
+    j = np.arange(n)
+    I_A = (j < 3).astype(float)
+    I_B = (j >= n // 2).astype(float)
+    Ap, rp, ubp = _positivity(n)
+    A = np.vstack([I_B * sgnB, I_A * sgnA, Ap])
+    Aeq, beq = _sum_to_one(n)
+    return dict(id=f"probAB(n={n})", a0=np.zeros(n), r0=0.0, P=None, A=A, r=np.zeros(n + 2),
+                ub=np.concatenate([[pB * sgnB, pA * sgnA], ubp]), Aeq=Aeq, beq=beq, x_where_defined=np.full(n, 1.0 / n))
+
+
 def _positivity(n: int):
     """Constraints.allCoordinatesPositive (Constraints.scala:26-69): -x_j <= 0, j = 0..n-1."""
     return -np.eye(n), np.zeros(n), np.zeros(n)

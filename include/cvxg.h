@@ -136,8 +136,9 @@ int cvxg_set_ineq(cvxg_ctx* ctx, const double* A, int ldA, int row_major, const 
 /* QuadraticConstraint(id, dim, ub, r, a, P): r + a.x + x'P x / 2 <= ub (QuadraticConstraint.scala:8-40).  Row
  * rows[k] (ascending) of the cvxg_set_ineq list holds its (a, r, ub); P_k is the n x n row-major block at
  * P + k n ldP (symmetric).  Call after cvxg_set_ineq (which clears the quadratic rows).  The barrier path
- * (value, gradient a + P x, Hessian terms G G'/d^2 + P/d, line search) handles them; the primal-dual solver
- * returns CVXG_E_UNSUPPORTED. */
+ * (value, gradient a + P x, Hessian terms G G'/d^2 + P/d, line search) and the primal-dual solver (KKT matrix
+ * terms G G' lambda/d + lambda P, PrimalDualSolver.scala:224-238; gradients a + P x in rhs1, the dual residual and
+ * dlambda) handle them. */
 int cvxg_set_quad(cvxg_ctx* ctx, int q, const int* rows, const double* P, int ldP);
 
 /* EqualityConstraint(A, b) (EqualityConstraint.scala:16). */
@@ -232,7 +233,8 @@ typedef struct cvxg_pd_solution {
 } cvxg_pd_solution;
 
 /* The primal-dual search direction at (t, x, lambda) (PrimalDualSolver.scala:216-261, 184-209): the KKT
- * matrix H_pd = hessian f + sum_i (lambda_i / -f_i) a_i a_i' (weighted SYRK), rhs1 = -grad f + sum_i a_i/(t f_i),
+ * matrix H_pd = hessian f + sum_i [lambda_i grad2 g_i + (lambda_i / -f_i) G_i G_i'] (weighted SYRK over the gradient
+ * rows G_i = a_i (+ P_i x), + lambda_k P_k), rhs1 = -grad f + sum_i G_i/(t f_i),
  * SymmetricLinearSystem(H_pd, rhs1).solve(tolEqSolve) (Ruiz, then choleskySolve with its own Ruiz, symSolve on any
  * failure), then dlambda.  lambda has m entries; dx (n) / dlambda (m) may be NULL.  No equality constraints. */
 int cvxg_pd_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, const double* lambda,

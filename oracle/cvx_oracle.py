@@ -26,6 +26,8 @@ What it is
                                                         CvxUtils.scala:61-87, SolverParams.scala:35-46
     * phase-I feasibility (linear constraints) ........ ConstraintSet.scala:123-168, 326-395, 556-575,
                                                         Constraint.scala:64-89, EqualityConstraint.scala:84-100
+    * sum-of-infeasibilities phase I ................. ConstraintSet.scala:233-275, 481-535,
+                                                        Constraint.scala:101-159, EqualityConstraint.scala:50-55
 
 Third-party arithmetic the reference reaches but does not vendor: Breeze 0.10 (`cholesky` = symmetry
 check + LAPACK dpotrf('L'); `eigSym` = LAPACK dsyevr), netlib-java 1.1.2 `LAPACK.dtrtrs`.  They are
@@ -891,6 +893,45 @@ def phase_I_analysis(pb: Problem, x_where_defined: np.ndarray, pars: SolverParam
     return sol.x[:n], float(sol.x[n])
 
 
+def phase_I_SOI_problem(pb: Problem, x_where_defined: np.ndarray) -> Tuple[Problem, np.ndarray]:
+    """The sum-of-infeasibilities phase-I problem in u = (x, s_1..s_p), p = number of constraints:
+    phase_I_SOI_ObjectiveFunction f(x, s) = sum(s) (ConstraintSet.scala:233-248); phase_I_SOI_Constraints
+    (ConstraintSet.scala:258-275 -> Constraint.phase_I_SOI_Constraints, Constraint.scala:101-159): row j = g_j(x) - s_j
+    <= ub_j (gradient (a_j, -e_j), a quadratic member's P in the x block), then the rows -s_j <= 0 in list order; the
+    feasible point (x0, s_j = max(0.5, 1 + g_j(x0) - ub_j)); equalities [A | 0] (EqualityConstraint.scala:50-55)."""
+    n, p = pb.n, pb.m
+    A1 = np.zeros((2 * p, n + p))
+    A1[:p, :n] = pb.A
+    A1[np.arange(p), n + np.arange(p)] = -1.0
+    A1[p + np.arange(p), n + np.arange(p)] = -1.0
+    r1 = np.concatenate([pb.r, np.zeros(p)])
+    ub1 = np.concatenate([pb.ub, np.zeros(p)])
+    a0 = np.concatenate([np.zeros(n), np.ones(p)])
+    s0 = np.array([max(0.5, 1 + constraint_value(pb, j, x_where_defined) - pb.ub[j]) for j in range(p)])
+    u0 = np.concatenate([x_where_defined, s0])
+    qP = None
+    if pb.qrows is not None:
+        qP = np.zeros((pb.qP.shape[0], n + p, n + p))
+        qP[:, :n, :n] = pb.qP
+    Aeq = None if pb.Aeq is None else np.hstack([pb.Aeq, np.zeros((pb.Aeq.shape[0], p))])
+    return Problem(a0=a0, r0=0.0, P=None, A=A1, r=r1, ub=ub1, Aeq=Aeq, beq=pb.beq, qrows=pb.qrows, qP=qP), u0
+
+
+def phase_I_analysis_soi(pb: Problem, x_where_defined: np.ndarray, pars: SolverParams):
+    """phase_I_Analysis_SOI (ConstraintSet.scala:503-535): the SOI barrier solver (phase_I_Solver_SOI, :481-490)
+    solved to the STANDARD termination (solver.solve), then x_feas = u[:n], s_feas = u[n:], the equality error
+    |A x_feas - b| and isStrictlySatisfied = (0 until n).forall(j => s_feas(j) < 0) && eqError < tolSolver -- the
+    reference's own expression (it ranges over n, not p; s_j > 0 keeps it false).  Returns (x_feas, s_feas,
+    isStrictlySatisfied, eqError or None, the barrier Solution)."""
+    pb1, u0 = phase_I_SOI_problem(pb, x_where_defined)
+    sol = barrier_solve(pb1, u0, pars)
+    n = pb.n
+    x_feas, s_feas = sol.x[:n], sol.x[n:]
+    eq_err = None if pb.Aeq is None else float(np.linalg.norm(pb.Aeq @ x_feas - pb.beq))
+    strict = all(s_feas[j] < 0 for j in range(n)) and (0.0 if eq_err is None else eq_err) < pars.tolSolver
+    return x_feas, s_feas, strict, eq_err, sol
+
+
 def with_feasible_point(pb: Problem, x_where_defined: np.ndarray, pars: SolverParams) -> np.ndarray:
     """ConstraintSet.withFeasiblePoint (:556-575): phase I, then a strictly feasible x0."""
     x_feas, s_feas = phase_I_analysis(pb, x_where_defined, pars)
@@ -1049,8 +1090,9 @@ def pd_kkt_matrix(pb: Problem, x: np.ndarray, lam: np.ndarray) -> np.ndarray:
         li = lam[i]
         fi = constraint_value(pb, i, x) - pb.ub[i]
         assert fi < 0, "line search did not pull back into strictly feasible region"
-        G = pb.A[i]
-        hpd = hpd + (np.zeros_like(hpd) * li - np.outer(G, G) * (li / fi))
+        G = constraint_gradient(pb, i, x)
+        Hq = constraint_hessian(pb, i)  # QuadraticConstraint.hessianAt = P; zeros for a LinearConstraint
+        hpd = hpd + ((Hq if Hq is not None else np.zeros_like(hpd)) * li - np.outer(G, G) * (li / fi))
     return hpd
 
 
@@ -1059,7 +1101,7 @@ def pd_rhs1(pb: Problem, t: float, x: np.ndarray) -> np.ndarray:
     res = -objective_gradient(pb, x)
     for i in range(pb.m):
         fx = constraint_value(pb, i, x) - pb.ub[i]
-        res = res + pb.A[i] / (t * fx)
+        res = res + constraint_gradient(pb, i, x) / (t * fx)
     return res
 
 
@@ -1070,8 +1112,11 @@ def pd_central_residual(pb: Problem, t: float, x: np.ndarray, lam: np.ndarray) -
 
 
 def pd_dual_residual(pb: Problem, x: np.ndarray, lam: np.ndarray) -> np.ndarray:
-    """:63-71 — grad f + Dg' lambda."""
-    return objective_gradient(pb, x) + pb.A.T @ lam
+    """:63-71 — grad f + Dg' lambda (Dg = ConstraintSet.gradientMatrixAt, the gradients G_i(x) in rows)."""
+    if pb.qrows is None:
+        return objective_gradient(pb, x) + pb.A.T @ lam
+    Dg = np.array([constraint_gradient(pb, i, x) for i in range(pb.m)])
+    return objective_gradient(pb, x) + Dg.T @ lam
 
 
 def pd_residual(pb: Problem, t: float, x: np.ndarray, lam: np.ndarray) -> np.ndarray:
@@ -1084,7 +1129,7 @@ def pd_delta_lambda(pb: Problem, t: float, x: np.ndarray, dx: np.ndarray, lam: n
     r_cent = pd_central_residual(pb, t, x, lam)
     gx = pd_constraint_function(pb, x)
     assert np.all(gx < 0), "line search did not pull back into strictly feasible region"
-    w = pb.A @ dx
+    w = pb.A @ dx if pb.qrows is None else np.array([constraint_gradient(pb, i, x) @ dx for i in range(pb.m)])
     return (-lam * w + r_cent) / gx
 
 

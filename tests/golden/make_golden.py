@@ -2,7 +2,7 @@
 
 The reference (Scala/Breeze) cannot run here, so these vectors are outputs of the
 restatement on seeded inputs; the restatement itself is pinned by the reference's known-answer tests
-(tests/test_oracle_known_answers.py).  Run:  python tests/golden/make_golden.py
+(tests/test_oracle_known_answers.py).  Run:  python tests/golden/make_golden.py [name ...]
 Each fixture: the packed problem + every inner Newton step of a full barrier solve
 (t, x, grad, f, dx, q, accepted step, backtrack counters, Ruiz sweeps, regularisation flag).
 """
@@ -21,12 +21,16 @@ from oracle import cvx_oracle as O  # noqa: E402
 
 
 def _problem(spec):
+    if spec.get("kl_B") is not None and np.size(spec["kl_R"]) == 1:  # vec_R = fill(n)(1/(n e)) (Dist_KL.scala:116)
+        spec = dict(spec, kl_R=np.full(spec["kl_B"].shape[1], float(np.ravel(spec["kl_R"])[0])))
     return O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"],
-                     Aeq=spec.get("Aeq"), beq=spec.get("beq"))
+                     Aeq=spec.get("Aeq"), beq=spec.get("beq"), qrows=spec.get("qrows"), qP=spec.get("qP"),
+                     kl_B=spec.get("kl_B"), kl_R=spec.get("kl_R"))
 
 
 def trajectory(spec, x0):
     pb = _problem(spec)
+    spec = dict(spec, kl_R=pb.kl_R)
     pars = O.standard_params()
     sol = O.barrier_solve(pb, x0, pars, record=True)
     recs = sol.records
@@ -43,10 +47,13 @@ def trajectory(spec, x0):
         out["P"] = spec["P"]
     if spec.get("Aeq") is not None:
         out["Aeq"], out["beq"] = spec["Aeq"], spec["beq"]
+    for k in ("qrows", "qP", "kl_B", "kl_R"):  # QuadraticConstraint rows; the KL dual objective
+        if spec.get(k) is not None:
+            out[k] = spec[k]
     return out
 
 
-def main():
+def main(names=None):
     pars = O.standard_params()
     fixtures = {}
     # dense QP, inequalities only (path A), n not a multiple of the 128 tile (padding)
@@ -76,10 +83,19 @@ def main():
     pbe = _problem(spec)
     x0 = O.with_feasible_point(pbe, spec["x_where_defined"], pars)
     fixtures["simplex_rank1_n10_p1"] = trajectory(spec, x0)
+    # QuadraticConstraint rows (QuadraticConstraint.scala:8-40) in the barrier path: the line search's quadratic
+    # trial expansion g + t e + t^2 f / 2 against the reference's fresh valueAt(x + s t)
+    spec = Z.random_qp_quad(30, 50, 3, instance=12)
+    fixtures["quad_n30_m50_q3"] = trajectory(spec, spec["x0"])
+    # the KL dual (Duality.dualProblem over Dist_KL, Duality.scala:99-112): exp terms in every trial
+    spec = Z.kl_dual_spec(300, 12, instance=3)
+    fixtures["kldual_n300_k12"] = trajectory(spec, spec["x0"])
     for name, fx in fixtures.items():
+        if names and name not in names:
+            continue
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **fx)
         print(name, {k: np.shape(v) for k, v in fx.items() if k in ("A", "x", "dx")}, "steps", int(fx["newton_steps"]))
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)
