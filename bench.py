@@ -196,13 +196,26 @@ def workload_spec(args, rank):
         workload = (f"C4: KL dual barrier (Dist_KL via Duality), {nout} outcomes, dual dimension {n}, {k} bound rows"
                     f", full barrier Newton iterations")
         return spec, n, m, syrk_rows, workload
+    if wl == "C4P":  # the direct KL solve: Dist_KL.objectiveFunction over kl_1's rows and sum(x) = 1 (KKT, p = 1)
+        n = args.n or 2048
+        spec = Z.kl_primal_spec(n, "kl_1")
+        m = spec["A"].shape[0]
+        workload = (f"C4P: KL primal barrier (Dist_KL.objectiveFunction, kl_1 rows: {n} positivity + 2 expectation "
+                    f"rows, sum(x) = 1), n = {n}, full barrier Newton iterations on the KKT path")
+        return spec, n, m, 2, workload
     n = args.n or (1024 if wl in ("C2", "C2PD") else 4096)
     m0 = args.m or (2048 if wl in ("C2", "C2PD") else 8192)
-    spec = Z.random_qp_bounds(n, m0, instance=rank) if wl == "C3B" else Z.random_qp(n, m0, instance=rank)
+    if wl == "C3B":
+        spec = Z.random_qp_bounds(n, m0, instance=rank)
+    elif wl == "C3EQ":  # KKTSystem.solve with p equality rows (p + 1 > 9: the wide Schur path)
+        spec = Z.random_qp_eq(n, m0, args.p, instance=rank)
+    else:
+        spec = Z.random_qp(n, m0, instance=rank)
     m = spec["A"].shape[0]
     syrk_rows = m0  # dense rows (the sparse rows' Hessian entries are per-entry sums, not SYRK work)
     workload = (f"{wl}: random dense QP n={n} m={m0}" + (f" plus {m - m0} sparse bound/difference rows"
                                                            if wl == "C3B" else "") +
+                (f" with {args.p} equality rows (KKT path)" if wl == "C3EQ" else "") +
                 (", primal-dual iterations (PrimalDualSolver: KKT-matrix SYRK + 2x Ruiz + Cholesky + solves + "
                  "residual line search)" if wl.endswith("PD") else
                  ", full barrier Newton iterations (assembly + Ruiz + Cholesky + solves + line search)") +
@@ -239,7 +252,8 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     spec, n, m, syrk_rows, workload = workload_spec(args, rank)
     pars = SolverParams.standardParams()
 
-    eng = engine_cls(n, m, 0, device=local_rank)
+    p_eq = 0 if spec.get("Aeq") is None else spec["Aeq"].shape[0]
+    eng = engine_cls(n, m, p_eq, device=local_rank)
     eng.load_problem(spec)
     eng.set_x(spec["x0"])
     state = {"t": 1.0}
@@ -376,10 +390,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C3B", "C4", "C2PD", "C3PD"],
+    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C3B", "C3EQ", "C4", "C4P", "C2PD", "C3PD"],
                     help="C3 (default, the metric's config): random dense QP n=4096 m=8192; C2: n=1024 m=2048; "
                          "C3B: C3 plus 9216 sparse bound / difference rows; C4: KL dual, 2048 outcomes, k=512; "
-                         "C2PD / C3PD: the primal-dual solver (solverType PD) on C2 / C3, steps = its KKT solves")
+                         "C2PD / C3PD: the primal-dual solver (solverType PD) on C2 / C3, steps = its KKT solves; "
+                         "C3EQ: C3 with --p equality rows (KKT path); C4P: the direct KL solve, n = 2048")
+    ap.add_argument("--p", type=int, default=64, help="equality rows of C3EQ")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--m", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -38,16 +38,32 @@ __device__ __forceinline__ double row_dot_wave(const double* __restrict__ row, c
 
 // a.v and |a|.|v| in one sweep (the abs dot bounds the rounding error of every evaluation order of a.v: the
 // line search's certified trial decisions, cvxg.cpp: line_search).
+// The same 4-sweeps-in-flight / two-accumulator structure as row_dot_wave, so a.v is bitwise row_dot_wave's.
 __device__ __forceinline__ double row_dot_wave_abs(const double* __restrict__ row, const double* __restrict__ v,
                                                    int cols, int lane, double* absdot) {
-  vd2 acc = {0.0, 0.0}, aab = {0.0, 0.0};
-  for (int j = 2 * lane; j < cols; j += 128) {
-    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), b0 = *reinterpret_cast<const vd2*>(v + j);
-    acc = __builtin_elementwise_fma(a0, b0, acc);
-    aab = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(b0), aab);
+  vd2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0}, aab0 = {0.0, 0.0}, aab1 = {0.0, 0.0};
+  int j = 2 * lane;
+  for (; j + 384 < cols; j += 512) {
+    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), a1 = *reinterpret_cast<const vd2*>(row + j + 128);
+    const vd2 a2 = *reinterpret_cast<const vd2*>(row + j + 256), a3 = *reinterpret_cast<const vd2*>(row + j + 384);
+    const vd2 b0 = *reinterpret_cast<const vd2*>(v + j), b1 = *reinterpret_cast<const vd2*>(v + j + 128);
+    const vd2 b2 = *reinterpret_cast<const vd2*>(v + j + 256), b3 = *reinterpret_cast<const vd2*>(v + j + 384);
+    acc0 = __builtin_elementwise_fma(a0, b0, acc0);
+    acc1 = __builtin_elementwise_fma(a1, b1, acc1);
+    acc0 = __builtin_elementwise_fma(a2, b2, acc0);
+    acc1 = __builtin_elementwise_fma(a3, b3, acc1);
+    aab0 = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(b0), aab0);
+    aab1 = __builtin_elementwise_fma(__builtin_elementwise_abs(a1), __builtin_elementwise_abs(b1), aab1);
+    aab0 = __builtin_elementwise_fma(__builtin_elementwise_abs(a2), __builtin_elementwise_abs(b2), aab0);
+    aab1 = __builtin_elementwise_fma(__builtin_elementwise_abs(a3), __builtin_elementwise_abs(b3), aab1);
   }
-  *absdot = wave_sum(aab[0] + aab[1]);
-  return wave_sum(acc[0] + acc[1]);
+  for (; j < cols; j += 128) {
+    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), b0 = *reinterpret_cast<const vd2*>(v + j);
+    acc0 = __builtin_elementwise_fma(a0, b0, acc0);
+    aab0 = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(b0), aab0);
+  }
+  *absdot = wave_sum((aab0[0] + aab0[1]) + (aab1[0] + aab1[1]));
+  return wave_sum((acc0[0] + acc0[1]) + (acc1[0] + acc1[1]));
 }
 
 __global__ __launch_bounds__(256) void k_constraint_eval(const double* __restrict__ A, int ld, int mp, int cols,
@@ -162,7 +178,8 @@ __global__ void k_gradient_finalize(const double* __restrict__ a0, const double*
   // objF.gradientAt(x) * t  (QuadraticObjectiveFunction.scala:32: a + P*x), then + sum_i a_i/d_i
   double g = (Px ? (a0[j] + Px[j]) : a0[j]) * t;
   double s = 0.0;
-  for (int c = 0; c < nchunks; ++c) s += part[(size_t)c * cols + j];
+#pragma unroll 16
+  for (int c = 0; c < nchunks; ++c) s += part[(size_t)c * cols + j];  // (loads in flight; the sum stays in order)
   y[j] = g + s;
 }
 
@@ -250,6 +267,7 @@ __global__ void k_sum_chunks(const double* __restrict__ part, int nchunks, int c
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cols) return;
   double s = 0.0;
+#pragma unroll 8
   for (int c = 0; c < nchunks; ++c) s += part[(size_t)c * cols + i];
   out[i] = s;
 }
@@ -705,7 +723,8 @@ __global__ void k_ls_finalize(const double* __restrict__ part_log, const int* __
   if (k >= LS_TRIALS) return;
   double s = 0.0, se = 0.0, sa = 0.0;
   int c4[4] = {0, 0, 0, 0};
-  for (int b = 0; b < nblocks; ++b) {
+#pragma unroll 8
+  for (int b = 0; b < nblocks; ++b) {  // (loads in flight; the sums stay in block order)
     const size_t o = (size_t)b * LS_TRIALS + k;
     s += part_log[o];
     se += part_aux[2 * o];

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Side workloads of bench.py (C2, C3B with and without the sparse-row split, C4), one line each into
+# Side workloads of bench.py (C2, C3B with and without the sparse-row split, C4, PD, C3EQ with p = 8 / 64, the
+# direct KL solve C4P), one line each into
 # gpurun_out/wl_<name>.json.  Each run has its own time limit; a fault or timeout ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -18,3 +19,6 @@ run C3B_dense CVXG_SPARSE_ROWS=0 python bench.py --workload C3B --no-cpu-baselin
 run C4 python bench.py --workload C4 --no-cpu-baseline --steps 50 --warmup 5
 run C2PD python bench.py --workload C2PD --no-cpu-baseline --steps 50
 run C3PD python bench.py --workload C3PD --no-cpu-baseline --steps 20
+run C3EQ8 python bench.py --workload C3EQ --p 8 --no-cpu-baseline --steps 10 --warmup 2
+run C3EQ64 python bench.py --workload C3EQ --p 64 --no-cpu-baseline --steps 10 --warmup 2
+run C4P python bench.py --workload C4P --no-cpu-baseline --steps 30 --warmup 3
