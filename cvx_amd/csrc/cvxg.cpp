@@ -65,10 +65,16 @@ struct cvxg_ctx {
   double *Px = nullptr, *Ps = nullptr, *e = nullptr;
   double *c = nullptr, *d = nullptr, *invd = nullptr, *w = nullptr, *logd = nullptr;
   double *eqd = nullptr, *eqtmp = nullptr;  // b - Aeq x
-  // wide KKT path (p + 1 > MAX_RHS): column-major [B' | Dq] -> X, R = B X, S, z; rocBLAS / rocSOLVER handle
-  double *kY = nullptr, *kR = nullptr, *kS = nullptr, *kzp = nullptr;
-  int* kinfo = nullptr;
-  void* blas = nullptr;
+  // KKT equality block (k_kkt.hip): X = Q^-1 [B' | Dq] in kY (np x kY_ld, row-major; the fused forward solve's rhs
+  // and the backward solve's sol buffers instead when p + 1 <= kkt_fused_rhs), R = B X partials, S / z, w
+  int kkt_fused_rhs = MAX_RHS;  // set at creation; CVXG_KKT_FUSED_RHS overrides (1: the many-column solves)
+  double *kY = nullptr, *kYg = nullptr, *kgram = nullptr, *kS = nullptr, *kzp = nullptr;
+  int kY_ld = 0, kY_chunks = 0, fm_gen = 0;
+  // p > 64: S factored by the dataflow Cholesky on its own buffers (pS = p rounded up to 64), w by its backward solve
+  double *sL = nullptr, *sLinv = nullptr, *sw = nullptr;
+  unsigned* s_tasks = nullptr;
+  int *s_work = nullptr, *s_bwd = nullptr;
+  int s_nblk = 0, s_ntasks = 0, s_gen = 0;
   // matrices
   double *H = nullptr, *L = nullptr, *Linv = nullptr, *Hsave = nullptr;
   double *ruiz0 = nullptr, *ruiz1 = nullptr, *dfin = nullptr, *hdiag = nullptr;
@@ -841,6 +847,9 @@ static int kkt_residual_check(cvxg_ctx* ctx, const double* qv, const double* bv,
   tstop(ctx, 3);
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
+  if (ctx->hctrl->df_status != 0)
+    return set_err(ctx, CVXG_E_HIP, "KKT Schur complement: dataflow dependency wait timed out (status %d)",
+                   ctx->hctrl->df_status);
   if (ctx->hctrl->chol_info != 0) return set_err(ctx, CVXG_E_NOT_PD, "KKT Schur complement not positive definite");
   auto relsize = [&](double na, double nb_) { return na / (nb_ < tol ? tol : tol + nb_); };
   const double err1 = relsize(sqrt(ctx->hctrl->sc[SC_RES2]), sqrt(ctx->hctrl->sc[SC_Q]));
@@ -851,13 +860,55 @@ static int kkt_residual_check(cvxg_ctx* ctx, const double* qv, const double* bv,
   return CVXG_OK;
 }
 
-// KKTSystem.solvePD(Hm, Aeq, q, b) (KKTSystem.scala:200-246) with the block elimination of
-// solveWithCholFactor (:99-167); Hm = ctx->H, q = qv (device n-vector), b = bv (device p-vector).
-// p + 1 <= MAX_RHS: the n x (p+1) right-hand side [B' | Dq] rides the factorization's fused forward solve and the
-// one-launch backward solve, and one workgroup forms and factors the p x p Schur complement (k_kkt_schur).
+// Lazily, once per context: the buffers of the equality block (k_kkt.hip) for this p.
+static int kkt_alloc(cvxg_ctx* ctx, bool fused) {
+  const int np = ctx->np, p = ctx->p, nr = p + 1;
+  if (!fused && !ctx->kY) {
+    ctx->kY_chunks = (nr + 15) / 16;
+    ctx->kY_ld = 16 * ctx->kY_chunks;
+    CHK(dalloc(ctx, &ctx->kY, (size_t)np * ctx->kY_ld));
+    HIPC(ctx, hipMemsetAsync(ctx->kY, 0, (size_t)np * ctx->kY_ld * sizeof(double), ctx->s));  // unused columns: 0
+    const size_t g = trsm_many_granule_doubles(ctx->nblk, ctx->kY_chunks);
+    CHK(dalloc(ctx, &ctx->kYg, g));
+    HIPC(ctx, hipMemsetAsync(ctx->kYg, 0, g * sizeof(double), ctx->s));
+  }
+  if (!ctx->kgram) {
+    CHK(dalloc(ctx, &ctx->kgram, schur_partial_doubles(np, p)));
+    if (p <= NB) {
+      CHK(dalloc(ctx, &ctx->kS, (size_t)p * p));
+      CHK(dalloc(ctx, &ctx->kzp, (size_t)p));
+    } else {  // the dataflow Cholesky of S on its own buffers
+      const int ps = round_up(p, NB);
+      ctx->s_nblk = ps / NB;
+      CHK(dalloc(ctx, &ctx->sL, (size_t)ps * ps));
+      HIPC(ctx, hipMemsetAsync(ctx->sL, 0, (size_t)ps * ps * sizeof(double), ctx->s));
+      CHK(dalloc(ctx, &ctx->sLinv, (size_t)ctx->s_nblk * NB * NB));
+      CHK(dalloc(ctx, &ctx->kzp, (size_t)ps));
+      CHK(dalloc(ctx, &ctx->sw, (size_t)ps));
+      std::vector<unsigned> order = chol_schedule(ctx->s_nblk, ctx->ncu);
+      ctx->s_ntasks = (int)order.size();
+      CHK(dalloc(ctx, &ctx->s_tasks, std::max<size_t>(order.size(), 1)));
+      if (!order.empty())
+        CHK(copy_sync(ctx, ctx->s_tasks, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+      CHK(dalloc(ctx, &ctx->s_work, chol_dataflow_work_ints(ctx->s_nblk)));
+      CHK(dalloc(ctx, &ctx->s_bwd, bwd_work_ints(ctx->s_nblk)));
+      HIPC(ctx, hipMemsetAsync(ctx->s_bwd, 0, bwd_work_ints(ctx->s_nblk) * sizeof(int), ctx->s));
+    }
+  }
+  return CVXG_OK;
+}
+
+// KKTSystem.solvePD(Hm, Aeq, q, b) (KKTSystem.scala:200-246) with the block elimination of solveWithCholFactor
+// (:99-167); Hm = ctx->H, q = qv (device n-vector), b = bv (device p-vector), on the factor L of Q = D Hm D
+// (k_kkt.hip), in the reference's sequence: X = Q^-1 [B' | Dq] -- the factorization's fused forward solve and the
+// one-launch backward solve when p + 1 <= MAX_RHS, otherwise the many-column dataflow solves with L and L' --,
+// R = B X (MFMA partials + a fixed-order reduction), S = (R + R')/2, z = -(b + R[:, p]), w = S^-1 z (one
+// workgroup for p <= 64, the dataflow Cholesky and backward solve beyond), y = -(X[:, p] + X[:, :p] w).
 static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
   hipStream_t s = ctx->s;
   const int n = ctx->n, np = ctx->np, p = ctx->p, nr = p + 1;
+  const bool fused = nr <= std::min(ctx->kkt_fused_rhs, MAX_RHS);
+  CHK(kkt_alloc(ctx, fused));
   tstart(ctx, 1);
   ruiz(ctx);
   tstop(ctx, 1);
@@ -865,10 +916,14 @@ static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, doubl
   int reg = 0;
   double mind = 0.0;
   int rc = regularized_cholesky(
-      ctx, nr,
+      ctx, fused ? nr : 1,
       [&]() {
-        launch_kkt_prep(s, ctx->Aeq, np, p, n, np, ctx->dfin, ctx->kB, ctx->rhs, nr);  // B = A diag(d), B'
-        launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, nr, p, ctx->rhs);            // D q
+        if (fused) {
+          launch_kkt_prep(s, ctx->Aeq, np, p, n, np, ctx->dfin, ctx->kB, ctx->rhs, nr);  // B = A diag(d), B'
+          launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, nr, p, ctx->rhs);            // D q
+        } else {
+          launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, 1, 0, ctx->rhs);
+        }
       },
       &reg, &mind, [] {});
   tstop(ctx, 2);
@@ -877,65 +932,39 @@ static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, doubl
   info->min_diag = mind;
   if (rc != CVXG_OK) return rc;
   tstart(ctx, 3);
-  backward_solve(ctx, nr);  // X = H^-1 [B' | Dq]
-  launch_ctrl_reset_chol(s, ctx->ctrl);
-  launch_kkt_schur(s, ctx->sol, nr, ctx->kB, np, p, np, bv, ctx->kw, ctx->kx, ctx->ctrl);
-  return kkt_residual_check(ctx, qv, bv, tol, info);
-}
-
-// The same for p + 1 > MAX_RHS (any number of equality rows): the factorization carries only Dq; the whole
-// [B' | Dq] (column-major n x (p+1)) is solved with the factor by two triangular solves, R = B X by a GEMM, and the
-// p x p Schur complement S = (R + R')/2 is factored by LAPACK dpotrf -- the reference's own sequence
-// (MatrixUtils.triangularSolve = dtrtrs, KKTSystem.scala:120-144), as rocBLAS / rocSOLVER calls (kkt_wide.cpp).
-static int kkt_solve_pd_wide(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
-  hipStream_t s = ctx->s;
-  const int n = ctx->n, np = ctx->np, p = ctx->p, nr = p + 1;
-  if (!ctx->blas || !ctx->kY || !ctx->kR || !ctx->kS || !ctx->kzp || !ctx->kinfo) {  // lazily, each piece once
-    if (!ctx->kY) CHK(dalloc(ctx, &ctx->kY, (size_t)np * nr));
-    if (!ctx->kR) CHK(dalloc(ctx, &ctx->kR, (size_t)p * nr));
-    if (!ctx->kS) CHK(dalloc(ctx, &ctx->kS, (size_t)p * p));
-    if (!ctx->kzp) CHK(dalloc(ctx, &ctx->kzp, (size_t)p));
-    if (!ctx->kinfo) CHK(dalloc(ctx, &ctx->kinfo, 1));
-    if (!ctx->blas && lib_handle_create(s, &ctx->blas) != 0)
-      return set_err(ctx, CVXG_E_HIP, "rocBLAS handle creation failed");
+  const double* X = ctx->sol;
+  int ldx = nr;
+  if (fused) {
+    backward_solve(ctx, nr);  // X = Q^-1 [B' | Dq]   (:120-121)
+  } else {
+    launch_kkt_prep(s, ctx->Aeq, np, p, n, np, ctx->dfin, ctx->kB, ctx->kY, ctx->kY_ld);  // [B' | Dq]
+    launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, ctx->kY_ld, p, ctx->kY);
+    launch_trsm_many(s, false, ctx->L, np, ctx->Linv, ctx->kY, ctx->kY_ld, ctx->nblk, ctx->kY_chunks, ctx->kYg,
+                     ++ctx->fm_gen, ctx->ctrl);
+    launch_trsm_many(s, true, ctx->L, np, ctx->Linv, ctx->kY, ctx->kY_ld, ctx->nblk, ctx->kY_chunks, ctx->kYg,
+                     ++ctx->fm_gen, ctx->ctrl);
+    X = ctx->kY;
+    ldx = ctx->kY_ld;
   }
-  tstart(ctx, 1);
-  ruiz(ctx);
-  tstop(ctx, 1);
-  tstart(ctx, 2);
-  int reg = 0;
-  double mind = 0.0;
-  int rc = regularized_cholesky(
-      ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, qv, 1.0, n, np, 1, 0, ctx->rhs); }, &reg, &mind, [] {});
-  tstop(ctx, 2);
-  info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
-  info->regularized = reg;
-  info->min_diag = mind;
-  if (rc != CVXG_OK) return rc;
-  tstart(ctx, 3);
-  launch_kkt_prep_cm(s, ctx->Aeq, np, p, n, np, ctx->dfin, qv, ctx->kB, ctx->kY);  // B = A diag(d); Y = [B' | Dq]
-  bool ok = lib_llt_solve(ctx->blas, n, nr, ctx->L, np, ctx->kY, np) == 0;            // X = Q^-1 Y   (:120-121)
-  // R = B X (p x (p+1)); column p = B Hinv_q   (:126, :141)
-  ok = ok && lib_gemm_h(ctx->blas, true, false, p, nr, n, 1.0, ctx->kB, np, ctx->kY, np, 0.0, ctx->kR, p) == 0;
-  launch_kkt_sym(s, ctx->kR, p, bv, ctx->kS, ctx->kzp);  // S = (R + R')/2, z = -(b + B Hinv_q)  (:139-141)
-  ok = ok && lib_potrf(ctx->blas, p, ctx->kS, p, ctx->kinfo) == 0;  // K = cholesky(S)  (:140)
-  HIPC(ctx, hipGetLastError());
-  int hinfo = 0;
-  CHK(copy_sync(ctx, &hinfo, ctx->kinfo, sizeof(int), hipMemcpyDeviceToHost));
-  if (!ok) return set_err(ctx, CVXG_E_HIP, "KKT (p = %d): rocBLAS / rocSOLVER call failed", p);
-  if (hinfo != 0) return set_err(ctx, CVXG_E_NOT_PD, "KKT Schur complement not positive definite (dpotrf info %d)", hinfo);
-  ok = lib_potrs(ctx->blas, p, ctx->kS, p, ctx->kzp) == 0;  // w: K u = z, K' w = u  (:143-144)
-  HIPC(ctx, hipMemcpyAsync(ctx->kw, ctx->kzp, (size_t)p * sizeof(double), hipMemcpyDeviceToDevice, s));
-  // y = -(Hinv_q + Hinv_At w)  (:145)
-  HIPC(ctx, hipMemcpyAsync(ctx->kx, ctx->kY + (size_t)p * np, (size_t)np * sizeof(double), hipMemcpyDeviceToDevice, s));
-  ok = ok && lib_gemv_h(ctx->blas, np, p, -1.0, ctx->kY, np, ctx->kw, -1.0, ctx->kx) == 0;
-  if (!ok) return set_err(ctx, CVXG_E_HIP, "KKT (p = %d): rocBLAS / rocSOLVER call failed", p);
   launch_ctrl_reset_chol(s, ctx->ctrl);
+  if (p <= NB) {
+    launch_schur_form(s, ctx->kB, np, X, ldx, p, np, ctx->kgram, bv, p, p, ctx->kS, ctx->kzp);
+    launch_schur_small(s, ctx->kS, p, ctx->kzp, ctx->kw, ctx->ctrl);
+  } else {
+    const int ps = ctx->s_nblk * NB;
+    launch_schur_form(s, ctx->kB, np, X, ldx, p, np, ctx->kgram, bv, ps, ps, ctx->sL, ctx->kzp);
+    launch_chol_dataflow(s, ctx->sL, ps, ctx->kzp, 1, ctx->sLinv, ctx->ctrl, ctx->s_work, ctx->s_nblk, ctx->s_tasks,
+                         ctx->s_ntasks, ctx->ncu, nullptr);
+    launch_bwd_dataflow(s, ctx->sL, ps, ctx->sLinv, ctx->kzp, ctx->sw, 1, ctx->s_nblk, ctx->s_bwd, ++ctx->s_gen,
+                        ctx->ctrl);
+    HIPC(ctx, hipMemcpyAsync(ctx->kw, ctx->sw, (size_t)p * sizeof(double), hipMemcpyDeviceToDevice, s));
+  }
+  launch_kkt_v(s, X, ldx, p, np, ctx->kw, ctx->kx);  // y = -(Hinv_q + Hinv_At w)   (:145)
   return kkt_residual_check(ctx, qv, bv, tol, info);
 }
 
 static int kkt_solve_any(cvxg_ctx* ctx, const double* qv, const double* bv, double tol, cvxg_step_info* info) {
-  return ctx->p + 1 <= MAX_RHS ? kkt_solve_pd(ctx, qv, bv, tol, info) : kkt_solve_pd_wide(ctx, qv, bv, tol, info);
+  return kkt_solve_pd(ctx, qv, bv, tol, info);
 }
 
 // KKTSystem.solve (KKTSystem.scala:43-66): solvePD(H) -> solvePD(H + A'A, q - A'b) -> kktSymSolve.
@@ -1374,6 +1403,10 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   const int slots = 2 * std::max(ncu, 1);
   ctx->slots = slots;
   if (const char* e = getenv("CVXG_SPARSE_ROWS")) ctx->sparse_rows = atoi(e) != 0;
+  // the fused forward solve carries the KKT columns only on small problems: at C3 (64 blocks) the many-column solves
+  // cost less than the 9-column chain (C3EQ8: 204.5 vs 191.5 solves/s)
+  ctx->kkt_fused_rhs = ctx->nblk < 8 ? MAX_RHS : 1;
+  if (const char* e = getenv("CVXG_KKT_FUSED_RHS")) ctx->kkt_fused_rhs = std::max(1, atoi(e));
   const int kchunks = (int)(mp / KC);
   std::vector<int> tl = syrk_tile_plan(nt, slots, &ctx->ntiles_main);
   ctx->ntiles = (int)tl.size();
@@ -1427,9 +1460,10 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->qextra_tr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)ctx->kY, (void*)ctx->kR, (void*)ctx->kS, (void*)ctx->kzp, (void*)ctx->kinfo})
+  for (void* p : {(void*)ctx->kY, (void*)ctx->kYg, (void*)ctx->kgram, (void*)ctx->kS, (void*)ctx->kzp,
+                  (void*)ctx->sL, (void*)ctx->sLinv, (void*)ctx->sw, (void*)ctx->s_tasks, (void*)ctx->s_work,
+                  (void*)ctx->s_bwd})
     if (p) (void)hipFree(p);
-  lib_handle_destroy(ctx->blas);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
   if (ctx->hls) (void)hipHostFree(ctx->hls);
   if (ctx->pd_hout) (void)hipHostFree(ctx->pd_hout);

@@ -741,82 +741,6 @@ void launch_ls_finalize(hipStream_t s, const double* part_log, const int* part_c
   k_ls_finalize<<<1, 64, 0, s>>>(part_log, part_cnt, part_aux, nblocks, out_log, out_cnt);
 }
 
-// ------------------------------------------------------------------------------------------------
-// KKT Schur complement for p <= CVXG_MAX_EQ equalities (KKTSystem.scala:99-167), one workgroup.
-// X = [H^-1 B' | H^-1 Dq] (n x nrhs row-major, nrhs = p+1), B = A diag(d) (p x ld row-major).
-// R = B X[:, :p]; S = (R+R')/2; K = chol(S); z = -(b + B X[:,p]); w = K'^-1 K^-1 z;
-// x = -(X[:,p] + X[:,:p] w).  chol failure -> ctrl->chol_info = -1.
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_kkt_schur(const double* __restrict__ X, int nrhs,
-                                                   const double* __restrict__ B, int ldb, int p, int n,
-                                                   const double* __restrict__ bvec, double* __restrict__ w_out,
-                                                   double* __restrict__ xsol, DevCtrl* ctrl) {
-  __shared__ double red[16];
-  __shared__ double R[8][9];  // R[a][0..p-1], column p holds B X[:,p]
-  __shared__ double wsh[8];
-  __shared__ int fail;
-  if (threadIdx.x == 0) fail = 0;
-  for (int a = 0; a < p; ++a) {
-    for (int c = 0; c <= p; ++c) {
-      double acc = 0.0;
-      for (int i = threadIdx.x; i < n; i += blockDim.x) acc = fma(B[(size_t)a * ldb + i], X[(size_t)i * nrhs + c], acc);
-      acc = block_sum(acc, red);
-      if (threadIdx.x == 0) R[a][c] = acc;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double S[8][8], K[8][8], z[8], u[8];
-    for (int a = 0; a < p; ++a)
-      for (int c = 0; c < p; ++c) S[a][c] = (R[a][c] + R[c][a]) * 0.5;  // KKTSystem.scala:139
-    // cholesky(S), lower (dpotrf semantics: fail on non-positive pivot)
-    for (int a = 0; a < p; ++a)
-      for (int c = 0; c < p; ++c) K[a][c] = 0.0;
-    for (int j = 0; j < p && !fail; ++j) {
-      double s = S[j][j];
-      for (int k = 0; k < j; ++k) s -= K[j][k] * K[j][k];
-      if (!(s > 0.0)) {
-        fail = 1;
-        break;
-      }
-      K[j][j] = sqrt(s);
-      for (int i = j + 1; i < p; ++i) {
-        double t = S[i][j];
-        for (int k = 0; k < j; ++k) t -= K[i][k] * K[j][k];
-        K[i][j] = t / K[j][j];
-      }
-    }
-    if (!fail) {
-      for (int a = 0; a < p; ++a) z[a] = -(bvec[a] + R[a][p]);  // z = -(b + A*Hinv_q)   :141
-      for (int i = 0; i < p; ++i) {                             // forwardSolve(K, z)  :143
-        double s = 0.0;
-        for (int j = 0; j < i; ++j) s += K[i][j] * u[j];
-        u[i] = (z[i] - s) / K[i][i];
-      }
-      for (int i = p - 1; i >= 0; --i) {                        // backSolve(K', u)    :144
-        double s = 0.0;
-        for (int j = p - 1; j > i; --j) s += K[j][i] * wsh[j];
-        wsh[i] = (u[i] - s) / K[i][i];
-      }
-      for (int a = 0; a < p; ++a) w_out[a] = wsh[a];
-    } else {
-      ctrl->chol_info = -1;
-    }
-  }
-  __syncthreads();
-  if (fail) return;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {          // x = -(Hinv_q + Hinv_At*w)  :145
-    double s = 0.0;
-    for (int a = 0; a < p; ++a) s += X[(size_t)i * nrhs + a] * wsh[a];
-    xsol[i] = -(X[(size_t)i * nrhs + p] + s);
-  }
-}
-
-void launch_kkt_schur(hipStream_t s, const double* X, int nrhs, const double* B, int ldb, int p, int n,
-                      const double* bvec, double* w_out, double* xsol, DevCtrl* ctrl) {
-  k_kkt_schur<<<1, 256, 0, s>>>(X, nrhs, B, ldb, p, n, bvec, w_out, xsol, ctrl);
-}
-
 }  // namespace cvxg
 
 // ------------------------------------------------------------------------------------------------
@@ -866,41 +790,6 @@ __global__ void k_kkt_prep(const double* __restrict__ Aeq, int ld, int p, int n,
 void launch_kkt_prep(hipStream_t s, const double* Aeq, int ld, int p, int n, int np, const double* d, double* B,
                      double* rhs, int nrhs) {
   k_kkt_prep<<<(np + 255) / 256, 256, 0, s>>>(Aeq, ld, p, n, np, d, B, rhs, nrhs);
-}
-
-// Wide KKT path: B = Aeq diag(d) (p x ld, row-major) and the column-major n x (p+1) right-hand side Y = [B' | Dq]
-// (KKTSystem.scala:114-118), leading dimension np (padding rows zero)
-__global__ void k_kkt_prep_cm(const double* __restrict__ Aeq, int ld, int p, int n, int np, const double* __restrict__ d,
-                              const double* __restrict__ q, double* __restrict__ B, double* __restrict__ Y) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int a = blockIdx.y;  // 0..p (p: the Dq column)
-  if (i >= np) return;
-  if (a < p) {
-    const double b = (i < n) ? d[i] * Aeq[(size_t)a * ld + i] : 0.0;
-    B[(size_t)a * ld + i] = b;
-    Y[(size_t)a * np + i] = b;
-  } else {
-    Y[(size_t)p * np + i] = (i < n) ? d[i] * q[i] : 0.0;
-  }
-}
-void launch_kkt_prep_cm(hipStream_t s, const double* Aeq, int ld, int p, int n, int np, const double* d,
-                        const double* q, double* B, double* Y) {
-  k_kkt_prep_cm<<<dim3((np + 255) / 256, p + 1), 256, 0, s>>>(Aeq, ld, p, n, np, d, q, B, Y);
-}
-
-// S = (R + R')/2 (KKTSystem.scala:139) and z = -(b + R[:, p]) (:141) from R = B X (p x (p+1), column-major)
-__global__ void k_kkt_sym(const double* __restrict__ R, int p, const double* __restrict__ b, double* __restrict__ S,
-                          double* __restrict__ z) {
-  const size_t pp = (size_t)p * p;  // p < n <= 65472: p*p exceeds int range
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= pp) return;
-  const size_t r = i % p, c = i / p;
-  S[i] = (R[c * p + r] + R[r * p + c]) * 0.5;
-  if (c == 0) z[r] = -(b[r] + R[pp + r]);
-}
-void launch_kkt_sym(hipStream_t s, const double* R, int p, const double* b, double* S, double* z) {
-  const size_t pp = (size_t)p * p;
-  k_kkt_sym<<<(unsigned)((pp + 255) / 256), 256, 0, s>>>(R, p, b, S, z);
 }
 
 // out = u + alpha*v elementwise with a strided source column: out_i = u_i + alpha * v[i*vs + vc]

@@ -162,9 +162,22 @@ int ls_klp_blocks(int n);
 void launch_ls_klp(hipStream_t s, const double* x, const double* sdir, int n, double nd, double tbase, double beta,
                    double* part, double* out);
 
-// ---- KKT Schur complement (p > 0) ------------------------------------------------------------------
-void launch_kkt_schur(hipStream_t s, const double* X, int nrhs, const double* B, int ldb, int p, int n,
-                      const double* bvec, double* w_out, double* xsol, DevCtrl* ctrl);
+// ---- KKT equality block (k_kkt.hip) ------------------------------------------------------------------
+// L Z = Y (transposed = false) or L' X = Y (true) in place for nchunk * 16 right-hand-side columns (row-major, leading
+// dimension ldy), one dataflow launch; gran: trsm_many_granule_doubles(nblk, nchunk) doubles of hand-off granules
+// (zeroed once; gen increases per launch)
+size_t trsm_many_granule_doubles(int nblk, int nchunk);
+void launch_trsm_many(hipStream_t s, bool transposed, const double* L, int ld, const double* Linv, double* Y, int ldy,
+                      int nblk, int nchunk, double* gran, int gen, DevCtrl* ctrl);
+// R = B X (B row-major p x ldb, X row-major np x ldx with p + 1 columns), S = (R + R')/2 (lower, rows >= p: identity
+// padding up to ps) and z = -(b + R[:, p]) (zero-padded to ps); part: schur_partial_doubles(np, p) doubles
+size_t schur_partial_doubles(int np, int p);
+void launch_schur_form(hipStream_t s, const double* B, int ldb, const double* X, int ldx, int p, int np, double* part,
+                       const double* bvec, int ps, int lds, double* S, double* z);
+// w = S^-1 z for p <= 64 (S row-major p x p, lower); a non-positive pivot sets ctrl->chol_info = -1
+void launch_schur_small(hipStream_t s, const double* S, int p, const double* z, double* w, DevCtrl* ctrl);
+// y = -(X[:, p] + X[:, :p] w)
+void launch_kkt_v(hipStream_t s, const double* X, int ldx, int p, int np, const double* w, double* y);
 
 // ---- symSolve / kktSymSolve fallback (symsolve.cpp, k_vec.hip) ----------------------------------------
 int sym_eig(hipStream_t s, double* M, int n2, int ldm, double* d, double* e_work, int* dinfo);
@@ -175,19 +188,6 @@ int lib_gemm(hipStream_t s, bool ta, bool tb, int m, int n, int k, const double*
 int lib_gemv(hipStream_t s, bool ta, int rows, int cols, double alpha, const double* A, int lda, const double* x,
              double beta, double* y);
 int lib_dot(hipStream_t s, int n, const double* u, const double* v, double* out);
-// kkt_wide.cpp: persistent-handle library calls of the wide KKT path (p + 1 > MAX_RHS)
-int lib_handle_create(hipStream_t s, void** out);
-void lib_handle_destroy(void* h);
-int lib_llt_solve(void* h, int n, int k, const double* L, int ldl, double* Y, int ldy);
-int lib_gemm_h(void* h, bool ta, bool tb, int m, int n, int k, double alpha, const double* A, int lda, const double* B,
-               int ldb, double beta, double* C, int ldc);
-int lib_gemv_h(void* h, int rows, int cols, double alpha, const double* A, int lda, const double* x, double beta,
-               double* y);
-int lib_potrf(void* h, int p, double* S, int lds, int* dinfo);
-int lib_potrs(void* h, int p, const double* K, int ldk, double* z);
-void launch_kkt_prep_cm(hipStream_t s, const double* Aeq, int ld, int p, int n, int np, const double* d,
-                        const double* q, double* B, double* Y);
-void launch_kkt_sym(hipStream_t s, const double* R, int p, const double* b, double* S, double* z);
 void launch_eig_coeffs(hipStream_t s, const double* dots, const double* d, int n2, int npad, double* a, double* z);
 void launch_sum_chunks(hipStream_t s, const double* part, int nchunks, int cols, double* out);
 void launch_kkt_matrix(hipStream_t s, const double* H, int ldh, const double* Aeq, int lda, int n, int p, int ld,

@@ -162,6 +162,29 @@ def _spec_of(fx):
                 kl_R=fx.get("kl_R"))
 
 
+def _kkt_cancellation(O, pb, t, x, g):
+    """Componentwise condition of the last combination of KKTSystem.solveWithCholFactor (KKTSystem.scala:145),
+    y = -(X_q + X_B w) with x = D y, in the oracle's arithmetic: || D (|X_q| + |X_B| |w|) || / || D y ||.  Every FP64
+    implementation carries ulp-level differences in X and w (blocked vs LAPACK triangular solves), which this
+    combination amplifies by cond; late in a centering with equalities it reaches ~1e9 (simplex_rank1_n10_p1 step 26:
+    a one-ulp change of z moves the oracle's own dx by 1.8e-7)."""
+    H = O.barrier_hessian(pb, t, x, literal=False)
+    d, Q, _ = O.ruiz_equilibrate(H)
+    B = pb.Aeq * d[None, :]
+    L, _ = O.regularized_cholesky(Q)
+    n, p = B.shape[1], B.shape[0]
+    rhs = np.zeros((n, p + 1))
+    rhs[:, :p] = B.T
+    rhs[:, p] = d * g
+    X = O.triangular_solve(L.T, "U", O.triangular_solve(L, "L", rhs))
+    R = B @ X[:, :p]
+    S = (R + R.T) * 0.5
+    z = -((pb.beq - pb.Aeq @ x) + B @ X[:, p])
+    w = np.linalg.solve(S, z)
+    y = -(X[:, p] + X[:, :p] @ w)
+    return float(np.linalg.norm(d * (np.abs(X[:, p]) + np.abs(X[:, :p]) @ np.abs(w))) / np.linalg.norm(d * y))
+
+
 def _centering_index(ts):
     """(first step of its centering, iteration within the centering) for every recorded step."""
     first, out = 0, []
@@ -175,7 +198,9 @@ def _centering_index(ts):
 @pytest.mark.parametrize("path", _fixtures(), ids=lambda p: os.path.basename(p))
 def test_golden_newton_steps(mods, path):
     """Every inner Newton step of the golden trajectories, given the oracle's (t, x, grad):
-    * t <= 1e4: dx within 1e-8 relative of the oracle's (BASELINE.json north star);
+    * t <= 1e4: dx within 1e-8 relative of the oracle's (BASELINE.json north star); on KKT steps whose final
+      combination y = -(X_q + X_B w) cancels (componentwise condition cond, _kkt_cancellation) within 8 u cond
+      whenever that exceeds 1e-8 -- below it FP64 does not determine dx (the steps are printed);
     * every step (also t > 1e4, where H is ill-conditioned and two FP64 factorizations legitimately differ in dx):
       the residual of the solve |H dx + g| (the engine's H) is within 4x of the oracle's own residual with its own H
       (or below 64 n u (|H|_F |dx| + |g|)), and the Newton decrement is on the same side of tol whenever it is not rounding
@@ -190,6 +215,7 @@ def test_golden_newton_steps(mods, path):
     n = spec["a0"].shape[0]
     u = np.finfo(float).eps / 2
     checked_bwd = 0
+    derived = []
     for k in range(nsteps):
         t, x = float(fx["t"][k]), fx["x"][k]
         # identical inputs: the oracle's (t, x, grad) -- the gradient near a centred point is a sum of
@@ -199,7 +225,13 @@ def test_golden_newton_steps(mods, path):
         dref = fx["dx"][k]
         rel = np.linalg.norm(dx - dref) / np.linalg.norm(dref)
         if t <= 1e4:
-            assert rel < 1e-8, f"step {k} (t={t}): rel {rel:.3e}"
+            bar = 1e-8
+            if spec.get("Aeq") is not None:  # KKT: dx = D(-(X_q + X_B w)) may cancel far below its terms
+                cond = _kkt_cancellation(O, pb, t, x, g)
+                if 8 * u * cond > bar:
+                    bar = 8 * u * cond
+                    derived.append((k, f"{rel:.2e}", f"{cond:.2e}"))
+            assert rel < bar, f"step {k} (t={t}): rel {rel:.3e}"
         if spec.get("Aeq") is None:  # p = 0: H dx = -g (the KKT steps are checked through dx and the trajectory)
             # each side against its own H: near the boundary d_i = ub_i - a_i.x cancels, so the engine's and the
             # oracle's H differ by ~u |a_i||x| / d_i in their largest weights -- a difference of the H evaluation,
@@ -218,6 +250,8 @@ def test_golden_newton_steps(mods, path):
             assert (-info.q / 2 > pars.tolSolver) == (-qr / 2 > pars.tolSolver), (k, t)
     if spec.get("Aeq") is None:
         assert checked_bwd == nsteps
+    if derived:
+        print(f"{os.path.basename(path)}: KKT steps held to 8 u cond instead of 1e-8 (step, rel, cond): {derived}")
     eng.close()
 
 
@@ -519,13 +553,17 @@ def test_equality_kkt_direction_vs_oracle(mods):
     eng.close()
 
 
-@pytest.mark.parametrize("p", [8, 9, 12, 64])
-def test_equality_kkt_direction_any_p(mods, p):
-    """KKTSystem.solve (KKTSystem.scala:43-167) for any number of equality rows: p + 1 <= 9 right-hand sides ride the
-    fused forward solve (p = 8), wider blocks take the rocBLAS / rocSOLVER sequence of solveWithCholFactor (p = 9,
-    12, 64).  dx within 1e-8 and w within 1e-7 of the oracle's KKTSystem at t = 1 and 100."""
+@pytest.mark.parametrize("n,p,fused", [(200, 1, 9), (200, 8, 9), (200, 8, 1), (200, 9, 9), (200, 12, 9), (200, 64, 9),
+                                       (200, 100, 9), (200, 150, 9), (1024, 40, 9), (1024, 130, 9)])
+def test_equality_kkt_direction_any_p(mods, n, p, fused, monkeypatch):
+    """KKTSystem.solve (KKTSystem.scala:43-167) for any number of equality rows (k_kkt.hip): X = Q^-1 [B' | Dq] from
+    the factorization's fused forward solve + the backward solve (p + 1 <= 9) or the many-column dataflow solves with
+    L and L' (p >= 9, and p = 8 with CVXG_KKT_FUSED_RHS=1), S = (R + R')/2 with R = B X factored by one workgroup
+    (p <= 64) or the dataflow Cholesky (p = 100, 150).  dx within 1e-8 and w within 1e-7 of the oracle's KKTSystem
+    at t = 1 and 100."""
+    monkeypatch.setenv("CVXG_KKT_FUSED_RHS", str(fused))
     Z, SP, Engine, O = mods
-    spec = Z.random_qp_eq(200, 360, p, instance=3)
+    spec = Z.random_qp_eq(n, 360 if n == 200 else 2 * n, p, instance=3)
     pb = _opb(O, spec)
     eng = _engine(Engine, spec)
     pars = SP.standardParams()
