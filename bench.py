@@ -282,18 +282,17 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     def pd_solve():  # one whole PrimalDualSolver.solve from x0; returns its KKT solves
         eng.set_x(spec["x0"])
         s_ = eng.pd_solve(pars)
-        record(eng.phase_times())
         return s_.newton_steps
 
     steps = args.steps
     if wl.endswith("PD"):
-        eng.set_timing(True)
         pd_solve()  # warm-up solve
-        syrk_ms.clear(), ruiz_ms.clear(), chol_ms.clear(), solve_ms.clear(), ls_ms.clear()
     else:
         for _ in range(args.warmup):
             one_step()
-        eng.set_timing(True)
+    # phase timers: HIP events on the stream of each phase, recorded per step into a ring and read once after the
+    # timed region (cvxg_get_phase_times), so the timing never makes a step wait
+    eng.set_timing(True)
     reruns0 = eng.ruiz_lookahead()
     D.barrier(device)
     sync()
@@ -305,11 +304,11 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
         steps = done
     for _ in range(0 if wl.endswith("PD") else steps):
         one_step()
-        record(eng.phase_times())
     sync()
     D.barrier(device)
     elapsed = time.perf_counter() - t0
     elapsed = D.max_over_ranks(elapsed, device)
+    record(eng.phase_times())  # per-step means over the timed steps (the last 63 at most)
     eng.set_timing(False)
     # timed steps whose Ruiz lookahead fell short (their Cholesky phase holds the re-run sweeps + factorization)
     ruiz_reruns = eng.ruiz_lookahead() - reruns0

@@ -28,11 +28,17 @@ namespace {
 
 constexpr int NT = 8;  // phase timers
 
+// Phase timers: HIP events recorded on the stream each phase runs on, one ring slot per Newton step (or PD iteration),
+// read only by cvxg_get_phase_times -- a step never waits on its own events, so timing does not serialise the
+// pipeline (the prefetched assembly of the next step runs beside the host's reads).
+constexpr int TRING = 64;
 struct Timer {
-  hipEvent_t ev[NT][2];
-  bool on = false;
-  bool rec[NT] = {false};
-  double ms[NT] = {0};
+  hipEvent_t ev[TRING][NT][2] = {};
+  bool on = false, created = false;
+  bool rec[TRING][NT] = {};
+  int tick = 0;      // the step being recorded: ring slot tick % TRING
+  int steps = 0;     // steps recorded since timing was enabled (capped at TRING - 1)
+  bool pf5 = false;  // slot 5 of the next tick already holds the prefetched assembly
 };
 
 }  // namespace
@@ -136,7 +142,12 @@ struct cvxg_ctx {
   unsigned long long* df_trace = nullptr;  // CVXG_DF_TRACE=<file>: per-task timeline of the last factorization
   std::string df_trace_path;
   DevCtrl* ctrl = nullptr;
-  DevCtrl* hctrl = nullptr;
+  DevCtrl* hctrl = nullptr;     // coherent pinned mirror of ctrl (written by k_publish_ctrl)
+  DevCtrl* hctrl_dev = nullptr; // its device-side address
+  unsigned* hflag = nullptr;    // coherent pinned sequence word of host_read, and its device-side address
+  unsigned* hflag_dev = nullptr;
+  unsigned hseq = 0;
+  double* hls_dev = nullptr;    // device-side address of hls (coherent pinned)
   double* hls = nullptr;  // pinned: [3*LS_TRIALS] {log sum, its error bound, sum |log|} then [4*LS_TRIALS] counts as ints
   // centering state
   double t = 1.0;
@@ -148,6 +159,14 @@ struct cvxg_ctx {
   double eqGap = 0.0;
   double f_at_x = 0.0;    // barrier value at x
   int x_eval_valid = 0;   // c/d/w/y/scalars correspond to the current x and t
+  // The next step's Hessian assembly, launched on s2 as soon as the step's constraint values (w) exist, so it runs
+  // beside the rest of the evaluation (P x, A'(1/d), the gradient, the reductions) and the host's read of them;
+  // s waits on ev_h right after that read, so all later work on s is ordered behind it.  h_valid: H holds the
+  // assembly at the current x and t (x_eval_valid too).
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_w = nullptr, ev_h = nullptr;
+  bool h_valid = false;
+  double* spart = nullptr;  // SYRK split-K partials (ctx->part belongs to the evaluation's A'(1/d))
   // affine re-parametrisation (cvxg_affine_from): x = z0 + F u with F (aff_n x n, column-major, ld aff_n)
   double *aff_F = nullptr, *aff_z0 = nullptr;
   int aff_n = 0;
@@ -191,28 +210,47 @@ static int dalloc(cvxg_ctx* ctx, T** p, size_t count) {
 }
 
 static void tstart(cvxg_ctx* ctx, int i) {
-  if (ctx->tm.on) (void)hipEventRecord(ctx->tm.ev[i][0], ctx->s);
+  if (ctx->tm.on) (void)hipEventRecord(ctx->tm.ev[ctx->tm.tick % TRING][i][0], ctx->s);
 }
 static void tstop(cvxg_ctx* ctx, int i) {
   if (ctx->tm.on) {
-    (void)hipEventRecord(ctx->tm.ev[i][1], ctx->s);
-    ctx->tm.rec[i] = true;
+    (void)hipEventRecord(ctx->tm.ev[ctx->tm.tick % TRING][i][1], ctx->s);
+    ctx->tm.rec[ctx->tm.tick % TRING][i] = true;
   }
 }
 
-// Copies are ordered on the ctx stream: it is created non-blocking, so a plain hipMemcpy (null stream) would
-// not wait for work queued on it (e.g. dalloc's zero fill) and could be overwritten by it.
 static int copy_sync(cvxg_ctx* ctx, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
   HIPC(ctx, hipMemcpyAsync(dst, src, bytes, kind, ctx->s));
   HIPC(ctx, hipStreamSynchronize(ctx->s));
   return CVXG_OK;
 }
 
-static int sync_ctrl(cvxg_ctx* ctx) {
-  HIPC(ctx, hipMemcpyAsync(ctx->hctrl, ctx->ctrl, sizeof(DevCtrl), hipMemcpyDeviceToHost, ctx->s));
-  HIPC(ctx, hipStreamSynchronize(ctx->s));
+// Host reads behind everything enqueued so far on ctx->s, without a stream synchronisation: k_publish copies the
+// ranges into coherent pinned host memory and then writes a sequence word that the host spins on (a stream
+// synchronisation's wake-up left the GPU idle ~20-30 us per read, profiles/r03 timeline).  A failed launch or a
+// faulted stream ends the spin through hipStreamQuery.
+static int host_read(cvxg_ctx* ctx, const void* s0, void* d0, size_t b0, const void* s1 = nullptr, void* d1 = nullptr,
+                     size_t b1 = 0) {
+  const unsigned seq = ++ctx->hseq;
+  launch_publish(ctx->s, s0, d0, b0, s1, d1, b1, ctx->hflag_dev, seq);
+  HIPC(ctx, hipGetLastError());
+  for (unsigned spins = 0;; ++spins) {
+    if (__atomic_load_n(ctx->hflag, __ATOMIC_ACQUIRE) == seq) break;
+    if ((spins & 1023) == 1023) {
+      const hipError_t q = hipStreamQuery(ctx->s);
+      if (q == hipSuccess) {  // the stream drained: the word must be there (re-read once, then report)
+        if (__atomic_load_n(ctx->hflag, __ATOMIC_ACQUIRE) == seq) break;
+        return set_err(ctx, CVXG_E_HIP, "host_read: stream idle but the sequence word was not published");
+      }
+      if (q != hipErrorNotReady)
+        return set_err(ctx, CVXG_E_HIP, "HIP error %d (%s) during a host read", (int)q, hipGetErrorString(q));
+    }
+    __builtin_ia32_pause();
+  }
   return CVXG_OK;
 }
+
+static int sync_ctrl(cvxg_ctx* ctx) { return host_read(ctx, ctx->ctrl, ctx->hctrl_dev, sizeof(DevCtrl)); }
 
 // Upload an n-vector into a zero-padded device vector of length np.
 static int upload_vec(cvxg_ctx* ctx, double* dst, const double* src, int n, int np) {
@@ -483,11 +521,26 @@ static void constraint_eval_all(cvxg_ctx* ctx) {
 
 // Barrier value / gradient pieces at the current x and ctrl->t (BarrierSolver.scala:280-301):
 // c, d, w, invd, logd, Px, y, eqDiff, and sc[A0X, XPX, SUMLOG, GG, EQ2].
-static int eval_at_x(cvxg_ctx* ctx) {
+static int assemble_hessian(cvxg_ctx* ctx, const double* wts, const double* qw, hipStream_t st);
+static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false) {
   hipStream_t s = ctx->s;
   const int np = ctx->np, mp = ctx->mp;
   launch_ctrl_reset_eval(s, ctx->ctrl);
   constraint_eval_all(ctx);
+  ctx->h_valid = false;
+  prefetch = prefetch && !ctx->kl && !ctx->klp;  // (their Hessians need the evaluation's y / diag(1/x) first)
+  if (prefetch) {  // the assembly needs w (and the quadratic rows' P_k x) only
+    HIPC(ctx, hipEventRecord(ctx->ev_w, s));
+    HIPC(ctx, hipStreamWaitEvent(ctx->s2, ctx->ev_w, 0));
+    const int nx = (ctx->tm.tick + 1) % TRING;  // timed as phase 5 of the step that will use it
+    if (ctx->tm.on) HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][0], ctx->s2));
+    CHK(assemble_hessian(ctx, nullptr, nullptr, ctx->s2));
+    if (ctx->tm.on) {
+      HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][1], ctx->s2));
+      ctx->tm.rec[nx][5] = ctx->tm.pf5 = true;
+    }
+    HIPC(ctx, hipEventRecord(ctx->ev_h, ctx->s2));
+  }
   const bool quad = ctx->hasP && !ctx->kl;
   const bool cert = ls_certified(ctx);
   if (quad) {
@@ -535,7 +588,12 @@ static int eval_at_x(cvxg_ctx* ctx) {
     launch_dot(s, ctx->eqd, nullptr, ctx->p, ctx->ctrl, SC_EQ2);
   }
   HIPC(ctx, hipGetLastError());
-  CHK(sync_ctrl(ctx));
+  const int rc_sync = sync_ctrl(ctx);
+  if (prefetch) {
+    HIPC(ctx, hipStreamWaitEvent(s, ctx->ev_h, 0));  // everything later on s follows the assembly
+    ctx->h_valid = rc_sync == CVXG_OK;
+  }
+  CHK(rc_sync);
   const DevCtrl& h = *ctx->hctrl;
   const double f0 = objective_from_ctrl(ctx, h);
   ctx->f_at_x = ctx->t * f0 - h.sc[SC_SUMLOG];
@@ -553,18 +611,21 @@ static double objective_at_x(cvxg_ctx* ctx) { return objective_from_ctrl(ctx, *c
 // H = t P + A' diag(wts) A (+ the sparse rows' entries) + sum_k qw_k P_k over the QuadraticConstraint rows; wts =
 // ctx->w = 1/d^2 and qw = 1/d for the barrier Hessian (BarrierSolver.scala:314), or the primal-dual KKT weights
 // lambda/d and qw = lambda (kktMatrix_noEqs, PrimalDualSolver.scala:226-238; then ctrl->t = 1).
-static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr, const double* qw = nullptr) {
-  tstart(ctx, 5);
+static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr, const double* qw = nullptr,
+                            hipStream_t st = nullptr) {
+  const bool own = st == nullptr;  // on ctx->s (timed here as phase 5); otherwise the prefetch on s2 (timed there)
+  if (own) st = ctx->s;
+  if (own) tstart(ctx, 5);
   const double* wsrc = wts ? wts : ctx->w;
   // full tiles in whole waves of workgroup slots, then the leftover tiles split along K across all slots
   // (partials + ordered reduce) so the last wave is not a handful of tiles on an otherwise idle chip.
   const double* P = ctx->hasP ? ctx->P : nullptr;
   if (ctx->kl) {  // objF.hessianAt(z) = B diag(y) B' (Dist_KL.scala:158-165) into P: a weighted SYRK over the outcomes
     if (ctx->ntiles_main > 0)
-      launch_syrk_assemble(ctx->s, ctx->KB, ctx->np, ctx->kl_y, ctx->noutp, nullptr, ctx->ctrl, ctx->P, ctx->np,
+      launch_syrk_assemble(st, ctx->KB, ctx->np, ctx->kl_y, ctx->noutp, nullptr, ctx->ctrl, ctx->P, ctx->np,
                            TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->part);
     if (ctx->ntiles > ctx->ntiles_main)  // the tail (all tiles for a small dual) split along the outcomes
-      launch_syrk_assemble(ctx->s, ctx->KB, ctx->np, ctx->kl_y, ctx->noutp, nullptr, ctx->ctrl, ctx->P, ctx->np,
+      launch_syrk_assemble(st, ctx->KB, ctx->np, ctx->kl_y, ctx->noutp, nullptr, ctx->ctrl, ctx->P, ctx->np,
                            TileList{ctx->tiles + ctx->ntiles_main, ctx->ntiles - ctx->ntiles_main}, ctx->kl_nsplit,
                            ctx->kl_spart);
   }
@@ -573,25 +634,25 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr, const do
   int rows = ctx->mp;
   if (ctx->have_sparse) {  // dense rows only; the sparse rows' entries are added below
     if (ctx->nq > 0)  // gradient rows G_k = a_k + P_k x of the quadratic constraints
-      launch_quad_rows(ctx->s, ctx->A, ctx->qPx, ctx->qrows, ctx->qslot, ctx->nq, ctx->np, ctx->As);
-    launch_gather_w(ctx->s, wsrc, ctx->didx, ctx->ndense, ctx->mdp, ctx->wd);
+      launch_quad_rows(st, ctx->A, ctx->qPx, ctx->qrows, ctx->qslot, ctx->nq, ctx->np, ctx->As);
+    launch_gather_w(st, wsrc, ctx->didx, ctx->ndense, ctx->mdp, ctx->wd);
     A = ctx->As;
     w = ctx->wd;
     rows = ctx->mdp;
   }
   const double* Pd = ctx->klp ? ctx->klp_hd : nullptr;  // the KL primal's diag(1/x) * t
   if (ctx->ntiles_main > 0)
-    launch_syrk_assemble(ctx->s, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
-                         TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->part, Pd);
+    launch_syrk_assemble(st, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
+                         TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->spart, Pd);
   if (ctx->ntiles > ctx->ntiles_main)
-    launch_syrk_assemble(ctx->s, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
+    launch_syrk_assemble(st, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
                          TileList{ctx->tiles + ctx->ntiles_main, ctx->ntiles - ctx->ntiles_main}, ctx->nsplit,
-                         ctx->part, Pd);
+                         ctx->spart, Pd);
   if (ctx->have_sparse)
-    launch_sparse_hess(ctx->s, ctx->sp_ptr, ctx->sp_pq, ctx->sp_row, ctx->sp_coef, wsrc, ctx->sp_T, ctx->H, ctx->np);
+    launch_sparse_hess(st, ctx->sp_ptr, ctx->sp_pq, ctx->sp_row, ctx->sp_coef, wsrc, ctx->sp_T, ctx->H, ctx->np);
   if (ctx->nq > 0)  // + hessianAt/d = P_k / d_k  (BarrierSolver.scala:314), or grad2_gi * l_i (PrimalDualSolver.scala:236)
-    launch_quad_hess(ctx->s, ctx->Pq, qw ? qw : ctx->invd, ctx->qrows, ctx->nq, ctx->np, ctx->H);
-  tstop(ctx, 5);
+    launch_quad_hess(st, ctx->Pq, qw ? qw : ctx->invd, ctx->qrows, ctx->nq, ctx->np, ctx->H);
+  if (own) tstop(ctx, 5);
   HIPC(ctx, hipGetLastError());
   return CVXG_OK;
 }
@@ -1006,9 +1067,13 @@ static int newton_direction_kkt(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_ste
 }
 
 static int newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
-  tstart(ctx, 0);
-  CHK(assemble_hessian(ctx));
-  tstop(ctx, 0);
+  if (ctx->h_valid && ctx->x_eval_valid) {  // assembled on s2 behind this x's evaluation (s already waits on it)
+  } else {
+    tstart(ctx, 0);
+    CHK(assemble_hessian(ctx));
+    tstop(ctx, 0);
+  }
+  ctx->h_valid = false;
   int rc;
   if (ctx->p == 0) {
     rc = newton_direction_p0(ctx, pars, info);
@@ -1078,10 +1143,15 @@ static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch
                    ctx->ls_paux, (cert && ctx->nq > 0) ? ctx->qfabs : nullptr);
   launch_ls_finalize(ctx->s, ctx->ls_plog, ctx->ls_pcnt, ctx->ls_paux, nb, ctx->ls_log, ctx->ls_cnt);
   HIPC(ctx, hipGetLastError());
-  HIPC(ctx, hipMemcpyAsync(ctx->hls, ctx->ls_log, 3 * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
-  HIPC(ctx, hipMemcpyAsync((int*)(ctx->hls + 3 * LS_TRIALS), ctx->ls_cnt, 4 * LS_TRIALS * sizeof(int),
-                           hipMemcpyDeviceToHost, ctx->s));
-  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  if (ctx->kl || ctx->klp) {  // (their trial sums went out by hipMemcpyAsync into the host-stack batch)
+    HIPC(ctx, hipMemcpyAsync(ctx->hls, ctx->ls_log, 3 * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
+    HIPC(ctx, hipMemcpyAsync((int*)(ctx->hls + 3 * LS_TRIALS), ctx->ls_cnt, 4 * LS_TRIALS * sizeof(int),
+                             hipMemcpyDeviceToHost, ctx->s));
+    HIPC(ctx, hipStreamSynchronize(ctx->s));
+  } else {
+    CHK(host_read(ctx, ctx->ls_log, ctx->hls_dev, 3 * LS_TRIALS * sizeof(double), ctx->ls_cnt,
+                  ctx->hls_dev + 3 * LS_TRIALS, 4 * LS_TRIALS * sizeof(int)));
+  }
   b->k0 = k0;
   const int* cnt = (const int*)(ctx->hls + 3 * LS_TRIALS);
   for (int k = 0; k < LS_TRIALS; ++k) {
@@ -1304,17 +1374,17 @@ static bool loop_cond(cvxg_ctx* ctx, const cvxg_params* pars) {
   return (ctx->nd > tol && ctx->normGrad > tol) || ctx->eqGap > tol;
 }
 
+// End of a timed step: the next ring slot (its events are re-recorded; slot 5 may already hold the next step's
+// prefetched assembly).
 static void timing_collect(cvxg_ctx* ctx) {
   if (!ctx->tm.on) return;
-  (void)hipStreamSynchronize(ctx->s);
-  for (int i = 0; i < NT; ++i) {
-    float ms = 0.f;
-    ctx->tm.ms[i] = 0.0;
-    if (ctx->tm.rec[i] && hipEventElapsedTime(&ms, ctx->tm.ev[i][0], ctx->tm.ev[i][1]) == hipSuccess)
-      ctx->tm.ms[i] = ms;
-    ctx->tm.rec[i] = false;
-  }
-  (void)hipGetLastError();  // never leave a timing error sticky for the next launch check
+  Timer& tm = ctx->tm;
+  tm.tick += 1;
+  tm.steps = std::min(tm.steps + 1, TRING - 1);
+  const int sl = tm.tick % TRING;
+  for (int i = 0; i < NT; ++i)
+    if (i != 5 || !tm.pf5) tm.rec[sl][i] = false;
+  tm.pf5 = false;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1417,6 +1487,11 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   if (ctx->nsplit > 1)
     part = std::max(part, (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE);
   CHK(dalloc(ctx, &ctx->part, part));
+  CHK(dalloc(ctx, &ctx->spart,
+             ctx->nsplit > 1 ? (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE : (size_t)1));
+  HIPC(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
+  HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_w, hipEventDisableTiming));
+  HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_h, hipEventDisableTiming));
   const int lsb = ls_blocks(std::max(m, 1));
   CHK(dalloc(ctx, &ctx->ls_plog, (size_t)lsb * LS_TRIALS));
   CHK(dalloc(ctx, &ctx->ls_paux, (size_t)lsb * LS_TRIALS * 2));
@@ -1427,13 +1502,14 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   for (double** v : {&ctx->cabs, &ctx->eabs, &ctx->c_tr, &ctx->d_tr, &ctx->invd_tr, &ctx->w_tr, &ctx->logd_tr})
     CHK(dalloc(ctx, v, mp));
   CHK(dalloc(ctx, &ctx->ctrl, 1));
-  HIPC(ctx, hipHostMalloc((void**)&ctx->hctrl, sizeof(DevCtrl), hipHostMallocDefault));
-  HIPC(ctx, hipHostMalloc((void**)&ctx->hls, 5 * LS_TRIALS * sizeof(double), hipHostMallocDefault));
+  HIPC(ctx, hipHostMalloc((void**)&ctx->hctrl, sizeof(DevCtrl), hipHostMallocCoherent | hipHostMallocMapped));
+  HIPC(ctx, hipHostMalloc((void**)&ctx->hflag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+  HIPC(ctx, hipHostGetDevicePointer((void**)&ctx->hctrl_dev, ctx->hctrl, 0));
+  HIPC(ctx, hipHostGetDevicePointer((void**)&ctx->hflag_dev, ctx->hflag, 0));
+  *ctx->hflag = 0;
+  HIPC(ctx, hipHostMalloc((void**)&ctx->hls, 5 * LS_TRIALS * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
+  HIPC(ctx, hipHostGetDevicePointer((void**)&ctx->hls_dev, ctx->hls, 0));
   memset(ctx->hctrl, 0, sizeof(DevCtrl));
-  for (int i = 0; i < NT; ++i) {
-    HIPC(ctx, hipEventCreate(&ctx->tm.ev[i][0]));
-    HIPC(ctx, hipEventCreate(&ctx->tm.ev[i][1]));
-  }
   HIPC(ctx, hipStreamSynchronize(ctx->s));
   return CVXG_OK;
 }
@@ -1465,12 +1541,18 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   (void*)ctx->s_bwd})
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
+  if (ctx->hflag) (void)hipHostFree(ctx->hflag);
   if (ctx->hls) (void)hipHostFree(ctx->hls);
   if (ctx->pd_hout) (void)hipHostFree(ctx->pd_hout);
-  for (int i = 0; i < NT; ++i) {
-    if (ctx->tm.ev[i][0]) (void)hipEventDestroy(ctx->tm.ev[i][0]);
-    if (ctx->tm.ev[i][1]) (void)hipEventDestroy(ctx->tm.ev[i][1]);
-  }
+  for (auto& slot : ctx->tm.ev)
+    for (auto& pr : slot)
+      for (hipEvent_t e : pr)
+        if (e) (void)hipEventDestroy(e);
+  if (ctx->s2) (void)hipStreamSynchronize(ctx->s2);
+  if (ctx->spart) (void)hipFree(ctx->spart);
+  for (hipEvent_t e : {ctx->ev_w, ctx->ev_h})
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
   if (ctx->s) (void)hipStreamDestroy(ctx->s);
   delete ctx;
 }
@@ -1886,7 +1968,7 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
     info->norm_grad = ctx->normGrad;
     return CVXG_OK;
   }
-  if (!ctx->x_eval_valid) CHK(eval_at_x(ctx));
+  if (!ctx->x_eval_valid) CHK(eval_at_x(ctx, true));
   const double tol = pars->tolSolver;
   info->f = ctx->f_at_x;
   info->norm_grad = ctx->normGrad;
@@ -1927,7 +2009,10 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
     info->backtracks_c = kc;
     info->backtracks_armijo = ka;
     info->took_step = 1;
-    rc = eval_at_x(ctx);  // y = objF.gradientAt(x); normGrad (and eqDiff)
+    // y = objF.gradientAt(x); normGrad (and eqDiff); the next step's assembly goes out behind the constraint values
+    // when the loop will go on (UnconstrainedSolver.scala:38-41: iter + 1 < maxIter and this step's decrement > tol;
+    // only normGrad <= tol, which the evaluation decides, could end it -- then the assembly is dropped)
+    rc = eval_at_x(ctx, ctx->iter + 1 < pars->maxIter && ctx->nd > tol);
     if (rc != CVXG_OK) return rc;
   }
   ctx->iter += 1;
@@ -2051,13 +2136,40 @@ int cvxg_batch_newton_step(int count, cvxg_ctx* const* ctxs, const cvxg_params* 
 
 int cvxg_set_timing(cvxg_ctx* ctx, int enabled) {
   if (!ctx) return CVXG_E_ARG;
-  ctx->tm.on = enabled != 0;
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  Timer& tm = ctx->tm;
+  if (enabled && !tm.created) {
+    for (auto& slot : tm.ev)
+      for (auto& pr : slot)
+        for (hipEvent_t& e : pr) HIPC(ctx, hipEventCreate(&e));
+    tm.created = true;
+  }
+  if (enabled) {  // a fresh record: the steps from here on
+    tm.steps = 0;
+    tm.pf5 = false;
+    for (auto& slot : tm.rec)
+      for (bool& r : slot) r = false;
+  }
+  tm.on = enabled != 0;
   return CVXG_OK;
 }
 
 int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count) {
   if (!ctx || !ms) return CVXG_E_ARG;
-  for (int i = 0; i < count && i < NT; ++i) ms[i] = ctx->tm.ms[i];
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  HIPC(ctx, hipStreamSynchronize(ctx->s));
+  HIPC(ctx, hipStreamSynchronize(ctx->s2));
+  const Timer& tm = ctx->tm;
+  for (int i = 0; i < count && i < NT; ++i) {
+    double sum = 0.0;
+    for (int k = 1; k <= tm.steps; ++k) {  // the completed steps, newest first
+      const int sl = ((tm.tick - k) % TRING + TRING) % TRING;
+      float v = 0.f;
+      if (tm.rec[sl][i] && hipEventElapsedTime(&v, tm.ev[sl][i][0], tm.ev[sl][i][1]) == hipSuccess) sum += v;
+    }
+    ms[i] = tm.steps > 0 ? sum / tm.steps : 0.0;
+  }
+  (void)hipGetLastError();  // never leave a timing error sticky for the next launch check
   return CVXG_OK;
 }
 

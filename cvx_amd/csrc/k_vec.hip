@@ -765,6 +765,25 @@ void launch_ctrl_set(hipStream_t s, DevCtrl* ctrl, int which, double v) { k_ctrl
 void launch_ctrl_reset_eval(hipStream_t s, DevCtrl* ctrl) { k_ctrl_reset_eval<<<1, 1, 0, s>>>(ctrl); }
 void launch_ctrl_reset_chol(hipStream_t s, DevCtrl* ctrl) { k_ctrl_reset_chol<<<1, 1, 0, s>>>(ctrl); }
 
+// A host read without a stream synchronisation: one workgroup copies up to two device ranges (8-byte words) into
+// coherent (fine-grained) pinned host memory, makes its stores visible at system scope, then raises the sequence word
+// the host spins on (cvxg.cpp: host_read).  Vector stores only.
+__global__ __launch_bounds__(256) void k_publish(const unsigned long long* __restrict__ s0, unsigned long long* d0, int w0,
+                                                 const unsigned long long* __restrict__ s1, unsigned long long* d1,
+                                                 int w1, unsigned* flag, unsigned seq) {
+  for (int i = threadIdx.x; i < w0; i += blockDim.x) d0[i] = s0[i];
+  for (int i = threadIdx.x; i < w1; i += blockDim.x) d1[i] = s1[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+void launch_publish(hipStream_t s, const void* s0, void* d0, size_t bytes0, const void* s1, void* d1, size_t bytes1,
+                    unsigned* flag, unsigned seq) {
+  k_publish<<<1, 256, 0, s>>>(static_cast<const unsigned long long*>(s0), static_cast<unsigned long long*>(d0),
+                              (int)(bytes0 / 8), static_cast<const unsigned long long*>(s1),
+                              static_cast<unsigned long long*>(d1), (int)(bytes1 / 8), flag, seq);
+}
+
 // rhs[i*nrhs + col] = d_i * sgn * v_i   (d*b with b = -grad for the Newton system)
 __global__ void k_scaled_col(const double* __restrict__ d, const double* __restrict__ v, double sgn, int n, int np,
                              int nrhs, int col, double* __restrict__ rhs) {

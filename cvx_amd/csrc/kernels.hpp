@@ -199,6 +199,10 @@ namespace cvxg {
 void launch_ctrl_set(hipStream_t s, DevCtrl* ctrl, int which, double v);
 void launch_ctrl_reset_eval(hipStream_t s, DevCtrl* ctrl);
 void launch_ctrl_reset_chol(hipStream_t s, DevCtrl* ctrl);
+// copy two device ranges (multiples of 8 bytes; bytes1 may be 0) into coherent host memory (device-side addresses),
+// then *flag = seq (system scope)
+void launch_publish(hipStream_t s, const void* s0, void* d0, size_t bytes0, const void* s1, void* d1, size_t bytes1,
+                    unsigned* flag, unsigned seq);
 void launch_scaled_col(hipStream_t s, const double* d, const double* v, double sgn, int n, int np, int nrhs, int col,
                        double* rhs);
 void launch_kkt_prep(hipStream_t s, const double* Aeq, int ld, int p, int n, int np, const double* d, double* B,

@@ -260,7 +260,12 @@ class Engine:
         self._check(self.lib.cvxg_set_ruiz_lookahead(self.h, int(sweeps), C.byref(n)))
         return n.value
 
+    def last_error(self) -> str:
+        """cvxg_last_error: the message of this context's last failing call."""
+        return self.lib.cvxg_last_error(self.h).decode()
+
     def phase_times(self) -> np.ndarray:
+        """cvxg_get_phase_times: per-step mean device time (ms) of each phase since set_timing(True)."""
         ms = np.zeros(8)
         self._check(self.lib.cvxg_get_phase_times(self.h, _dp(ms), 8))
         return ms

@@ -281,9 +281,11 @@ int cvxg_affine_map(cvxg_ctx* dst, const double* u, double* x);
 
 /* ---- instrumentation ----------------------------------------------------------------------------- */
 
-/* Per-phase device time of the last cvxg_newton_step (ms), measured with HIP events on the ctx
- * stream when timing is enabled: [0] assembly (GEMVs+SYRK) [1] Ruiz+scale [2] Cholesky (+fused forward
- * solve) [3] backward solve + residual [4] line search [5] SYRK kernel alone. */
+/* Per-phase device time (ms), the mean per Newton step (or PD iteration) over the steps since timing was enabled (at
+ * most the last 63), measured with HIP events on the stream each phase runs on; the steps never wait on them (only
+ * this call synchronises): [0] assembly when not prefetched [1] Ruiz+scale [2] Cholesky (+fused forward solve)
+ * [3] backward solve + residual [4] line search [5] the assembly SYRK alone (on its own stream when it was launched
+ * behind the previous evaluation). */
 int cvxg_set_timing(cvxg_ctx* ctx, int enabled);
 int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count);
 

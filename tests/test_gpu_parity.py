@@ -1488,7 +1488,7 @@ def test_batch_full_size_contexts_share_one_gpu(mods):
     got_steps = [[], [], [], []]
     for _ in range(2):
         infos, st = batch_newton_step(engs, pars)
-        assert st == [0, 0, 0, 0]
+        assert st == [0, 0, 0, 0], [e.last_error() for e in engs]
         for i, inf in enumerate(infos):
             got_steps[i].append(tuple(getattr(inf, f) for f in fields))
     for i, e in enumerate(engs):
@@ -1497,7 +1497,7 @@ def test_batch_full_size_contexts_share_one_gpu(mods):
     for e, spec in zip(engs, specs):
         e.set_x(spec["x0"])
     sols, st = batch_barrier_solve(engs, pars, 0)
-    assert st == [0, 0, 0, 0]
+    assert st == [0, 0, 0, 0], [e.last_error() for e in engs]
     for i, (e, s) in enumerate(zip(engs, sols)):
         _, _, x, steps, outer, gap = ref[i]
         assert np.array_equal(e.get_x(), x), i
