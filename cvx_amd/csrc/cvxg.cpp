@@ -166,6 +166,12 @@ struct cvxg_ctx {
   hipStream_t s2 = nullptr;
   hipEvent_t ev_w = nullptr, ev_h = nullptr;
   bool h_valid = false;
+  // The line search's setup (A s, P s, their dots) and first trial batch, enqueued behind each factorization attempt
+  // of a Newton step with s = dx (the trust radius does not clamp in the common case), so the attempt's host read
+  // carries them: spec_allowed (set by cvxg_newton_step), spec_launched (this attempt enqueued them), spec_have (the
+  // last host read holds them for the current dx).
+  bool spec_allowed = false, spec_launched = false, spec_have = false;
+  double spec_beta = 0.5;
   double* spart = nullptr;  // SYRK split-K partials (ctx->part belongs to the evaluation's A'(1/d))
   // affine re-parametrisation (cvxg_affine_from): x = z0 + F u with F (aff_n x n, column-major, ld aff_n)
   double *aff_F = nullptr, *aff_z0 = nullptr;
@@ -702,16 +708,23 @@ static void ruiz_learn(cvxg_ctx* ctx, int sweeps) {
 template <class F, class G>
 static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G after) {
   hipStream_t s = ctx->s;
-  launch_ctrl_set(s, ctx->ctrl, 1, reg);
-  launch_ctrl_reset_chol(s, ctx->ctrl);
+  launch_factor_prep(s, ctx->ctrl, reg, ctx->df_work, chol_dataflow_work_ints(ctx->nblk));  // reg, chol fields, work
   launch_form_q(s, ctx->H, ctx->L, ctx->np, ctx->n, ctx->np, ctx->dfin, ctx->ctrl);
   fill_rhs();
   // the whole factorization as one persistent launch over the 64 x 64 tile DAG (k_dataflow.hip)
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
-                       ctx->df_ntasks, ctx->ncu, ctx->df_trace);
+                       ctx->df_ntasks, ctx->ncu, ctx->df_trace, false);
+  ctx->spec_launched = false;
   after();
   HIPC(ctx, hipGetLastError());
-  CHK(sync_ctrl(ctx));
+  if (ctx->spec_launched) {  // the control block and the speculative line-search batch in one host read
+    CHK(host_read(ctx, ctx->ctrl, ctx->hctrl_dev, sizeof(DevCtrl), ctx->ls_log, ctx->hls_dev,
+                  5 * LS_TRIALS * sizeof(double)));
+  } else {
+    CHK(sync_ctrl(ctx));
+  }
+  ctx->spec_have = ctx->spec_launched;
+  ctx->spec_launched = false;
   if (ctx->hctrl->df_status != 0)
     return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
   if (ctx->df_trace) {  // instrumentation only: task order + timeline of this factorization
@@ -759,6 +772,9 @@ static void backward_solve(cvxg_ctx* ctx, int nrhs) {
                       ++ctx->bwd_gen, ctx->ctrl);
 }
 
+static void ls_setup_launch(cvxg_ctx* ctx);
+static void ls_batch_launch(cvxg_ctx* ctx, double tbase, double beta);
+
 // MatrixUtils.choleskySolve(H, b = -grad, tol) (MatrixUtils.scala:468-516); result in ctx->dx.
 static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
   hipStream_t s = ctx->s;
@@ -782,6 +798,13 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
     db.add(DOT_FMA, ctx->dx, ctx->y, ctx->np, SC_Q);
     launch_dots(s, db, ctx->ctrl);
     tstop(ctx, 3);
+    if (ctx->spec_allowed) {  // the line search's setup and first batch for s = dx ride this attempt's host read
+      tstart(ctx, 4);
+      (void)hipMemcpyAsync(ctx->sdir, ctx->dx, (size_t)ctx->np * sizeof(double), hipMemcpyDeviceToDevice, s);
+      ls_setup_launch(ctx);
+      ls_batch_launch(ctx, 1.0, ctx->spec_beta);
+      ctx->spec_launched = true;
+    }
   };
   int rc = regularized_cholesky(
       ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, ctx->y, -1.0, ctx->n, ctx->np, 1, 0, ctx->rhs); }, &reg, &mind,
@@ -872,6 +895,7 @@ static int newton_direction_p0(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step
   info->fallback = 1;
   if (rc == CVXG_OK || rc == CVXG_E_HIP) return rc;
   info->fallback = 2;
+  ctx->spec_have = false;  // (the speculative line-search setup belonged to a rejected direction)
   // symSolve(H, -y) (UnconstrainedSolver.scala:64)
   CHK(eig_alloc(ctx));
   HIPC(ctx, hipMemsetAsync(ctx->eig_b, 0, (size_t)ctx->eig_ldm * sizeof(double), ctx->s));
@@ -1124,6 +1148,30 @@ static int ls_objective_trials(cvxg_ctx* ctx, double tbase, double beta, TrialBa
   return CVXG_OK;
 }
 
+// Launch one batch of LS_TRIALS trials t_k = tbase beta^k (inequality rows: the counts and log sums into ls_log).
+static void ls_batch_launch(cvxg_ctx* ctx, double tbase, double beta) {
+  const int nb = ls_blocks(ctx->m);
+  const bool cert = ls_certified(ctx);
+  launch_ls_trials(ctx->s, ctx->c, ctx->e, ctx->ub, ctx->m, tbase, beta, ctx->ls_plog, ctx->ls_pcnt,
+                   ctx->nq > 0 ? ctx->qf : nullptr, cert ? ctx->cabs : nullptr, ctx->eabs, ls_gamma(ctx),
+                   ctx->ls_paux, (cert && ctx->nq > 0) ? ctx->qfabs : nullptr);
+  launch_ls_finalize(ctx->s, ctx->ls_plog, ctx->ls_pcnt, ctx->ls_paux, nb, ctx->ls_log, ctx->ls_cnt);
+}
+// The batch from its host copy (hls).
+static void ls_batch_parse(const cvxg_ctx* ctx, int k0, TrialBatch* b) {
+  b->k0 = k0;
+  const int* cnt = (const int*)(ctx->hls + 3 * LS_TRIALS);
+  for (int k = 0; k < LS_TRIALS; ++k) {
+    b->logs[k] = ctx->hls[3 * k];
+    b->lerr[k] = ctx->hls[3 * k + 1];
+    b->labs[k] = ctx->hls[3 * k + 2];
+    b->viol[k] = cnt[4 * k];
+    b->npos[k] = cnt[4 * k + 1];
+    b->sure[k] = cnt[4 * k + 2];
+    b->amb[k] = cnt[4 * k + 3];
+  }
+}
+
 static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch* b) {
   if (ctx->m == 0) {  // no inequality constraints: every trial is in C and contributes no log terms
     CHK(ls_objective_trials(ctx, tbase, beta, b));
@@ -1136,33 +1184,15 @@ static int ls_batch(cvxg_ctx* ctx, int k0, double tbase, double beta, TrialBatch
     return CVXG_OK;
   }
   CHK(ls_objective_trials(ctx, tbase, beta, b));
-  const int nb = ls_blocks(ctx->m);
-  const bool cert = ls_certified(ctx);
-  launch_ls_trials(ctx->s, ctx->c, ctx->e, ctx->ub, ctx->m, tbase, beta, ctx->ls_plog, ctx->ls_pcnt,
-                   ctx->nq > 0 ? ctx->qf : nullptr, cert ? ctx->cabs : nullptr, ctx->eabs, ls_gamma(ctx),
-                   ctx->ls_paux, (cert && ctx->nq > 0) ? ctx->qfabs : nullptr);
-  launch_ls_finalize(ctx->s, ctx->ls_plog, ctx->ls_pcnt, ctx->ls_paux, nb, ctx->ls_log, ctx->ls_cnt);
+  ls_batch_launch(ctx, tbase, beta);
   HIPC(ctx, hipGetLastError());
   if (ctx->kl || ctx->klp) {  // (their trial sums went out by hipMemcpyAsync into the host-stack batch)
-    HIPC(ctx, hipMemcpyAsync(ctx->hls, ctx->ls_log, 3 * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
-    HIPC(ctx, hipMemcpyAsync((int*)(ctx->hls + 3 * LS_TRIALS), ctx->ls_cnt, 4 * LS_TRIALS * sizeof(int),
-                             hipMemcpyDeviceToHost, ctx->s));
+    HIPC(ctx, hipMemcpyAsync(ctx->hls, ctx->ls_log, 5 * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost, ctx->s));
     HIPC(ctx, hipStreamSynchronize(ctx->s));
   } else {
-    CHK(host_read(ctx, ctx->ls_log, ctx->hls_dev, 3 * LS_TRIALS * sizeof(double), ctx->ls_cnt,
-                  ctx->hls_dev + 3 * LS_TRIALS, 4 * LS_TRIALS * sizeof(int)));
+    CHK(host_read(ctx, ctx->ls_log, ctx->hls_dev, 5 * LS_TRIALS * sizeof(double)));
   }
-  b->k0 = k0;
-  const int* cnt = (const int*)(ctx->hls + 3 * LS_TRIALS);
-  for (int k = 0; k < LS_TRIALS; ++k) {
-    b->logs[k] = ctx->hls[3 * k];
-    b->lerr[k] = ctx->hls[3 * k + 1];
-    b->labs[k] = ctx->hls[3 * k + 2];
-    b->viol[k] = cnt[4 * k];
-    b->npos[k] = cnt[4 * k + 1];
-    b->sure[k] = cnt[4 * k + 2];
-    b->amb[k] = cnt[4 * k + 3];
-  }
+  ls_batch_parse(ctx, k0, b);
   return CVXG_OK;
 }
 
@@ -1227,13 +1257,11 @@ static int trial_fresh(cvxg_ctx* ctx, double tt, FreshTrial* out) {
 //    among themselves).  It is taken from the batch value and counted in *ties.  (Deciding these from a fresh
 //    evaluation was measured: late in the path -- t = 1e10 -- the noise then rejected trial after trial and a
 //    centering ran into maxIter.)
-static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int limit, double* t_out, int* k_c,
-                       int* k_a, int* fresh, int* ties) {
+// e = A s (and |A||s|), and the quadratic pieces of f0(x + s t), s = ctx->sdir: launches only.
+static void ls_setup_launch(cvxg_ctx* ctx) {
   hipStream_t s = ctx->s;
-  const double beta = pars->beta, alpha = pars->alpha;
   const bool cert = ls_certified(ctx);
   const bool quad = ctx->hasP && !ctx->kl;
-  // e = A s (and |A||s|), and the quadratic pieces of f0(x + s t)
   if (ctx->m > 0) {
     if (cert) launch_rowdot_abs(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e, ctx->eabs);
     else launch_rowdot(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e);
@@ -1269,8 +1297,20 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
     }
   }
   launch_dots(s, db, ctx->ctrl);
-  HIPC(ctx, hipGetLastError());
-  CHK(sync_ctrl(ctx));
+}
+
+// use_spec: the setup and the first batch went out behind the factorization (cholesky_solve) and arrived with its host
+// read; otherwise they are launched here.
+static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int limit, double* t_out, int* k_c,
+                       int* k_a, int* fresh, int* ties, bool use_spec) {
+  const double beta = pars->beta, alpha = pars->alpha;
+  const bool cert = ls_certified(ctx);
+  const bool quad = ctx->hasP && !ctx->kl;
+  if (!use_spec) {
+    ls_setup_launch(ctx);
+    HIPC(ctx, hipGetLastError());
+    CHK(sync_ctrl(ctx));
+  }
   const DevCtrl h = *ctx->hctrl;
   const double tb = ctx->t, f = ctx->f_at_x;
   // r + a.(x+st) + (x+st)'P(x+st)/2, or w.(z+st) + R.exp(-B'(z+st)), or the KL primal (x+st).log(n (x+st))
@@ -1299,6 +1339,11 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
   double tcur = 1.0;
   double tbatch = 1.0;  // t at the start of the next batch (products of beta, UnconstrainedSolver.scala:93)
   int next_k0 = 0;
+  if (use_spec) {  // batch 0 (t = 1 ... beta^63) is already on the host
+    ls_batch_parse(ctx, 0, &b);
+    for (int i = 0; i < LS_TRIALS; ++i) tbatch *= beta;
+    next_k0 = LS_TRIALS;
+  }
   auto ensure = [&](int k) -> int {
     while (!(b.k0 >= 0 && k >= b.k0 && k < b.k0 + LS_TRIALS)) {
       CHK(ls_batch(ctx, next_k0, tbatch, beta, &b));
@@ -1496,8 +1541,8 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   CHK(dalloc(ctx, &ctx->ls_plog, (size_t)lsb * LS_TRIALS));
   CHK(dalloc(ctx, &ctx->ls_paux, (size_t)lsb * LS_TRIALS * 2));
   CHK(dalloc(ctx, &ctx->ls_pcnt, (size_t)lsb * LS_TRIALS * 4));
-  CHK(dalloc(ctx, &ctx->ls_log, 3 * LS_TRIALS));
-  CHK(dalloc(ctx, &ctx->ls_cnt, 4 * LS_TRIALS));
+  CHK(dalloc(ctx, &ctx->ls_log, 5 * LS_TRIALS));  // {log sums} then the counts as ints: one host read for both
+  ctx->ls_cnt = reinterpret_cast<int*>(ctx->ls_log + 3 * LS_TRIALS);
   for (double** v : {&ctx->Pxa, &ctx->Psa, &ctx->xtr, &ctx->Pxtr}) CHK(dalloc(ctx, v, np));
   for (double** v : {&ctx->cabs, &ctx->eabs, &ctx->c_tr, &ctx->d_tr, &ctx->invd_tr, &ctx->w_tr, &ctx->logd_tr})
     CHK(dalloc(ctx, v, mp));
@@ -1522,7 +1567,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
                   ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
-                  ctx->ls_log, ctx->ls_pcnt, ctx->ls_cnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
+                  ctx->ls_log, ctx->ls_pcnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,
                   ctx->kl_negBy, ctx->kl_part, ctx->kl_ls, ctx->As, ctx->wd, ctx->didx, ctx->sp_ptr,
@@ -1972,14 +2017,19 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
   const double tol = pars->tolSolver;
   info->f = ctx->f_at_x;
   info->norm_grad = ctx->normGrad;
+  ctx->spec_allowed = ctx->p == 0 && ctx->m > 0 && !ctx->kl && !ctx->klp;
+  ctx->spec_beta = pars->beta;
+  ctx->spec_have = false;
   int rc = newton_direction(ctx, pars, info);
+  ctx->spec_allowed = false;
+  const bool spec = ctx->spec_have;
+  ctx->spec_have = false;
   if (rc != CVXG_OK) return rc;
   const double q = ctx->hctrl->sc[SC_Q];
   ctx->nd = -q / 2;
   info->q = q;
   info->newton_decrement = ctx->nd;
   if (ctx->nd > tol) {
-    tstart(ctx, 4);
     double scale = 1.0;
     int limit = 100;
     if (ctx->p == 0) {
@@ -1991,14 +2041,17 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
       if (!(ctx->iter == 0 || hNorm <= ctx->trust)) scale = ctx->trust / hNorm;
       limit = 200;
     }
-    if (scale == 1.0) {
+    const bool use_spec = spec && scale == 1.0;  // s = dx: the setup and first batch are already on the host
+    if (!use_spec) tstart(ctx, 4);  // (else phase 4 began with the speculative launches)
+    if (use_spec) {
+    } else if (scale == 1.0) {
       HIPC(ctx, hipMemcpyAsync(ctx->sdir, ctx->dx, ctx->np * sizeof(double), hipMemcpyDeviceToDevice, ctx->s));
     } else {
       launch_axpy_strided(ctx->s, nullptr, ctx->dx, 1, 0, scale, ctx->np, ctx->sdir);  // d * (radius/hNorm)
     }
     double tacc = 1.0;
     int kc = 0, ka = 0, fresh = 0, ties = 0;
-    rc = line_search(ctx, pars, q, limit, &tacc, &kc, &ka, &fresh, &ties);
+    rc = line_search(ctx, pars, q, limit, &tacc, &kc, &ka, &fresh, &ties, use_spec);
     info->ls_fresh = fresh;
     info->ls_ties = ties;
     tstop(ctx, 4);

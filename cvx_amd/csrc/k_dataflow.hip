@@ -580,8 +580,8 @@ size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1)
 
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
-                          unsigned long long* trace) {
-  (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
+                          unsigned long long* trace, bool zero_work) {
+  if (zero_work) (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
   k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace);
 }
 

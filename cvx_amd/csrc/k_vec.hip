@@ -764,6 +764,19 @@ __global__ void k_ctrl_reset_chol(DevCtrl* ctrl) {
 void launch_ctrl_set(hipStream_t s, DevCtrl* ctrl, int which, double v) { k_ctrl_set<<<1, 1, 0, s>>>(ctrl, which, v); }
 void launch_ctrl_reset_eval(hipStream_t s, DevCtrl* ctrl) { k_ctrl_reset_eval<<<1, 1, 0, s>>>(ctrl); }
 void launch_ctrl_reset_chol(hipStream_t s, DevCtrl* ctrl) { k_ctrl_reset_chol<<<1, 1, 0, s>>>(ctrl); }
+__global__ void k_factor_prep(DevCtrl* ctrl, double reg, int* __restrict__ work, int nwork) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nwork) work[i] = 0;
+  if (i == 0) {
+    ctrl->reg = reg;
+    ctrl->chol_info = 0;
+    ctrl->df_status = 0;
+    ctrl->min_diag = (unsigned long long)__double_as_longlong(__builtin_inf());
+  }
+}
+void launch_factor_prep(hipStream_t s, DevCtrl* ctrl, double reg, int* work, size_t nwork) {
+  k_factor_prep<<<(unsigned)((nwork + 255) / 256), 256, 0, s>>>(ctrl, reg, work, (int)nwork);
+}
 
 // A host read without a stream synchronisation: one workgroup copies up to two device ranges (8-byte words) into
 // coherent (fine-grained) pinned host memory, makes its stores visible at system scope, then raises the sequence word

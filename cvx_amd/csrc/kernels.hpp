@@ -128,7 +128,8 @@ void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double*
 size_t chol_dataflow_work_ints(int nblk);
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
-                          unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */);
+                          unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */,
+                          bool zero_work = true /* false: launch_factor_prep zeroed it */);
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
 size_t bwd_work_ints(int nblk);  // flag words + the data-tagged u granules of k_bwd_dataflow
 void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,
@@ -199,6 +200,8 @@ namespace cvxg {
 void launch_ctrl_set(hipStream_t s, DevCtrl* ctrl, int which, double v);
 void launch_ctrl_reset_eval(hipStream_t s, DevCtrl* ctrl);
 void launch_ctrl_reset_chol(hipStream_t s, DevCtrl* ctrl);
+// one launch before a factorization attempt: ctrl->reg = reg, the chol fields reset, the dataflow work words zeroed
+void launch_factor_prep(hipStream_t s, DevCtrl* ctrl, double reg, int* work, size_t nwork);
 // copy two device ranges (multiples of 8 bytes; bytes1 may be 0) into coherent host memory (device-side addresses),
 // then *flag = seq (system scope)
 void launch_publish(hipStream_t s, const void* s0, void* d0, size_t bytes0, const void* s1, void* d1, size_t bytes1,
