@@ -159,9 +159,9 @@ struct cvxg_ctx {
   double eqGap = 0.0;
   double f_at_x = 0.0;    // barrier value at x
   int x_eval_valid = 0;   // c/d/w/y/scalars correspond to the current x and t
-  // The next step's Hessian assembly, launched on s2 as soon as the step's constraint values (w) exist, so it runs
-  // beside the rest of the evaluation (P x, A'(1/d), the gradient, the reductions) and the host's read of them;
-  // s waits on ev_h right after that read, so all later work on s is ordered behind it.  h_valid: H holds the
+  // The next step's Hessian assembly, launched on the main stream as soon as the step's constraint values (w) exist,
+  // while the rest of the evaluation (P x, A'(1/d), the gradient, the reductions) and the host's read of it run on s2
+  // behind ev_w; the main stream then waits on ev_h (that tail) only if it has not finished.  h_valid: H holds the
   // assembly at the current x and t (x_eval_valid too).
   hipStream_t s2 = nullptr;
   hipEvent_t ev_w = nullptr, ev_h = nullptr;
@@ -236,14 +236,15 @@ static int copy_sync(cvxg_ctx* ctx, void* dst, const void* src, size_t bytes, hi
 // synchronisation's wake-up left the GPU idle ~20-30 us per read, profiles/r03 timeline).  A failed launch or a
 // faulted stream ends the spin through hipStreamQuery.
 static int host_read(cvxg_ctx* ctx, const void* s0, void* d0, size_t b0, const void* s1 = nullptr, void* d1 = nullptr,
-                     size_t b1 = 0) {
+                     size_t b1 = 0, hipStream_t st = nullptr) {
+  if (!st) st = ctx->s;
   const unsigned seq = ++ctx->hseq;
-  launch_publish(ctx->s, s0, d0, b0, s1, d1, b1, ctx->hflag_dev, seq);
+  launch_publish(st, s0, d0, b0, s1, d1, b1, ctx->hflag_dev, seq);
   HIPC(ctx, hipGetLastError());
   for (unsigned spins = 0;; ++spins) {
     if (__atomic_load_n(ctx->hflag, __ATOMIC_ACQUIRE) == seq) break;
     if ((spins & 1023) == 1023) {
-      const hipError_t q = hipStreamQuery(ctx->s);
+      const hipError_t q = hipStreamQuery(st);
       if (q == hipSuccess) {  // the stream drained: the word must be there (re-read once, then report)
         if (__atomic_load_n(ctx->hflag, __ATOMIC_ACQUIRE) == seq) break;
         return set_err(ctx, CVXG_E_HIP, "host_read: stream idle but the sequence word was not published");
@@ -535,17 +536,18 @@ static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false) {
   constraint_eval_all(ctx);
   ctx->h_valid = false;
   prefetch = prefetch && !ctx->kl && !ctx->klp;  // (their Hessians need the evaluation's y / diag(1/x) first)
-  if (prefetch) {  // the assembly needs w (and the quadratic rows' P_k x) only
+  if (prefetch) {  // the assembly needs w (and the quadratic rows' P_k x) only: it stays on the main stream, and the
+                   // rest of the evaluation moves to s2 behind the constraint values
     HIPC(ctx, hipEventRecord(ctx->ev_w, s));
     HIPC(ctx, hipStreamWaitEvent(ctx->s2, ctx->ev_w, 0));
     const int nx = (ctx->tm.tick + 1) % TRING;  // timed as phase 5 of the step that will use it
-    if (ctx->tm.on) HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][0], ctx->s2));
-    CHK(assemble_hessian(ctx, nullptr, nullptr, ctx->s2));
+    if (ctx->tm.on) HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][0], s));
+    CHK(assemble_hessian(ctx, nullptr, nullptr, s));
     if (ctx->tm.on) {
-      HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][1], ctx->s2));
+      HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][1], s));
       ctx->tm.rec[nx][5] = ctx->tm.pf5 = true;
     }
-    HIPC(ctx, hipEventRecord(ctx->ev_h, ctx->s2));
+    s = ctx->s2;
   }
   const bool quad = ctx->hasP && !ctx->kl;
   const bool cert = ls_certified(ctx);
@@ -594,9 +596,18 @@ static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false) {
     launch_dot(s, ctx->eqd, nullptr, ctx->p, ctx->ctrl, SC_EQ2);
   }
   HIPC(ctx, hipGetLastError());
-  const int rc_sync = sync_ctrl(ctx);
+  if (prefetch) HIPC(ctx, hipEventRecord(ctx->ev_h, s));  // the end of the evaluation's tail (before its publish)
+  const int rc_sync = host_read(ctx, ctx->ctrl, ctx->hctrl_dev, sizeof(DevCtrl), nullptr, nullptr, 0, s);
   if (prefetch) {
-    HIPC(ctx, hipStreamWaitEvent(s, ctx->ev_h, 0));  // everything later on s follows the assembly
+    // the main stream (with the assembly) waits on the evaluation's tail only if it has not finished -- the host read
+    // above has just seen it finish, so normally there is no cross-queue wait (a barrier packet costs 15-25 us on the
+    // main stream, profiles/r03 timeline)
+    hipError_t q = hipEventQuery(ctx->ev_h);
+    for (int spins = 0; q == hipErrorNotReady && spins < 4096; ++spins) {
+      __builtin_ia32_pause();
+      q = hipEventQuery(ctx->ev_h);
+    }
+    if (q != hipSuccess) HIPC(ctx, hipStreamWaitEvent(ctx->s, ctx->ev_h, 0));
     ctx->h_valid = rc_sync == CVXG_OK;
   }
   CHK(rc_sync);
@@ -800,7 +811,7 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
     tstop(ctx, 3);
     if (ctx->spec_allowed) {  // the line search's setup and first batch for s = dx ride this attempt's host read
       tstart(ctx, 4);
-      (void)hipMemcpyAsync(ctx->sdir, ctx->dx, (size_t)ctx->np * sizeof(double), hipMemcpyDeviceToDevice, s);
+      launch_axpy_strided(s, nullptr, ctx->dx, 1, 0, 1.0, ctx->np, ctx->sdir);  // s = dx (a kernel: no blit gap)
       ls_setup_launch(ctx);
       ls_batch_launch(ctx, 1.0, ctx->spec_beta);
       ctx->spec_launched = true;

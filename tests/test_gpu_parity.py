@@ -579,6 +579,28 @@ def test_equality_kkt_direction_any_p(mods, n, p, fused, monkeypatch):
     eng.close()
 
 
+def test_equality_kkt_direction_c3_size(mods):
+    """The KKT equality block at the bench's C3EQ size (n = 4096, m = 8192, p = 64: the many-column dataflow solves
+    with L and L' over 64 block rows, R = B X on MFMA, the one-wave Schur factorization) against the oracle's
+    KKTSystem.solve (KKTSystem.scala:43-167): dx within 1e-8 and w within 1e-7 at t = 1."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp_eq(4096, 8192, 64, instance=5)
+    pb = _opb(O, spec)
+    eng = _engine(Engine, spec)
+    pars = SP.standardParams()
+    x = spec["x0"]
+    dx, w, info = eng.newton_direction(pars, 1.0, x)
+    eng.close()
+    assert info.fallback == 0
+    y = O.barrier_gradient(pb, 1.0, x)
+    H = O.barrier_hessian(pb, 1.0, x, literal="blas")  # the literal rank-1 fold takes minutes at this size
+    dref, wref = O.kkt_solve(H, pb.Aeq, y, pb.beq - pb.Aeq @ x, pars.tolEqSolve)
+    rel_dx = np.linalg.norm(dx - dref) / np.linalg.norm(dref)
+    rel_w = np.linalg.norm(w - wref) / np.linalg.norm(wref)
+    print(f"C3EQ64 direction: rel dx {rel_dx:.2e}, rel w {rel_w:.2e}")
+    assert rel_dx < 1e-8 and rel_w < 1e-7
+
+
 def test_equality_barrier_solve_wide_p_vs_oracle(mods):
     """A whole equality-constrained barrier solve (EqualityConstrainedSolver, BarrierSolver.solveWithEQs) with p = 12
     on the KKT path: final x within 1e-6 of the oracle's, equality gap and duality gap below tol."""
