@@ -302,8 +302,9 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
         while done < steps:
             done += pd_solve()
         steps = done
+    full_steps = 0  # timed steps whose line search accepted t = 1 (their next evaluation rides the search's sweep)
     for _ in range(0 if wl.endswith("PD") else steps):
-        one_step()
+        full_steps += int(one_step().step == 1.0)
     sync()
     D.barrier(device)
     elapsed = time.perf_counter() - t0
@@ -379,6 +380,7 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
         "kkt_factor_solve_per_s": 1e3 / kkt_ms if kkt_ms > 0 else None,
         "cholesky_tflops": tf(n ** 3 / 3, chol),
         "ruiz_lookahead_reruns": ruiz_reruns,
+        "ls_full_steps": full_steps,
         "gathered_ranks": len(gathered),
     }
     return out, gathered

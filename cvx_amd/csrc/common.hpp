@@ -28,6 +28,8 @@ struct DevCtrl {
   unsigned long long pd_s0;       // bits of the primal-dual step bound s0 (PrimalDualSolver.scala:331-338)
   unsigned long long ruiz_rho[RUIZ_MAX + 2];
   double sc[40];                  // reduced scalars, see SC_* below
+  int spec_infeasible;            // the speculative evaluation at x + s (k_ls_setup_eval): its infeasible / not_strict
+  int spec_not_strict;
 };
 
 enum {
@@ -64,6 +66,16 @@ enum {
   SC_COUNT
 };
 static_assert(SC_COUNT <= 40, "DevCtrl::sc too small");
+
+// Bounded waits of the inter-workgroup hand-offs: a waiting workgroup gives up (and raises its abort / failure
+// signal) after SPIN_LIMIT_TICKS of wall time on the 100 MHz real-time counter -- never a hung GPU on a scheduling
+// bug, and no false alarm when other contexts' kernels share the device (a poll count bound fired under a batch of
+// concurrent factorizations).  Callers test it every 256 polls.
+constexpr unsigned long long SPIN_LIMIT_TICKS = 500000000ull;  // 5 s
+__device__ __forceinline__ unsigned long long spin_clock() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ bool spin_expired(unsigned spins, unsigned long long t0) {
+  return (spins & 255u) == 255u && spin_clock() - t0 > SPIN_LIMIT_TICKS;
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

@@ -95,6 +95,10 @@ struct cvxg_ctx {
   double *cabs = nullptr, *eabs = nullptr, *Pxa = nullptr, *Psa = nullptr;
   double *xtr = nullptr, *Pxtr = nullptr, *c_tr = nullptr, *d_tr = nullptr, *invd_tr = nullptr, *w_tr = nullptr,
          *logd_tr = nullptr;
+  // the speculative evaluation at x1 = x + dx (k_ls_setup_eval), swapped with c/d/invd/w/logd/cabs when the line
+  // search accepts t = 1
+  double *x1 = nullptr, *c1 = nullptr, *d1 = nullptr, *invd1 = nullptr, *w1 = nullptr, *logd1 = nullptr,
+         *cabs1 = nullptr;
   int* tiles = nullptr;
   int ntiles = 0, nsplit = 1;
   int ntiles_main = 0;  // tiles assembled without K split (whole waves of slots); the rest use nsplit
@@ -171,6 +175,8 @@ struct cvxg_ctx {
   // carries them: spec_allowed (set by cvxg_newton_step), spec_launched (this attempt enqueued them), spec_have (the
   // last host read holds them for the current dx).
   bool spec_allowed = false, spec_launched = false, spec_have = false;
+  // spec_eval_*: the setup's sweep over A also evaluated the constraints at x + dx (linear rows only)
+  bool spec_eval_launched = false, spec_eval_have = false;
   double spec_beta = 0.5;
   double* spart = nullptr;  // SYRK split-K partials (ctx->part belongs to the evaluation's A'(1/d))
   // affine re-parametrisation (cvxg_affine_from): x = z0 + F u with F (aff_n x n, column-major, ld aff_n)
@@ -529,11 +535,28 @@ static void constraint_eval_all(cvxg_ctx* ctx) {
 // Barrier value / gradient pieces at the current x and ctrl->t (BarrierSolver.scala:280-301):
 // c, d, w, invd, logd, Px, y, eqDiff, and sc[A0X, XPX, SUMLOG, GG, EQ2].
 static int assemble_hessian(cvxg_ctx* ctx, const double* wts, const double* qw, hipStream_t st);
-static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false) {
+// The setup sweep of a speculative line search also evaluates the constraints at x + dx (k_ls_setup_eval): linear
+// rows, certified line search.
+static bool spec_eval_ok(const cvxg_ctx* ctx) {
+  return ls_certified(ctx) && ctx->nq == 0 && !ctx->kl && !ctx->klp && ctx->p == 0;
+}
+// taken: the line search accepted t = 1 along s = dx, and the speculative evaluation at x1 = x + dx (bitwise the
+// x + s t of the step) is the constraint evaluation at the new x
+static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false) {
   hipStream_t s = ctx->s;
   const int np = ctx->np, mp = ctx->mp;
-  launch_ctrl_reset_eval(s, ctx->ctrl);
-  constraint_eval_all(ctx);
+  if (taken) {
+    std::swap(ctx->c, ctx->c1);
+    std::swap(ctx->d, ctx->d1);
+    std::swap(ctx->invd, ctx->invd1);
+    std::swap(ctx->w, ctx->w1);
+    std::swap(ctx->logd, ctx->logd1);
+    std::swap(ctx->cabs, ctx->cabs1);
+    launch_ctrl_take_spec(s, ctx->ctrl);
+  } else {
+    launch_ctrl_reset_eval(s, ctx->ctrl);
+    constraint_eval_all(ctx);
+  }
   ctx->h_valid = false;
   prefetch = prefetch && !ctx->kl && !ctx->klp;  // (their Hessians need the evaluation's y / diag(1/x) first)
   if (prefetch) {  // the assembly needs w (and the quadratic rows' P_k x) only: it stays on the main stream, and the
@@ -720,11 +743,11 @@ template <class F, class G>
 static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G after) {
   hipStream_t s = ctx->s;
   launch_factor_prep(s, ctx->ctrl, reg, ctx->df_work, chol_dataflow_work_ints(ctx->nblk));  // reg, chol fields, work
-  launch_form_q(s, ctx->H, ctx->L, ctx->np, ctx->n, ctx->np, ctx->dfin, ctx->ctrl);
   fill_rhs();
-  // the whole factorization as one persistent launch over the 64 x 64 tile DAG (k_dataflow.hip)
+  // the whole factorization as one persistent launch over the 64 x 64 tile DAG (k_dataflow.hip); Q = (d d') o H
+  // (+ reg I) is formed as each tile is first read (no separate k_form_q pass)
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
-                       ctx->df_ntasks, ctx->ncu, ctx->df_trace, false);
+                       ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n);
   ctx->spec_launched = false;
   after();
   HIPC(ctx, hipGetLastError());
@@ -735,7 +758,9 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
     CHK(sync_ctrl(ctx));
   }
   ctx->spec_have = ctx->spec_launched;
+  ctx->spec_eval_have = ctx->spec_launched && ctx->spec_eval_launched;
   ctx->spec_launched = false;
+  ctx->spec_eval_launched = false;
   if (ctx->hctrl->df_status != 0)
     return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
   if (ctx->df_trace) {  // instrumentation only: task order + timeline of this factorization
@@ -783,7 +808,7 @@ static void backward_solve(cvxg_ctx* ctx, int nrhs) {
                       ++ctx->bwd_gen, ctx->ctrl);
 }
 
-static void ls_setup_launch(cvxg_ctx* ctx);
+static void ls_setup_launch(cvxg_ctx* ctx, bool spec_eval = false);
 static void ls_batch_launch(cvxg_ctx* ctx, double tbase, double beta);
 
 // MatrixUtils.choleskySolve(H, b = -grad, tol) (MatrixUtils.scala:468-516); result in ctx->dx.
@@ -811,10 +836,13 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
     tstop(ctx, 3);
     if (ctx->spec_allowed) {  // the line search's setup and first batch for s = dx ride this attempt's host read
       tstart(ctx, 4);
-      launch_axpy_strided(s, nullptr, ctx->dx, 1, 0, 1.0, ctx->np, ctx->sdir);  // s = dx (a kernel: no blit gap)
-      ls_setup_launch(ctx);
+      const bool se = spec_eval_ok(ctx);
+      if (se) launch_spec_prep(s, ctx->dx, ctx->x, ctx->np, ctx->sdir, ctx->x1, ctx->ctrl);  // s = dx, x1 = x + s
+      else launch_axpy_strided(s, nullptr, ctx->dx, 1, 0, 1.0, ctx->np, ctx->sdir);  // s = dx (a kernel: no blit gap)
+      ls_setup_launch(ctx, se);
       ls_batch_launch(ctx, 1.0, ctx->spec_beta);
       ctx->spec_launched = true;
+      ctx->spec_eval_launched = se;
     }
   };
   int rc = regularized_cholesky(
@@ -907,6 +935,7 @@ static int newton_direction_p0(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step
   if (rc == CVXG_OK || rc == CVXG_E_HIP) return rc;
   info->fallback = 2;
   ctx->spec_have = false;  // (the speculative line-search setup belonged to a rejected direction)
+  ctx->spec_eval_have = false;
   // symSolve(H, -y) (UnconstrainedSolver.scala:64)
   CHK(eig_alloc(ctx));
   HIPC(ctx, hipMemsetAsync(ctx->eig_b, 0, (size_t)ctx->eig_ldm * sizeof(double), ctx->s));
@@ -1269,12 +1298,15 @@ static int trial_fresh(cvxg_ctx* ctx, double tt, FreshTrial* out) {
 //    evaluation was measured: late in the path -- t = 1e10 -- the noise then rejected trial after trial and a
 //    centering ran into maxIter.)
 // e = A s (and |A||s|), and the quadratic pieces of f0(x + s t), s = ctx->sdir: launches only.
-static void ls_setup_launch(cvxg_ctx* ctx) {
+static void ls_setup_launch(cvxg_ctx* ctx, bool spec_eval) {
   hipStream_t s = ctx->s;
   const bool cert = ls_certified(ctx);
   const bool quad = ctx->hasP && !ctx->kl;
   if (ctx->m > 0) {
-    if (cert) launch_rowdot_abs(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e, ctx->eabs);
+    if (spec_eval)  // e, eabs and the constraint evaluation at x1 = x + s in one sweep over A
+      launch_ls_setup_eval(s, ctx->A, ctx->np, ctx->mp, ctx->np, ctx->sdir, ctx->x1, ctx->e, ctx->eabs, ctx->r,
+                           ctx->ub, ctx->c1, ctx->d1, ctx->invd1, ctx->w1, ctx->logd1, ctx->cabs1, ctx->ctrl);
+    else if (cert) launch_rowdot_abs(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e, ctx->eabs);
     else launch_rowdot(s, ctx->A, ctx->np, ctx->m, ctx->np, ctx->sdir, ctx->e);
   }
   if (ctx->nq > 0) {  // e_k = G_k.s and f_k = s'P_k s: g_k(x + t s) = g_k + t e_k + t^2 f_k / 2
@@ -1555,8 +1587,10 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   CHK(dalloc(ctx, &ctx->ls_log, 5 * LS_TRIALS));  // {log sums} then the counts as ints: one host read for both
   ctx->ls_cnt = reinterpret_cast<int*>(ctx->ls_log + 3 * LS_TRIALS);
   for (double** v : {&ctx->Pxa, &ctx->Psa, &ctx->xtr, &ctx->Pxtr}) CHK(dalloc(ctx, v, np));
-  for (double** v : {&ctx->cabs, &ctx->eabs, &ctx->c_tr, &ctx->d_tr, &ctx->invd_tr, &ctx->w_tr, &ctx->logd_tr})
+  for (double** v : {&ctx->cabs, &ctx->eabs, &ctx->c_tr, &ctx->d_tr, &ctx->invd_tr, &ctx->w_tr, &ctx->logd_tr,
+                     &ctx->c1, &ctx->d1, &ctx->invd1, &ctx->w1, &ctx->logd1, &ctx->cabs1})
     CHK(dalloc(ctx, v, mp));
+  CHK(dalloc(ctx, &ctx->x1, np));
   CHK(dalloc(ctx, &ctx->ctrl, 1));
   HIPC(ctx, hipHostMalloc((void**)&ctx->hctrl, sizeof(DevCtrl), hipHostMallocCoherent | hipHostMallocMapped));
   HIPC(ctx, hipHostMalloc((void**)&ctx->hflag, 64, hipHostMallocCoherent | hipHostMallocMapped));
@@ -1589,7 +1623,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->Psa, ctx->xtr, ctx->Pxtr, ctx->c_tr, ctx->d_tr, ctx->invd_tr, ctx->w_tr, ctx->logd_tr,
                   ctx->klp_lx, ctx->klp_g0, ctx->klp_hd, ctx->klp_ab, ctx->klp_lxt, ctx->klp_part, ctx->klp_ls,
                   ctx->kl_vabs, ctx->kl_uabs, ctx->kl_vtr, ctx->kl_ytr, ctx->qPxa, ctx->qPsa, ctx->qfabs, ctx->qPx_tr,
-                  ctx->qextra_tr};
+                  ctx->qextra_tr, ctx->x1, ctx->c1, ctx->d1, ctx->invd1, ctx->w1, ctx->logd1, ctx->cabs1};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->kY, (void*)ctx->kYg, (void*)ctx->kgram, (void*)ctx->kS, (void*)ctx->kzp,
@@ -2031,10 +2065,13 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
   ctx->spec_allowed = ctx->p == 0 && ctx->m > 0 && !ctx->kl && !ctx->klp;
   ctx->spec_beta = pars->beta;
   ctx->spec_have = false;
+  ctx->spec_eval_have = false;
   int rc = newton_direction(ctx, pars, info);
   ctx->spec_allowed = false;
   const bool spec = ctx->spec_have;
+  const bool spec_eval = spec && ctx->spec_eval_have;
   ctx->spec_have = false;
+  ctx->spec_eval_have = false;
   if (rc != CVXG_OK) return rc;
   const double q = ctx->hctrl->sc[SC_Q];
   ctx->nd = -q / 2;
@@ -2056,7 +2093,7 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
     if (!use_spec) tstart(ctx, 4);  // (else phase 4 began with the speculative launches)
     if (use_spec) {
     } else if (scale == 1.0) {
-      HIPC(ctx, hipMemcpyAsync(ctx->sdir, ctx->dx, ctx->np * sizeof(double), hipMemcpyDeviceToDevice, ctx->s));
+      launch_axpy_strided(ctx->s, nullptr, ctx->dx, 1, 0, 1.0, ctx->np, ctx->sdir);  // s = dx (a kernel: no blit gap)
     } else {
       launch_axpy_strided(ctx->s, nullptr, ctx->dx, 1, 0, scale, ctx->np, ctx->sdir);  // d * (radius/hNorm)
     }
@@ -2076,7 +2113,7 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
     // y = objF.gradientAt(x); normGrad (and eqDiff); the next step's assembly goes out behind the constraint values
     // when the loop will go on (UnconstrainedSolver.scala:38-41: iter + 1 < maxIter and this step's decrement > tol;
     // only normGrad <= tol, which the evaluation decides, could end it -- then the assembly is dropped)
-    rc = eval_at_x(ctx, ctx->iter + 1 < pars->maxIter && ctx->nd > tol);
+    rc = eval_at_x(ctx, ctx->iter + 1 < pars->maxIter && ctx->nd > tol, use_spec && spec_eval && tacc == 1.0);
     if (rc != CVXG_OK) return rc;
   }
   ctx->iter += 1;
@@ -2205,7 +2242,8 @@ int cvxg_set_timing(cvxg_ctx* ctx, int enabled) {
   if (enabled && !tm.created) {
     for (auto& slot : tm.ev)
       for (auto& pr : slot)
-        for (hipEvent_t& e : pr) HIPC(ctx, hipEventCreate(&e));
+        // timing only: no system-scope fence (its L2 writeback left a 5-10 us gap at every phase boundary)
+        for (hipEvent_t& e : pr) HIPC(ctx, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     tm.created = true;
   }
   if (enabled) {  // a fresh record: the steps from here on

@@ -59,8 +59,9 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
       const int rho = t / NB, cc = t % NB;
       const int off = 2 * ((i * NB + cc) * nrhs + rho);
       f64x2 v = gr.ld2(off);
+      const unsigned long long t0 = spin_clock();
       for (unsigned spins = 0; __double_as_longlong(v[1]) != (long long)gen; ++spins) {
-        if (spins > (1u << 22)) {  // bounded wait: never hang the GPU on a scheduling bug
+        if (spin_expired(spins, t0)) {  // bounded wait: never hang the GPU on a scheduling bug
           s_bad = 1;
           break;
         }

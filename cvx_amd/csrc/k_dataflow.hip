@@ -35,6 +35,41 @@ static_assert(sizeof(ChainSmem) <= DF_SMEM * sizeof(double), "chain workspace ex
 
 __device__ __forceinline__ int df_tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
+// Q = (d d') o H (+ reg I), padded part identity — k_form_q's entries (MatrixUtils.scala:267, :454), formed as each
+// tile is first read (POTRF(0), the chain's staging of block 1, TRSM(i,0), UPDATE(i,j,0)) instead of by a separate
+// pass over the lower triangle.  The same expression in the same order as k_form_q, so the factor is bit-identical.
+struct QFold {
+  const double* H;  // nullptr: L already holds the matrix to factor
+  const double* d;
+  int n;
+  double reg;
+};
+__device__ __forceinline__ double qf_entry(const QFold& f, int r, int c, double h) {
+  if (r < f.n && c < f.n) {
+    double v = (f.d[r] * f.d[c]) * h;
+    if (r == c) v += f.reg;
+    return v;
+  }
+  return (r == c) ? 1.0 : 0.0;
+}
+// a 64 x 64 tile's loads (df_load layout) of Q(r0.., c0..) from H
+__device__ __forceinline__ void qf_load(f64x2 (&v)[NB * NB / 512], const QFold& f, int ld, int r0, int c0) {
+  const int tid = threadIdx.x;
+  const Sc1Mem mH(const_cast<double*>(f.H) + (size_t)r0 * ld + c0, tile_bytes(ld));
+#pragma unroll
+  for (int q = 0; q < NB * NB / 512; ++q) {
+    const int idx = q * 256 + tid;
+    v[q] = mH.ld2((idx >> 5) * ld + 2 * (idx & 31));
+  }
+#pragma unroll
+  for (int q = 0; q < NB * NB / 512; ++q) {
+    const int idx = q * 256 + tid;
+    const int r = r0 + (idx >> 5), c = c0 + 2 * (idx & 31);
+    v[q][0] = qf_entry(f, r, c, v[q][0]);
+    v[q][1] = qf_entry(f, r, c + 1, v[q][1]);
+  }
+}
+
 __device__ __forceinline__ int df_poll(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -42,12 +77,14 @@ __device__ __forceinline__ int df_poll(const int* p) {
 __device__ __forceinline__ void df_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Thread 0 waits until state[idx] >= want.  Returns false when the launch aborts (failed pivot elsewhere)
-// or after ~2^22 polls (then it raises the abort word itself with code 2: a scheduling bug, not a hang).
+// or after SPIN_LIMIT_TICKS of wall time (then it raises the abort word itself with code 2: a scheduling bug, not a
+// hang).
 __device__ bool df_wait(const int* state, int idx, int want, int* abortw, DevCtrl* ctrl) {
+  const unsigned long long t0 = spin_clock();
   for (unsigned spins = 0;; ++spins) {
     if (df_poll(state + idx) >= want) return true;
     if ((spins & 15) == 15 && df_poll(abortw)) return false;
-    if (spins > (1u << 22)) {
+    if (spin_expired(spins, t0)) {
       __hip_atomic_store(abortw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       atomicExch(&ctrl->df_status, 2);
       return false;
@@ -113,12 +150,31 @@ __device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, cons
 }
 
 // UPDATE(i,j,k): A_ij -= L_ik L_jk^T.  On a diagonal tile the strictly-upper 32 x 32 wave block is skipped.
-__device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, double* smem) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const bool active = !(i == j && wc > wr);
-  const Sc1Mem mC(L + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
-  d4f acc[2][2];
+// The tile's C operand in MFMA accumulator layout: from L, or on its first touch (k == 0) Q from H.
+__device__ __forceinline__ void df_load_c(d4f (&acc)[2][2], const Sc1Mem& mC, int ld, int i, int j, bool fold,
+                                          const QFold& qf, int wr, int wc, int lane) {
+  if (fold) {
+    const Sc1Mem mH(const_cast<double*>(qf.H) + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+          acc[mi][nj][r] = mH.ld(row * ld + col);
+        }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
+          acc[mi][nj][r] = qf_entry(qf, i * NB + row, j * NB + col, acc[mi][nj][r]);
+        }
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -128,6 +184,15 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
         const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
         acc[mi][nj][r] = mC.ld(row * ld + col);
       }
+}
+
+__device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, double* smem, const QFold& qf) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const bool active = !(i == j && wc > wr);
+  const Sc1Mem mC(L + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
+  d4f acc[2][2];
+  df_load_c(acc, mC, ld, i, j, qf.H && k == 0, qf, wr, wc, lane);
   double* Pi = smem;
   double* Pj = (i == j) ? smem : smem + NB * DF_SP;
   {  // both panel tiles' loads in flight together (one round trip, behind the C loads), then the LDS stores
@@ -154,22 +219,14 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
 
 // UPDATE4(i,j,k0): A_ij -= sum_{k=k0}^{k0+3} L_ik L_jk^T — one read-modify-write of the tile for four panels,
 // with the operand tiles of panel k+1 loaded into registers while the MFMAs of panel k run (two LDS buffers).
-__device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0, double* smem) {
+__device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0, double* smem, const QFold& qf) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const bool active = !(i == j && wc > wr);
   const bool diag = (i == j);
   const Sc1Mem mC(L + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
   d4f acc[2][2];
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int nj = 0; nj < 2; ++nj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr * 32 + mi * 16 + (lane >> 4) + 4 * r, col = wc * 32 + nj * 16 + (lane & 15);
-        acc[mi][nj][r] = mC.ld(row * ld + col);
-      }
+  df_load_c(acc, mC, ld, i, j, qf.H && k0 == 0, qf, wr, wc, lane);
   f64x2 vi[NB * NB / 512], vj[NB * NB / 512];
   auto tile = [&](int r, int k) { return Sc1Mem(L + (size_t)r * NB * ld + (size_t)k * NB, tile_bytes(ld)); };
   df_load(vi, tile(i, k0), ld);
@@ -210,7 +267,7 @@ __device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0,
 // only before the rhs update, so the L tile is not held back by POTRF's forward solve.  False: the launch aborted.
 __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __restrict__ rhs, int nrhs,
                         double* __restrict__ Linv, double* smem, const int* state, int* abortw, DevCtrl* ctrl,
-                        int* s_ok) {
+                        int* s_ok, const QFold& qf) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   double* Pi = smem;
   double* Pj = smem + NB * DF_SP;
@@ -219,7 +276,8 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
   const Sc1Mem mR(rhs + (size_t)i * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
   {  // both operand tiles' loads in flight together, then the LDS stores
     f64x2 va[NB * NB / 512], vl[NB * NB / 512];
-    df_load(va, mA, ld);
+    if (qf.H && k == 0) qf_load(va, qf, ld, i * NB, 0);
+    else df_load(va, mA, ld);
     df_load(vl, Sc1Mem(Linv + (size_t)k * NB * NB, tile_bytes(NB)), NB);
     df_put(Pi, va);
     df_put(Pj, vl);
@@ -329,7 +387,9 @@ __device__ __forceinline__ void ch_update(d4f (&dacc)[3], const double* Lp, int 
 __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L, int ld, double* __restrict__ rhs,
                                                           int nrhs, double* __restrict__ Linv, DevCtrl* ctrl,
                                                           int* __restrict__ work, const unsigned* __restrict__ tasks,
-                                                          int ntasks, int nblk, unsigned long long* __restrict__ trace) {
+                                                          int ntasks, int nblk, unsigned long long* __restrict__ trace,
+                                                          const double* __restrict__ Hq, const double* __restrict__ dq,
+                                                          int nq) {
   __shared__ __attribute__((aligned(16))) double smem[DF_SMEM];
   __shared__ unsigned s_task;
   __shared__ int s_ok;
@@ -339,6 +399,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   int* state = work + 64;  // own cache lines
   int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published (0..4)
   const int tid = threadIdx.x;
+  const QFold qf{Hq, dq, nq, Hq ? ctrl->reg : 0.0};
   if (blockIdx.x < 2) {
     // ---- workgroups 0 and 1: the critical chain, ping-pong.  Workgroup c factors the diagonal blocks b = c,
     // c + 2, ...  Before POTRF(b) it runs TRSM(b, b-1) and UPDATE(b, b, b-1) in four 16-column slices, each
@@ -365,7 +426,19 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     constexpr int NBLK16 = 3;  // (kChIB / kChJB: this wave's lower 16 x 16 blocks)
     for (int b = blockIdx.x; b < nblk; b += 2) {
       if (b == 0) {
-        potrf64w_stage<Sc1Mem>(L, ld, 0, rhs, 0, nrhs, ps);
+        if (qf.H) {
+          f64x2 v[NB * NB / 512];
+          qf_load(v, qf, ld, 0, 0);
+#pragma unroll
+          for (int q = 0; q < NB * NB / 512; ++q) {
+            const int idx = q * 256 + tid;
+            *reinterpret_cast<f64x2*>(ps.S + (idx >> 5) * P64_SP + 2 * (idx & 31)) = v[q];
+          }
+          const Sc1Mem mR(rhs, (unsigned)(NB * nrhs) * 8u);
+          for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
+        } else {
+          potrf64w_stage<Sc1Mem>(L, ld, 0, rhs, 0, nrhs, ps);
+        }
       } else {
         const int k = b - 1;
         mark(k, 1, 0);
@@ -381,15 +454,20 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         d4f dacc[NBLK16];
         {
           f64x2 va[NB * NB / 512];
-          df_load(va, mA, ld);
-          const Sc1Mem mD(L + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
+          const bool fold = qf.H && k == 0;  // block 1: A_1,0 and D_1 are first read here
+          if (fold) qf_load(va, qf, ld, b * NB, 0);
+          else df_load(va, mA, ld);
+          const Sc1Mem mD(const_cast<double*>(fold ? qf.H : L) + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
 #pragma unroll
           for (int q = 0; q < NBLK16; ++q) {
             const int ib = kChIB[wv][q], jb = kChJB[wv][q];
             if (ib >= 0) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r)
-                dacc[q][r] = mD.ld((16 * ib + (lane >> 4) + 4 * r) * ld + 16 * jb + (lane & 15));
+              for (int r = 0; r < 4; ++r) {
+                const int rr = 16 * ib + (lane >> 4) + 4 * r, cc = 16 * jb + (lane & 15);
+                const double h = mD.ld(rr * ld + cc);
+                dacc[q][r] = fold ? qf_entry(qf, b * NB + rr, b * NB + cc, h) : h;
+              }
             }
           }
           const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
@@ -552,14 +630,14 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     if (!s_ok) break;
     int done_idx, done_val = k + 1;
     if (type == 1) {
-      if (!df_trsm(L, ld, i, k, rhs, nrhs, Linv, smem, state, abortw, ctrl, &s_ok)) break;
+      if (!df_trsm(L, ld, i, k, rhs, nrhs, Linv, smem, state, abortw, ctrl, &s_ok, qf)) break;
       done_idx = df_tri(i, k);
     } else if (type == 3) {
-      df_update4(L, ld, i, j, k, smem);
+      df_update4(L, ld, i, j, k, smem, qf);
       done_idx = df_tri(i, j);
       done_val = k + 4;
     } else {
-      df_update(L, ld, i, j, k, smem);
+      df_update(L, ld, i, j, k, smem, qf);
       done_idx = df_tri(i, j);
     }
     df_drain();  // every storing wave: its sc1 stores have left
@@ -580,9 +658,9 @@ size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1)
 
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
-                          unsigned long long* trace, bool zero_work) {
+                          unsigned long long* trace, bool zero_work, const double* Hq, const double* dq, int nq) {
   if (zero_work) (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
-  k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace);
+  k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq);
 }
 
 }  // namespace cvxg

@@ -120,12 +120,13 @@ __global__ __launch_bounds__(256) void k_trsm_many(const double* __restrict__ L,
     f64x2 zv[NB * FM_CW / 256];
 #pragma unroll
     for (int q = 0; q < NB * FM_CW / 256; ++q) zv[q] = g.ld2(2 * (tid + 256 * q));
+    const unsigned long long t0 = spin_clock();
     for (unsigned spins = 0;; ++spins) {  // all four granules polled together
       bool ready = true;
 #pragma unroll
       for (int q = 0; q < NB * FM_CW / 256; ++q) ready = ready && __double_as_longlong(zv[q][1]) == (long long)gen;
       if (ready) break;
-      if (spins > (1u << 22)) {  // bounded wait: never hang the GPU on a scheduling bug
+      if (spin_expired(spins, t0)) {  // bounded wait: never hang the GPU on a scheduling bug
         s_bad = 1;
         break;
       }
@@ -161,12 +162,13 @@ __global__ __launch_bounds__(256) void k_trsm_many(const double* __restrict__ L,
     f64x2 zf[16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) zf[s] = g.ld2(2 * ((4 * s + k4) * FM_CW + (lane & 15)));
+    const unsigned long long t0 = spin_clock();
     for (unsigned spins = 0; !bad; ++spins) {
       bool ready = true;
 #pragma unroll
       for (int s = 0; s < 16; ++s) ready = ready && __double_as_longlong(zf[s][1]) == (long long)gen;
       if (ready) break;
-      if (spins > (1u << 22)) {
+      if (spin_expired(spins, t0)) {
         bad = true;
         break;
       }

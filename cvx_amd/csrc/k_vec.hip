@@ -1,6 +1,6 @@
 // k_vec.hip — HBM-streaming kernels of the barrier Newton step (gfx950).
 //
-// Row-major constraint matrix A (row i = a_i, LinearConstraint.scala:7-32), one 64-lane wave per row so
+// Row-major constraint matrix A (row i = a_i, LinearConstraint.scala:7-32), 64-lane waves over rows so
 // each row is read as 1 KiB coalesced double2 sweeps; column reductions write per-64-row-chunk partials
 // that a second pass sums in a fixed order (results are bitwise reproducible run to run).
 #include <math.h>
@@ -10,62 +10,83 @@
 namespace cvxg {
 
 // ------------------------------------------------------------------------------------------------
-// Row dot products: one wave per row, double2 loads, fixed-order wave reduction.
+// Row dot products: two rows per wave, double2 loads, fixed-order wave reduction.
 // ------------------------------------------------------------------------------------------------
 typedef double vd2 __attribute__((ext_vector_type(2)));
 
-// cols is a multiple of 128 for every caller (padded layouts); 4 independent 1 KiB sweeps in flight.
-__device__ __forceinline__ double row_dot_wave(const double* __restrict__ row, const double* __restrict__ v,
-                                               int cols, int lane) {
-  vd2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
+// a.v (and |a|.|v|, which bounds the rounding error of every evaluation order of a.v: the line search's certified
+// trial decisions) for two rows per wave.  cols is a multiple of 128 for every caller (padded layouts).  Per row each
+// lane accumulates its double2 columns j = 2 lane + 128 k in two accumulators (k even / odd) with 4 sweeps in flight,
+// then a fixed-order wave reduction: the result does not depend on the pairing or on ABS.  Each load of v serves both
+// rows (with one row per wave every element of M costs two vector loads, and the sweep is load-issue bound below the
+// HBM rate).  `two` is wave-uniform: false for the last row of an odd count.
+template <bool ABS>
+__device__ __forceinline__ void row_dot2_wave(const double* __restrict__ r0, const double* __restrict__ r1, bool two,
+                                              const double* __restrict__ v, int cols, int lane, double (&dot)[2],
+                                              double (&absdot)[2]) {
+  const vd2 z = {0.0, 0.0};
+  vd2 acc0[2] = {z, z}, acc1[2] = {z, z}, aab0[2] = {z, z}, aab1[2] = {z, z};
+  const double* rows[2] = {r0, r1};
   int j = 2 * lane;
   for (; j + 384 < cols; j += 512) {
-    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), a1 = *reinterpret_cast<const vd2*>(row + j + 128);
-    const vd2 a2 = *reinterpret_cast<const vd2*>(row + j + 256), a3 = *reinterpret_cast<const vd2*>(row + j + 384);
     const vd2 b0 = *reinterpret_cast<const vd2*>(v + j), b1 = *reinterpret_cast<const vd2*>(v + j + 128);
     const vd2 b2 = *reinterpret_cast<const vd2*>(v + j + 256), b3 = *reinterpret_cast<const vd2*>(v + j + 384);
-    acc0 = __builtin_elementwise_fma(a0, b0, acc0);
-    acc1 = __builtin_elementwise_fma(a1, b1, acc1);
-    acc0 = __builtin_elementwise_fma(a2, b2, acc0);
-    acc1 = __builtin_elementwise_fma(a3, b3, acc1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q == 1 && !two) break;
+      const double* row = rows[q];
+      const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), a1 = *reinterpret_cast<const vd2*>(row + j + 128);
+      const vd2 a2 = *reinterpret_cast<const vd2*>(row + j + 256), a3 = *reinterpret_cast<const vd2*>(row + j + 384);
+      acc0[q] = __builtin_elementwise_fma(a0, b0, acc0[q]);
+      acc1[q] = __builtin_elementwise_fma(a1, b1, acc1[q]);
+      acc0[q] = __builtin_elementwise_fma(a2, b2, acc0[q]);
+      acc1[q] = __builtin_elementwise_fma(a3, b3, acc1[q]);
+      if (ABS) {
+        aab0[q] = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(b0), aab0[q]);
+        aab1[q] = __builtin_elementwise_fma(__builtin_elementwise_abs(a1), __builtin_elementwise_abs(b1), aab1[q]);
+        aab0[q] = __builtin_elementwise_fma(__builtin_elementwise_abs(a2), __builtin_elementwise_abs(b2), aab0[q]);
+        aab1[q] = __builtin_elementwise_fma(__builtin_elementwise_abs(a3), __builtin_elementwise_abs(b3), aab1[q]);
+      }
+    }
   }
   for (; j < cols; j += 128) {
-    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), b0 = *reinterpret_cast<const vd2*>(v + j);
-    acc0 = __builtin_elementwise_fma(a0, b0, acc0);
+    const vd2 b0 = *reinterpret_cast<const vd2*>(v + j);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q == 1 && !two) break;
+      const vd2 a0 = *reinterpret_cast<const vd2*>(rows[q] + j);
+      acc0[q] = __builtin_elementwise_fma(a0, b0, acc0[q]);
+      if (ABS)
+        aab0[q] = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(b0), aab0[q]);
+    }
   }
-  return wave_sum((acc0[0] + acc0[1]) + (acc1[0] + acc1[1]));
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    dot[q] = wave_sum((acc0[q][0] + acc0[q][1]) + (acc1[q][0] + acc1[q][1]));
+    absdot[q] = ABS ? wave_sum((aab0[q][0] + aab0[q][1]) + (aab1[q][0] + aab1[q][1])) : 0.0;
+  }
 }
 
-// a.v and |a|.|v| in one sweep (the abs dot bounds the rounding error of every evaluation order of a.v: the
-// line search's certified trial decisions, cvxg.cpp: line_search).
-// The same 4-sweeps-in-flight / two-accumulator structure as row_dot_wave, so a.v is bitwise row_dot_wave's.
-__device__ __forceinline__ double row_dot_wave_abs(const double* __restrict__ row, const double* __restrict__ v,
-                                                   int cols, int lane, double* absdot) {
-  vd2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0}, aab0 = {0.0, 0.0}, aab1 = {0.0, 0.0};
-  int j = 2 * lane;
-  for (; j + 384 < cols; j += 512) {
-    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), a1 = *reinterpret_cast<const vd2*>(row + j + 128);
-    const vd2 a2 = *reinterpret_cast<const vd2*>(row + j + 256), a3 = *reinterpret_cast<const vd2*>(row + j + 384);
-    const vd2 b0 = *reinterpret_cast<const vd2*>(v + j), b1 = *reinterpret_cast<const vd2*>(v + j + 128);
-    const vd2 b2 = *reinterpret_cast<const vd2*>(v + j + 256), b3 = *reinterpret_cast<const vd2*>(v + j + 384);
-    acc0 = __builtin_elementwise_fma(a0, b0, acc0);
-    acc1 = __builtin_elementwise_fma(a1, b1, acc1);
-    acc0 = __builtin_elementwise_fma(a2, b2, acc0);
-    acc1 = __builtin_elementwise_fma(a3, b3, acc1);
-    aab0 = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(b0), aab0);
-    aab1 = __builtin_elementwise_fma(__builtin_elementwise_abs(a1), __builtin_elementwise_abs(b1), aab1);
-    aab0 = __builtin_elementwise_fma(__builtin_elementwise_abs(a2), __builtin_elementwise_abs(b2), aab0);
-    aab1 = __builtin_elementwise_fma(__builtin_elementwise_abs(a3), __builtin_elementwise_abs(b3), aab1);
-  }
-  for (; j < cols; j += 128) {
-    const vd2 a0 = *reinterpret_cast<const vd2*>(row + j), b0 = *reinterpret_cast<const vd2*>(v + j);
-    acc0 = __builtin_elementwise_fma(a0, b0, acc0);
-    aab0 = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(b0), aab0);
-  }
-  *absdot = wave_sum((aab0[0] + aab0[1]) + (aab1[0] + aab1[1]));
-  return wave_sum((acc0[0] + acc0[1]) + (acc1[0] + acc1[1]));
+// one row's constraint evaluation from a.x (and |a|.|x|), lane 0
+__device__ __forceinline__ void constraint_eval_row(int row, double dot, double adot, const double* __restrict__ r,
+                                                    const double* __restrict__ ub, double* __restrict__ c,
+                                                    double* __restrict__ d, double* __restrict__ invd,
+                                                    double* __restrict__ w, double* __restrict__ logd, DevCtrl* ctrl,
+                                                    const double* __restrict__ extra, double* __restrict__ cabs) {
+  if (cabs) cabs[row] = fabs(r[row]) + adot;  // |r| + |a|.|x|: scale of the rounding error of r + a.x
+  // r + (a dot x)  (LinearConstraint.scala:23), + (x dot P x)/2 for a QuadraticConstraint row (:31)
+  const double ci = extra ? (r[row] + dot) + extra[row] : r[row] + dot;
+  const double di = ub[row] - ci;          // d = ub - valueAt(x)    BarrierSolver.scala:283
+  c[row] = ci;
+  d[row] = di;
+  invd[row] = 1.0 / di;
+  w[row] = 1.0 / (di * di);                // GGt/(d*d)              BarrierSolver.scala:314
+  logd[row] = (di > 0.0) ? log(di) : 0.0;
+  if (!(di > 0.0)) atomicAdd(&ctrl->infeasible, 1);
+  if (!(ci * (1 + 3e-16) < ub[row])) atomicAdd(&ctrl->not_strict, 1);  // Constraint.scala:23
 }
 
+template <bool ABS>
 __global__ __launch_bounds__(256) void k_constraint_eval(const double* __restrict__ A, int ld, int mp, int cols,
                                                          const double* __restrict__ x,
                                                          const double* __restrict__ r,
@@ -75,67 +96,186 @@ __global__ __launch_bounds__(256) void k_constraint_eval(const double* __restric
                                                          DevCtrl* ctrl, const double* __restrict__ extra,
                                                          double* __restrict__ cabs) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = 2 * (blockIdx.x * 4 + (threadIdx.x >> 6));
   if (row >= mp) return;
-  double adot = 0.0;
-  const double dot = cabs ? row_dot_wave_abs(A + (size_t)row * ld, x, cols, lane, &adot)
-                          : row_dot_wave(A + (size_t)row * ld, x, cols, lane);
+  const bool two = row + 1 < mp;
+  double dot[2], adot[2];
+  row_dot2_wave<ABS>(A + (size_t)row * ld, A + (size_t)(two ? row + 1 : row) * ld, two, x, cols, lane, dot, adot);
   if (lane == 0) {
-    if (cabs) cabs[row] = fabs(r[row]) + adot;  // |r| + |a|.|x|: scale of the rounding error of r + a.x
-    // r + (a dot x)  (LinearConstraint.scala:23), + (x dot P x)/2 for a QuadraticConstraint row (:31)
-    const double ci = extra ? (r[row] + dot) + extra[row] : r[row] + dot;
-    const double di = ub[row] - ci;          // d = ub - valueAt(x)    BarrierSolver.scala:283
-    c[row] = ci;
-    d[row] = di;
-    invd[row] = 1.0 / di;
-    w[row] = 1.0 / (di * di);                // GGt/(d*d)              BarrierSolver.scala:314
-    logd[row] = (di > 0.0) ? log(di) : 0.0;
-    if (!(di > 0.0)) atomicAdd(&ctrl->infeasible, 1);
-    if (!(ci * (1 + 3e-16) < ub[row])) atomicAdd(&ctrl->not_strict, 1);  // Constraint.scala:23
+    constraint_eval_row(row, dot[0], adot[0], r, ub, c, d, invd, w, logd, ctrl, extra, cabs);
+    if (two) constraint_eval_row(row + 1, dot[1], adot[1], r, ub, c, d, invd, w, logd, ctrl, extra, cabs);
   }
 }
 
 void launch_constraint_eval(hipStream_t s, const double* A, int ld, int mp, int n_cols, const double* x,
                             const double* r, const double* ub, double* c, double* d, double* invd,
                             double* w, double* logd, DevCtrl* ctrl, const double* extra, double* cabs) {
-  k_constraint_eval<<<(mp + 3) / 4, 256, 0, s>>>(A, ld, mp, n_cols, x, r, ub, c, d, invd, w, logd, ctrl, extra, cabs);
+  const int grid = ((mp + 1) / 2 + 3) / 4;
+  if (cabs) k_constraint_eval<true><<<grid, 256, 0, s>>>(A, ld, mp, n_cols, x, r, ub, c, d, invd, w, logd, ctrl, extra, cabs);
+  else k_constraint_eval<false><<<grid, 256, 0, s>>>(A, ld, mp, n_cols, x, r, ub, c, d, invd, w, logd, ctrl, extra, cabs);
 }
 
+template <bool ABS>
 __global__ __launch_bounds__(256) void k_rowdot(const double* __restrict__ M, int ld, int rows, int cols,
                                                 const double* __restrict__ v, const double* __restrict__ add,
-                                                double* __restrict__ y) {
+                                                double* __restrict__ y, double* __restrict__ yabs) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = 2 * (blockIdx.x * 4 + (threadIdx.x >> 6));
   if (row >= rows) return;
-  const double dot = row_dot_wave(M + (size_t)row * ld, v, cols, lane);
-  if (lane == 0) y[row] = add ? dot + add[row] : dot;
+  const bool two = row + 1 < rows;
+  double dot[2], adot[2];
+  row_dot2_wave<ABS>(M + (size_t)row * ld, M + (size_t)(two ? row + 1 : row) * ld, two, v, cols, lane, dot, adot);
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q == 1 && !two) break;
+      y[row + q] = add ? dot[q] + add[row + q] : dot[q];
+      if (ABS) yabs[row + q] = adot[q];
+    }
+  }
 }
+static int rowdot_grid(int rows) { return ((rows + 1) / 2 + 3) / 4; }
 
 void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y) {
-  k_rowdot<<<(rows + 3) / 4, 256, 0, s>>>(M, ld, rows, cols, v, nullptr, y);
+  k_rowdot<false><<<rowdot_grid(rows), 256, 0, s>>>(M, ld, rows, cols, v, nullptr, y, nullptr);
 }
 void launch_rowdot_add(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
                        const double* add, double* y) {
-  k_rowdot<<<(rows + 3) / 4, 256, 0, s>>>(M, ld, rows, cols, v, add, y);
-}
-
-__global__ __launch_bounds__(256) void k_rowdot_abs(const double* __restrict__ M, int ld, int rows, int cols,
-                                                    const double* __restrict__ v, double* __restrict__ y,
-                                                    double* __restrict__ yabs) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  double adot;
-  const double dot = row_dot_wave_abs(M + (size_t)row * ld, v, cols, lane, &adot);
-  if (lane == 0) {
-    y[row] = dot;
-    yabs[row] = adot;
-  }
+  k_rowdot<false><<<rowdot_grid(rows), 256, 0, s>>>(M, ld, rows, cols, v, add, y, nullptr);
 }
 void launch_rowdot_abs(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y,
                        double* yabs) {
-  k_rowdot_abs<<<(rows + 3) / 4, 256, 0, s>>>(M, ld, rows, cols, v, y, yabs);
+  k_rowdot<true><<<rowdot_grid(rows), 256, 0, s>>>(M, ld, rows, cols, v, nullptr, y, yabs);
 }
+
+// The line search's setup sweep over A for s = dx (e = A s, eabs = |A| |s|) fused with the next step's constraint
+// evaluation at x1 = x + s (k_constraint_eval's outputs and counters into a second set of buffers): when the line
+// search accepts t = 1 -- the common case -- the next evaluation is already done and A is read once instead of twice.
+// Each wave takes two rows, so every s / x1 load serves two rows of A (three vector loads per element of A would make
+// the sweep load-issue bound, 3.7 instead of 5.3 TB/s).  Per row and vector the accumulation has row_dot2_wave's
+// structure, so every output is bitwise the standalone kernels' (k_rowdot<true>, k_constraint_eval<true>).
+struct RowAcc {
+  vd2 sa0, sa1, sb0, sb1, xa0, xa1, xb0, xb1;  // s: dot, |.| dot; x1: dot, |.| dot (two accumulators each)
+};
+__device__ __forceinline__ void row_acc4(RowAcc& q, const double* __restrict__ a, int j, const vd2 (&sv)[4],
+                                         const vd2 (&yv)[4]) {
+  const vd2 a0 = *reinterpret_cast<const vd2*>(a + j), a1 = *reinterpret_cast<const vd2*>(a + j + 128);
+  const vd2 a2 = *reinterpret_cast<const vd2*>(a + j + 256), a3 = *reinterpret_cast<const vd2*>(a + j + 384);
+  const vd2 b0 = __builtin_elementwise_abs(a0), b1 = __builtin_elementwise_abs(a1);
+  const vd2 b2 = __builtin_elementwise_abs(a2), b3 = __builtin_elementwise_abs(a3);
+  q.sa0 = __builtin_elementwise_fma(a0, sv[0], q.sa0);
+  q.sa1 = __builtin_elementwise_fma(a1, sv[1], q.sa1);
+  q.sa0 = __builtin_elementwise_fma(a2, sv[2], q.sa0);
+  q.sa1 = __builtin_elementwise_fma(a3, sv[3], q.sa1);
+  q.sb0 = __builtin_elementwise_fma(b0, __builtin_elementwise_abs(sv[0]), q.sb0);
+  q.sb1 = __builtin_elementwise_fma(b1, __builtin_elementwise_abs(sv[1]), q.sb1);
+  q.sb0 = __builtin_elementwise_fma(b2, __builtin_elementwise_abs(sv[2]), q.sb0);
+  q.sb1 = __builtin_elementwise_fma(b3, __builtin_elementwise_abs(sv[3]), q.sb1);
+  q.xa0 = __builtin_elementwise_fma(a0, yv[0], q.xa0);
+  q.xa1 = __builtin_elementwise_fma(a1, yv[1], q.xa1);
+  q.xa0 = __builtin_elementwise_fma(a2, yv[2], q.xa0);
+  q.xa1 = __builtin_elementwise_fma(a3, yv[3], q.xa1);
+  q.xb0 = __builtin_elementwise_fma(b0, __builtin_elementwise_abs(yv[0]), q.xb0);
+  q.xb1 = __builtin_elementwise_fma(b1, __builtin_elementwise_abs(yv[1]), q.xb1);
+  q.xb0 = __builtin_elementwise_fma(b2, __builtin_elementwise_abs(yv[2]), q.xb0);
+  q.xb1 = __builtin_elementwise_fma(b3, __builtin_elementwise_abs(yv[3]), q.xb1);
+}
+__device__ __forceinline__ void row_acc1(RowAcc& q, const double* __restrict__ a, int j, vd2 s0, vd2 y0) {
+  const vd2 a0 = *reinterpret_cast<const vd2*>(a + j);
+  q.sa0 = __builtin_elementwise_fma(a0, s0, q.sa0);
+  q.sb0 = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(s0), q.sb0);
+  q.xa0 = __builtin_elementwise_fma(a0, y0, q.xa0);
+  q.xb0 = __builtin_elementwise_fma(__builtin_elementwise_abs(a0), __builtin_elementwise_abs(y0), q.xb0);
+}
+__device__ __forceinline__ void ls_setup_eval_row(const RowAcc& q, int row, double* __restrict__ e,
+                                                  double* __restrict__ eabs, const double* __restrict__ r,
+                                                  const double* __restrict__ ub, double* __restrict__ c,
+                                                  double* __restrict__ d, double* __restrict__ invd,
+                                                  double* __restrict__ w, double* __restrict__ logd,
+                                                  double* __restrict__ cabs, DevCtrl* ctrl, int lane) {
+  const double sab = wave_sum((q.sb0[0] + q.sb0[1]) + (q.sb1[0] + q.sb1[1]));
+  const double sdt = wave_sum((q.sa0[0] + q.sa0[1]) + (q.sa1[0] + q.sa1[1]));
+  const double xab = wave_sum((q.xb0[0] + q.xb0[1]) + (q.xb1[0] + q.xb1[1]));
+  const double xdt = wave_sum((q.xa0[0] + q.xa0[1]) + (q.xa1[0] + q.xa1[1]));
+  if (lane == 0) {
+    e[row] = sdt;
+    eabs[row] = sab;
+    cabs[row] = fabs(r[row]) + xab;  // as k_constraint_eval (linear rows, certified)
+    const double ci = r[row] + xdt;
+    const double di = ub[row] - ci;
+    c[row] = ci;
+    d[row] = di;
+    invd[row] = 1.0 / di;
+    w[row] = 1.0 / (di * di);
+    logd[row] = (di > 0.0) ? log(di) : 0.0;
+    if (!(di > 0.0)) atomicAdd(&ctrl->spec_infeasible, 1);
+    if (!(ci * (1 + 3e-16) < ub[row])) atomicAdd(&ctrl->spec_not_strict, 1);
+  }
+}
+__global__ __launch_bounds__(256) void k_ls_setup_eval(const double* __restrict__ A, int ld, int mp, int cols,
+                                                       const double* __restrict__ s, const double* __restrict__ x1,
+                                                       double* __restrict__ e, double* __restrict__ eabs,
+                                                       const double* __restrict__ r, const double* __restrict__ ub,
+                                                       double* __restrict__ c, double* __restrict__ d,
+                                                       double* __restrict__ invd, double* __restrict__ w,
+                                                       double* __restrict__ logd, double* __restrict__ cabs,
+                                                       DevCtrl* ctrl) {
+  const int lane = threadIdx.x & 63;
+  const int row = 2 * (blockIdx.x * 4 + (threadIdx.x >> 6));  // rows row, row + 1 (mp is even)
+  if (row >= mp) return;
+  const double* __restrict__ a0 = A + (size_t)row * ld;
+  const double* __restrict__ a1 = a0 + ld;
+  const vd2 z = {0.0, 0.0};
+  RowAcc q0{z, z, z, z, z, z, z, z}, q1{z, z, z, z, z, z, z, z};
+  int j = 2 * lane;
+  for (; j + 384 < cols; j += 512) {
+    vd2 sv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sv[u] = *reinterpret_cast<const vd2*>(s + j + 128 * u);
+      yv[u] = *reinterpret_cast<const vd2*>(x1 + j + 128 * u);
+    }
+    row_acc4(q0, a0, j, sv, yv);
+    row_acc4(q1, a1, j, sv, yv);
+  }
+  for (; j < cols; j += 128) {
+    const vd2 s0 = *reinterpret_cast<const vd2*>(s + j), y0 = *reinterpret_cast<const vd2*>(x1 + j);
+    row_acc1(q0, a0, j, s0, y0);
+    row_acc1(q1, a1, j, s0, y0);
+  }
+  ls_setup_eval_row(q0, row, e, eabs, r, ub, c, d, invd, w, logd, cabs, ctrl, lane);
+  ls_setup_eval_row(q1, row + 1, e, eabs, r, ub, c, d, invd, w, logd, cabs, ctrl, lane);
+}
+void launch_ls_setup_eval(hipStream_t st, const double* A, int ld, int mp, int cols, const double* s, const double* x1,
+                          double* e, double* eabs, const double* r, const double* ub, double* c, double* d,
+                          double* invd, double* w, double* logd, double* cabs, DevCtrl* ctrl) {
+  k_ls_setup_eval<<<(mp / 2 + 3) / 4, 256, 0, st>>>(A, ld, mp, cols, s, x1, e, eabs, r, ub, c, d, invd, w, logd, cabs,
+                                                    ctrl);
+}
+
+// s = dx and x1 = x + s * 1 (k_axpy's expression at t = 1); the speculative counters zeroed
+__global__ void k_spec_prep(const double* __restrict__ dx, const double* __restrict__ x, int n, double* __restrict__ s,
+                            double* __restrict__ x1, DevCtrl* ctrl) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const double v = dx[i];
+    s[i] = v;
+    x1[i] = x[i] + v * 1.0;
+  }
+  if (i == 0) {
+    ctrl->spec_infeasible = 0;
+    ctrl->spec_not_strict = 0;
+  }
+}
+void launch_spec_prep(hipStream_t st, const double* dx, const double* x, int n, double* s, double* x1, DevCtrl* ctrl) {
+  k_spec_prep<<<(n + 255) / 256, 256, 0, st>>>(dx, x, n, s, x1, ctrl);
+}
+// the evaluation's counters from the speculative ones (the evaluation at x1 is taken over)
+__global__ void k_ctrl_take_spec(DevCtrl* ctrl) {
+  ctrl->infeasible = ctrl->spec_infeasible;
+  ctrl->not_strict = ctrl->spec_not_strict;
+}
+void launch_ctrl_take_spec(hipStream_t st, DevCtrl* ctrl) { k_ctrl_take_spec<<<1, 1, 0, st>>>(ctrl); }
 
 // ------------------------------------------------------------------------------------------------
 // Column reductions A' v: grid (cols/512, rows/64); thread owns 2 adjacent columns, loops 64 rows.

@@ -28,6 +28,11 @@ void launch_rowdot_add(hipStream_t s, const double* M, int ld, int rows, int col
 // y = M v and yabs = |M| |v| in the same sweep
 void launch_rowdot_abs(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y,
                        double* yabs);
+void launch_ls_setup_eval(hipStream_t st, const double* A, int ld, int mp, int cols, const double* s, const double* x1,
+                          double* e, double* eabs, const double* r, const double* ub, double* c, double* d,
+                          double* invd, double* w, double* logd, double* cabs, DevCtrl* ctrl);
+void launch_spec_prep(hipStream_t st, const double* dx, const double* x, int n, double* s, double* x1, DevCtrl* ctrl);
+void launch_ctrl_take_spec(hipStream_t st, DevCtrl* ctrl);
 // part[chunk][j] = sum_{i in chunk} M[i][j] v[i]  (chunks of COLDOT_ROWS rows; rows % 64 == 0)
 int coldot_chunks(int rows);
 void launch_coldot_partials(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
@@ -129,7 +134,10 @@ size_t chol_dataflow_work_ints(int nblk);
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */,
-                          bool zero_work = true /* false: launch_factor_prep zeroed it */);
+                          bool zero_work = true /* false: launch_factor_prep zeroed it */,
+                          const double* Hq = nullptr /* non-null: factor Q = (d d') o H + reg I (k_form_q's entries),
+                                                        formed as each tile is first read; L is then output only */,
+                          const double* dq = nullptr, int nq = 0);
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
 size_t bwd_work_ints(int nblk);  // flag words + the data-tagged u granules of k_bwd_dataflow
 void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,

@@ -1530,6 +1530,42 @@ def test_batch_full_size_contexts_share_one_gpu(mods):
         e.close()
 
 
+def test_speculative_next_evaluation_bitwise(mods):
+    """The line search's setup sweep over A for s = dx also evaluates the constraints at x + dx (k_ls_setup_eval);
+    when the search accepts t = 1 the next step takes that evaluation over instead of re-reading A.  After every such
+    step, the next step's f(x) and q = dx . grad equal bitwise those of a fresh evaluation + direction at the same x
+    on a second engine (BarrierSolver.scala:280-315 evaluated at x + s t, UnconstrainedSolver.scala:130)."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp(600, 1400, instance=31)
+    pars = SP.standardParams()
+    a = _engine(Engine, spec)
+    b = _engine(Engine, spec)
+    a.set_x(spec["x0"])
+    t = 1.0
+    a.centering_begin(t)
+    full_steps = 0
+    prev = None
+    for _ in range(40):
+        x = a.get_x()
+        st = a.newton_step(pars)
+        if prev is not None and prev.took_step and prev.step == 1.0 and st.q != 0.0:  # (q = 0: the loop had ended)
+            f_ref, _, _ = b.barrier_eval(t, x, want_grad=False)
+            _, _, ib = b.newton_direction(pars, t, x)
+            assert st.f == f_ref, f"f after a t = 1 step: {st.f!r} vs fresh {f_ref!r}"
+            assert st.q == ib.q, f"q after a t = 1 step: {st.q!r} vs fresh {ib.q!r}"
+            full_steps += 1
+        prev = st
+        if st.done:
+            t *= 10.0
+            a.centering_begin(t)
+            prev = None
+            if t > 1e6:
+                break
+    a.close()
+    b.close()
+    assert full_steps >= 3, f"only {full_steps} steps took t = 1"
+
+
 @pytest.mark.parametrize("n,m", [(384, 700), (1024, 2048)])
 def test_ruiz_lookahead_equals_full_loop(mods, n, m):
     """The Newton step first launches only the Ruiz sweeps the previous step needed + 1 (cvxg.cpp: ruiz_lookahead)
