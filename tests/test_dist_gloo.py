@@ -52,6 +52,7 @@ class OracleEngine:
         d = O.newton_direction(self.pb, self.t, self.x, y, pars.tolEqSolve)
         q = float(d @ y)
         took = -q / 2 > pars.tolSolver
+        st = 0.0
         if took:
             if self.it == 0:
                 self.radius = np.sqrt(-q)
@@ -59,7 +60,7 @@ class OracleEngine:
             s, st, _, _ = O.unconstrained_line_search(self.pb, self.t, self.x, d, q, f, self.it, self.radius, pars)
             self.x = self.x + s * st
         self.it += 1
-        return types.SimpleNamespace(done=not took, took_step=int(took))
+        return types.SimpleNamespace(done=not took, took_step=int(took), step=float(st))
 
     def set_timing(self, on):
         pass
