@@ -35,6 +35,8 @@ constexpr int TRING = 64;
 struct Timer {
   hipEvent_t ev[TRING][NT][2] = {};
   bool on = false, created = false;
+  bool all = false;  // every phase; otherwise only the assembly and Cholesky phases (0, 2, 5): an event record is a
+                     // marker packet that leaves the GPU idle ~3-4 us between kernels (microbench/hostcost.hip)
   bool rec[TRING][NT] = {};
   int tick = 0;      // the step being recorded: ring slot tick % TRING
   int steps = 0;     // steps recorded since timing was enabled (capped at TRING - 1)
@@ -138,6 +140,8 @@ struct cvxg_ctx {
   int bwd_gen = 0;
   // Ruiz lookahead (cholesky_solve): the sweeps the next step launches first, and how often more had to follow
   int ruiz_launch = RUIZ_MAX;
+  int ruiz_k1 = 0;            // Ruiz sweeps launched so far in this step (lookahead)
+  bool ruiz_pending = false;  // the lookahead went out without a host read: the next factor attempt checks it
   long long ruiz_relaunches = 0;
   int ncu = 256;
   unsigned* df_tasks = nullptr;
@@ -221,11 +225,12 @@ static int dalloc(cvxg_ctx* ctx, T** p, size_t count) {
   return CVXG_OK;
 }
 
+static bool timed(const cvxg_ctx* ctx, int i) { return ctx->tm.on && (ctx->tm.all || i == 0 || i == 2 || i == 5); }
 static void tstart(cvxg_ctx* ctx, int i) {
-  if (ctx->tm.on) (void)hipEventRecord(ctx->tm.ev[ctx->tm.tick % TRING][i][0], ctx->s);
+  if (timed(ctx, i)) (void)hipEventRecord(ctx->tm.ev[ctx->tm.tick % TRING][i][0], ctx->s);
 }
 static void tstop(cvxg_ctx* ctx, int i) {
-  if (ctx->tm.on) {
+  if (timed(ctx, i)) {
     (void)hipEventRecord(ctx->tm.ev[ctx->tm.tick % TRING][i][1], ctx->s);
     ctx->tm.rec[ctx->tm.tick % TRING][i] = true;
   }
@@ -552,7 +557,8 @@ static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false) {
     std::swap(ctx->w, ctx->w1);
     std::swap(ctx->logd, ctx->logd1);
     std::swap(ctx->cabs, ctx->cabs1);
-    launch_ctrl_take_spec(s, ctx->ctrl);
+    // (the evaluation's counters are taken over on the stream that publishes them; with the prefetch that is s2)
+    if (!prefetch || ctx->kl || ctx->klp) launch_ctrl_take_spec(s, ctx->ctrl);
   } else {
     launch_ctrl_reset_eval(s, ctx->ctrl);
     constraint_eval_all(ctx);
@@ -561,8 +567,9 @@ static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false) {
   prefetch = prefetch && !ctx->kl && !ctx->klp;  // (their Hessians need the evaluation's y / diag(1/x) first)
   if (prefetch) {  // the assembly needs w (and the quadratic rows' P_k x) only: it stays on the main stream, and the
                    // rest of the evaluation moves to s2 behind the constraint values
-    HIPC(ctx, hipEventRecord(ctx->ev_w, s));
-    HIPC(ctx, hipStreamWaitEvent(ctx->s2, ctx->ev_w, 0));
+    // Taken: x (= x1, swapped in by the caller) and the constraint values were final before the line search's host
+    // read, so s2 needs no wait on the main stream (one event marker less in front of the assembly)
+    if (!taken) HIPC(ctx, hipEventRecord(ctx->ev_w, s));
     const int nx = (ctx->tm.tick + 1) % TRING;  // timed as phase 5 of the step that will use it
     if (ctx->tm.on) HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][0], s));
     CHK(assemble_hessian(ctx, nullptr, nullptr, s));
@@ -570,7 +577,11 @@ static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false) {
       HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][1], s));
       ctx->tm.rec[nx][5] = ctx->tm.pf5 = true;
     }
+    // the second stream's wait is issued after the assembly's launches: the GPU is idle until they are (the host's
+    // hipStreamWaitEvent costs ~8 us, microbench/hostcost.hip)
+    if (!taken) HIPC(ctx, hipStreamWaitEvent(ctx->s2, ctx->ev_w, 0));
     s = ctx->s2;
+    if (taken) launch_ctrl_take_spec(s, ctx->ctrl);
   }
   const bool quad = ctx->hasP && !ctx->kl;
   const bool cert = ls_certified(ctx);
@@ -710,22 +721,31 @@ static void ruiz_sweeps(cvxg_ctx* ctx, int k0, int k1) {
   }
   launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl, k1);
 }
-static void ruiz(cvxg_ctx* ctx) { ruiz_sweeps(ctx, 0, RUIZ_MAX); }
+static void ruiz(cvxg_ctx* ctx) {
+  ctx->ruiz_pending = false;
+  ruiz_sweeps(ctx, 0, RUIZ_MAX);
+}
 // The Newton step's Ruiz launches only the sweeps the previous step needed plus RUIZ_MARGIN (a sweep that exits on
 // rho <= 1e-6 still costs a launch pair, ~9 us), reads the control block, and launches RUIZ_CHUNK more at a time
 // while the loop is not done.  The sweeps that run, dfin and the sweep count are those of the full loop; a short
 // lookahead costs one more host round trip.
 constexpr int RUIZ_MARGIN = 1, RUIZ_CHUNK = 2;
+// The sweeps go out without a host read: the factorization attempt behind them is gated on the device (a launch that
+// finds the loop still open leaves at once), and its one host read tells whether the loop was done (factor_attempt).
 static int ruiz_lookahead(cvxg_ctx* ctx) {
-  int k1 = ctx->ruiz_launch;
-  ruiz_sweeps(ctx, 0, k1);
+  ctx->ruiz_k1 = ctx->ruiz_launch;
+  ruiz_sweeps(ctx, 0, ctx->ruiz_k1);
   HIPC(ctx, hipGetLastError());
-  CHK(sync_ctrl(ctx));
+  ctx->ruiz_pending = true;
+  return CVXG_OK;
+}
+// A short lookahead: RUIZ_CHUNK more sweeps at a time, each batch followed by a host read, until the loop is done.
+static int ruiz_finish(cvxg_ctx* ctx) {
   while (ctx->hctrl->ruiz_sweeps < 0) {
     ++ctx->ruiz_relaunches;
-    const int k2 = std::min(RUIZ_MAX, k1 + RUIZ_CHUNK);
-    ruiz_sweeps(ctx, k1, k2);
-    k1 = k2;
+    const int k2 = std::min(RUIZ_MAX, ctx->ruiz_k1 + RUIZ_CHUNK);
+    ruiz_sweeps(ctx, ctx->ruiz_k1, k2);
+    ctx->ruiz_k1 = k2;
     HIPC(ctx, hipGetLastError());
     CHK(sync_ctrl(ctx));
   }
@@ -747,7 +767,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   // the whole factorization as one persistent launch over the 64 x 64 tile DAG (k_dataflow.hip); Q = (d d') o H
   // (+ reg I) is formed as each tile is first read (no separate k_form_q pass)
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
-                       ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n);
+                       ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending);
   ctx->spec_launched = false;
   after();
   HIPC(ctx, hipGetLastError());
@@ -756,6 +776,15 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
                   5 * LS_TRIALS * sizeof(double)));
   } else {
     CHK(sync_ctrl(ctx));
+  }
+  if (ctx->ruiz_pending) {
+    ctx->ruiz_pending = false;
+    if (ctx->hctrl->ruiz_sweeps < 0) {  // the Ruiz loop was still open: this attempt was void (nothing factored)
+      ctx->spec_launched = ctx->spec_eval_launched = false;
+      CHK(ruiz_finish(ctx));
+      tstart(ctx, 2);  // (phase 2 times the factorization that counts)
+      return factor_attempt(ctx, reg, nrhs, fill_rhs, after);
+    }
   }
   ctx->spec_have = ctx->spec_launched;
   ctx->spec_eval_have = ctx->spec_launched && ctx->spec_eval_launched;
@@ -803,12 +832,12 @@ static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regula
   return CVXG_OK;
 }
 
-static void backward_solve(cvxg_ctx* ctx, int nrhs) {
+static void backward_solve(cvxg_ctx* ctx, int nrhs, BwdEpilogue epi = {}) {
   launch_bwd_dataflow(ctx->s, ctx->L, ctx->np, ctx->Linv, ctx->rhs, ctx->sol, nrhs, ctx->nblk, ctx->bwd_flags,
-                      ++ctx->bwd_gen, ctx->ctrl);
+                      ++ctx->bwd_gen, ctx->ctrl, epi);
 }
 
-static void ls_setup_launch(cvxg_ctx* ctx, bool spec_eval = false);
+static void ls_setup_launch(cvxg_ctx* ctx, bool spec_eval = false, DotBatch db = {});
 static void ls_batch_launch(cvxg_ctx* ctx, double tbase, double beta);
 
 // MatrixUtils.choleskySolve(H, b = -grad, tol) (MatrixUtils.scala:468-516); result in ctx->dx.
@@ -825,21 +854,29 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
   auto solve_and_residual = [&]() {
     tstop(ctx, 2);
     tstart(ctx, 3);
-    backward_solve(ctx, 1);
-    launch_scale_vec(s, ctx->sol, ctx->dfin, ctx->np, ctx->dx);  // x = d :* u
+    // x = d :* u, and for the speculative line search s = dx (x1 = x + s when the trial evaluation goes out too), in
+    // the backward solve's epilogue
+    const bool se = ctx->spec_allowed && spec_eval_ok(ctx);
+    BwdEpilogue epi;
+    epi.d = ctx->dfin;
+    epi.dx = ctx->dx;
+    if (ctx->spec_allowed) epi.s = ctx->sdir;
+    if (se) {
+      epi.x = ctx->x;
+      epi.x1 = ctx->x1;
+      epi.sctrl = ctx->ctrl;
+    }
+    backward_solve(ctx, 1, epi);
     // relativeSize(H*x - b, b, tol), b = -grad  (MatrixUtils.scala:437-442, 496)
     launch_rowdot_add(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->dx, ctx->y, ctx->vtmp);  // H x + grad = H x - b
     DotBatch db{};
     db.add(DOT_FMA, ctx->vtmp, nullptr, ctx->n, SC_RES2);
     db.add(DOT_FMA, ctx->dx, ctx->y, ctx->np, SC_Q);
-    launch_dots(s, db, ctx->ctrl);
+    if (!ctx->spec_allowed) launch_dots(s, db, ctx->ctrl);  // (else in one launch with the line search's dots)
     tstop(ctx, 3);
     if (ctx->spec_allowed) {  // the line search's setup and first batch for s = dx ride this attempt's host read
       tstart(ctx, 4);
-      const bool se = spec_eval_ok(ctx);
-      if (se) launch_spec_prep(s, ctx->dx, ctx->x, ctx->np, ctx->sdir, ctx->x1, ctx->ctrl);  // s = dx, x1 = x + s
-      else launch_axpy_strided(s, nullptr, ctx->dx, 1, 0, 1.0, ctx->np, ctx->sdir);  // s = dx (a kernel: no blit gap)
-      ls_setup_launch(ctx, se);
+      ls_setup_launch(ctx, se, db);  // (s = dx and x1 = x + s came with the backward solve)
       ls_batch_launch(ctx, 1.0, ctx->spec_beta);
       ctx->spec_launched = true;
       ctx->spec_eval_launched = se;
@@ -1298,7 +1335,8 @@ static int trial_fresh(cvxg_ctx* ctx, double tt, FreshTrial* out) {
 //    evaluation was measured: late in the path -- t = 1e10 -- the noise then rejected trial after trial and a
 //    centering ran into maxIter.)
 // e = A s (and |A||s|), and the quadratic pieces of f0(x + s t), s = ctx->sdir: launches only.
-static void ls_setup_launch(cvxg_ctx* ctx, bool spec_eval) {
+// db: reductions already enqueued by the caller (the residual's), launched together with the setup's own
+static void ls_setup_launch(cvxg_ctx* ctx, bool spec_eval, DotBatch db) {
   hipStream_t s = ctx->s;
   const bool cert = ls_certified(ctx);
   const bool quad = ctx->hasP && !ctx->kl;
@@ -1326,17 +1364,23 @@ static void ls_setup_launch(cvxg_ctx* ctx, bool spec_eval) {
     if (cert) launch_rowdot_abs(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps, ctx->Psa);
     else launch_rowdot(s, ctx->P, ctx->np, ctx->np, ctx->np, ctx->sdir, ctx->Ps);
   }
-  DotBatch db{};
-  db.add(DOT_FMA, ctx->a0, ctx->sdir, ctx->np, SC_A0S);
+  auto add = [&](int k, const double* u, const double* v, int len, int sl) {
+    if (db.full()) {
+      launch_dots(s, db, ctx->ctrl);
+      db.count = 0;
+    }
+    db.add(k, u, v, len, sl);
+  };
+  add(DOT_FMA, ctx->a0, ctx->sdir, ctx->np, SC_A0S);
   if (quad) {
-    db.add(DOT_FMA, ctx->sdir, ctx->Px, ctx->np, SC_SPX);
-    db.add(DOT_FMA, ctx->sdir, ctx->Ps, ctx->np, SC_SPS);
+    add(DOT_FMA, ctx->sdir, ctx->Px, ctx->np, SC_SPX);
+    add(DOT_FMA, ctx->sdir, ctx->Ps, ctx->np, SC_SPS);
   }
   if (cert) {
-    db.add(DOT_ABS, ctx->a0, ctx->sdir, ctx->np, SC_A0SA);
+    add(DOT_ABS, ctx->a0, ctx->sdir, ctx->np, SC_A0SA);
     if (quad) {
-      db.add(DOT_ABS, ctx->sdir, ctx->Pxa, ctx->np, SC_SPXA);
-      db.add(DOT_ABS, ctx->sdir, ctx->Psa, ctx->np, SC_SPSA);
+      add(DOT_ABS, ctx->sdir, ctx->Pxa, ctx->np, SC_SPXA);
+      add(DOT_ABS, ctx->sdir, ctx->Psa, ctx->np, SC_SPSA);
     }
   }
   launch_dots(s, db, ctx->ctrl);
@@ -2104,7 +2148,9 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
     info->ls_ties = ties;
     tstop(ctx, 4);
     if (rc != CVXG_OK) return rc;
-    launch_axpy(ctx->s, ctx->x, ctx->sdir, tacc, ctx->np, ctx->x);  // x = x + s*t
+    const bool taken = use_spec && spec_eval && tacc == 1.0;
+    if (taken) std::swap(ctx->x, ctx->x1);  // x1 = x + s*1, formed (bitwise as below) before the host read
+    else launch_axpy(ctx->s, ctx->x, ctx->sdir, tacc, ctx->np, ctx->x);  // x = x + s*t
     HIPC(ctx, hipGetLastError());
     info->step = tacc;
     info->backtracks_c = kc;
@@ -2113,7 +2159,7 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
     // y = objF.gradientAt(x); normGrad (and eqDiff); the next step's assembly goes out behind the constraint values
     // when the loop will go on (UnconstrainedSolver.scala:38-41: iter + 1 < maxIter and this step's decrement > tol;
     // only normGrad <= tol, which the evaluation decides, could end it -- then the assembly is dropped)
-    rc = eval_at_x(ctx, ctx->iter + 1 < pars->maxIter && ctx->nd > tol, use_spec && spec_eval && tacc == 1.0);
+    rc = eval_at_x(ctx, ctx->iter + 1 < pars->maxIter && ctx->nd > tol, taken);
     if (rc != CVXG_OK) return rc;
   }
   ctx->iter += 1;
@@ -2253,6 +2299,7 @@ int cvxg_set_timing(cvxg_ctx* ctx, int enabled) {
       for (bool& r : slot) r = false;
   }
   tm.on = enabled != 0;
+  tm.all = enabled != 1;
   return CVXG_OK;
 }
 

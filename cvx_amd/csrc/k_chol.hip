@@ -20,8 +20,8 @@ namespace cvxg {
 __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__ L, int ld,
                                                       const double* __restrict__ Linv, const double* __restrict__ rhs,
                                                       double* __restrict__ out, int nrhs, int nblk, int* flags, int gen,
-                                                      const DevCtrl* ctrl) {
-  if (ctrl->chol_info != 0) return;
+                                                      const DevCtrl* ctrl, BwdEpilogue epi) {
+  if (ctrl->chol_info != 0 || ctrl->ruiz_sweeps < 0) return;  // a failed or void factorization attempt
   __shared__ double u[MAX_RHS][NB];
   __shared__ double part[4][MAX_RHS][NB];
   __shared__ int s_bad;
@@ -108,15 +108,27 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
       gr.st2(2 * ((b * NB + c) * nrhs + rho), f64x2{s, tag});  // the hand-off granule first
       out[(size_t)(b * NB + c) * nrhs + rho] = s;              // the solution (read after the launch)
     }
+    if (epi.d) {  // Newton step (nrhs = 1): dx = d :* u, and the line search's s = dx, x1 = x + s*1 (k_scale_vec,
+                  // k_spec_prep fused)
+      const int i = b * NB + c;
+      const double v = epi.d[i] * out[i];
+      epi.dx[i] = v;
+      if (epi.s) epi.s[i] = v;
+      if (epi.x1) epi.x1[i] = epi.x[i] + v * 1.0;
+    }
+  }
+  if (epi.sctrl && b == 0 && threadIdx.x == 0) {
+    epi.sctrl->spec_infeasible = 0;
+    epi.sctrl->spec_not_strict = 0;
   }
 }
 
 size_t bwd_work_ints(int nblk) { return (size_t)((nblk + 63) & ~63) + (size_t)nblk * NB * MAX_RHS * 4; }
 
 void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,
-                         int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl) {
+                         int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl, BwdEpilogue epi) {
   // (flags: nblk words + the granules, bwd_work_ints)
-  k_bwd_dataflow<<<nblk, 256, 0, s>>>(L, ld, Linv, rhs, out, nrhs, nblk, flags, gen, ctrl);
+  k_bwd_dataflow<<<nblk, 256, 0, s>>>(L, ld, Linv, rhs, out, nrhs, nblk, flags, gen, ctrl, epi);
 }
 
 }  // namespace cvxg

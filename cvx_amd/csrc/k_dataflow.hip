@@ -389,7 +389,10 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
                                                           int* __restrict__ work, const unsigned* __restrict__ tasks,
                                                           int ntasks, int nblk, unsigned long long* __restrict__ trace,
                                                           const double* __restrict__ Hq, const double* __restrict__ dq,
-                                                          int nq) {
+                                                          int nq, int ruiz_gate) {
+  // the Ruiz loop launched ahead of the factorization without a host read may still be open (k_ruiz_final: -1): then
+  // the launch is void and the host finishes the loop and factors again
+  if (ruiz_gate && ctrl->ruiz_sweeps < 0) return;
   __shared__ __attribute__((aligned(16))) double smem[DF_SMEM];
   __shared__ unsigned s_task;
   __shared__ int s_ok;
@@ -658,9 +661,11 @@ size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1)
 
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
-                          unsigned long long* trace, bool zero_work, const double* Hq, const double* dq, int nq) {
+                          unsigned long long* trace, bool zero_work, const double* Hq, const double* dq, int nq,
+                          bool ruiz_gate) {
   if (zero_work) (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
-  k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq);
+  k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq,
+                                      ruiz_gate ? 1 : 0);
 }
 
 }  // namespace cvxg

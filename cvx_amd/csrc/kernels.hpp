@@ -137,11 +137,23 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                           bool zero_work = true /* false: launch_factor_prep zeroed it */,
                           const double* Hq = nullptr /* non-null: factor Q = (d d') o H + reg I (k_form_q's entries),
                                                         formed as each tile is first read; L is then output only */,
-                          const double* dq = nullptr, int nq = 0);
+                          const double* dq = nullptr, int nq = 0,
+                          bool ruiz_gate = false /* true: every workgroup leaves at once when ctrl->ruiz_sweeps < 0
+                                                    (a short Ruiz lookahead, cvxg.cpp: factor_attempt) */);
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
 size_t bwd_work_ints(int nblk);  // flag words + the data-tagged u granules of k_bwd_dataflow
+// Optional epilogue (nrhs = 1): dx = d :* u; with s, also s = dx and x1 = x + s (the speculative line search's
+// direction and trial point), and sctrl's speculative evaluation counters reset.
+struct BwdEpilogue {
+  const double* d = nullptr;
+  double* dx = nullptr;
+  double* s = nullptr;
+  const double* x = nullptr;
+  double* x1 = nullptr;
+  DevCtrl* sctrl = nullptr;
+};
 void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,
-                         int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl);
+                         int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl, BwdEpilogue epi = {});
 
 // ---- line search ----------------------------------------------------------------------------------
 // For trials k in [0, LS_TRIALS): t_k = tbase*beta^k; g_i = c_i + t_k e_i; per-block partials of

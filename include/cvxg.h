@@ -285,7 +285,8 @@ int cvxg_affine_map(cvxg_ctx* dst, const double* u, double* x);
  * most the last 63), measured with HIP events on the stream each phase runs on; the steps never wait on them (only
  * this call synchronises): [0] assembly when not prefetched [1] Ruiz+scale [2] Cholesky (+fused forward solve)
  * [3] backward solve + residual [4] line search [5] the assembly SYRK alone (on its own stream when it was launched
- * behind the previous evaluation). */
+ * behind the previous evaluation).  enabled = 1 records only the assembly and Cholesky phases ([0], [2], [5]): every
+ * event record leaves the GPU idle a few microseconds between kernels; any other non-zero value records every phase. */
 int cvxg_set_timing(cvxg_ctx* ctx, int enabled);
 int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count);
 

@@ -62,7 +62,7 @@ class OracleEngine:
         self.it += 1
         return types.SimpleNamespace(done=not took, took_step=int(took), step=float(st))
 
-    def set_timing(self, on):
+    def set_timing(self, on, all_phases=True):
         pass
 
     def phase_times(self):
