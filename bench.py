@@ -163,10 +163,10 @@ def cpu_baseline_blas(spec, steps: int = 3):
                        f"steps ({ts:.3f} s/step)")}
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
 
 
-def pmc_traffic(kernel_prefixes):
+def pmc_traffic(kernel_prefixes, exclude=()):
     """HBM bytes of one phase from the committed rocprofv3 PMC passes (scripts/pmc_traffic.py: FETCH_SIZE x2 +
     WRITE_SIZE, gfx950 corrections), summed over the launches the phase consists of (for the assembly: the main
     wave, the split-K tail and the ordered reduce, the same region the HIP events time); None if absent."""
@@ -176,7 +176,8 @@ def pmc_traffic(kernel_prefixes):
         return None, None
     total, used = 0.0, []
     for k, v in sorted(doc.get("kernels", {}).items()):
-        if any(p in k for p in kernel_prefixes):  # template kernels carry a "void " prefix and "<N>"
+        if any(p in k for p in kernel_prefixes) and not any(k.endswith(x) for x in exclude):
+            # (template kernels carry a "void " prefix and "<N>")
             total += v["hbm_bytes_per_launch"]
             used.append(k)
     if not used:
@@ -340,7 +341,8 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     kkt_ms = float(np.mean(ruiz_ms)) + chol + float(np.mean(solve_ms))
     flops_chol = n ** 3 / 3.0 + n * n / 2.0 + n / 6.0  # dpotrf flops; all but O(n^2) are trailing SYRK/GEMM
     frac = (lambda a: a / FP64_MFMA_PEAK_TFLOPS if a is not None else None)  # noqa: E731
-    chol_traffic, chol_src = pmc_traffic(("cvxg::k_chol_dataflow",)) if wl == "C3" else (None, None)
+    chol_traffic, chol_src = (pmc_traffic(("cvxg::k_chol_dataflow",), exclude=("/short",)) if wl == "C3"
+                              else (None, None))  # ("/short": attempts voided by an open Ruiz lookahead)
     chol_sq = None
     if wl == "C3":  # MFMA utilisation of the Cholesky from the committed SQ counter passes (scripts/pmc_sq.sh)
         try:
