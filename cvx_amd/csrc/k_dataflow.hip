@@ -477,9 +477,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
           df_put(cs.Sa, va);
         }
+        potrf64w_reset(ps);  // the slices leave POTRF's L^-1 workspace and flags alone: clear them off the chain
         mark(k, 1, 1);
         const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
-        double* Lp = ps.X;      // L_b,k, row stride DF_SP
+        // L_b,k, row stride DF_SP: written over A_b,k in Sa (every wave holds its row-block of A in af before the first
+        // slice's barrier), where it stays for the rhs correction at the end of POTRF(b) — no copy before POTRF
+        double* Lp = cs.Sa;
         // row-block cb of L_kk^-1 (published by the other workgroup's POTRF(k) as cflag[k] reaches cb + 1) is
         // loaded into registers one slice ahead when it is already published, so its latency hides behind the
         // MFMAs of the current slice
@@ -547,11 +550,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           const int ib = kChIB[wv][q], jb = kChJB[wv][q];
           if (ib >= 0) c16_store(ps.S + 16 * ib * P64_SP + 16 * jb, P64_SP, dacc[q], lane);
         }
-        // keep L_b,k for the rhs correction at the end of POTRF(b) (X is POTRF's workspace)
-        for (int t = tid; t < NB * NB / 2; t += 256) {
-          const int rr = t >> 5, cc = 2 * (t & 31);
-          *reinterpret_cast<f64x2*>(cs.Sa + rr * DF_SP + cc) = *reinterpret_cast<const f64x2*>(Lp + rr * DF_SP + cc);
-        }
         publish(df_tri(b, k), k + 1);  // L_b,k stored
         mark(k, 1, 2);
       }
@@ -584,8 +582,10 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         mark(k, 2, 2);
         return true;
       };
-      potrf64w_reset(ps);
-      __syncthreads();
+      if (b == 0) {
+        potrf64w_reset(ps);
+        __syncthreads();
+      }  // b > 0: reset behind the staging, the tile's LDS stores behind publish()'s barrier
       if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
