@@ -547,7 +547,9 @@ static bool spec_eval_ok(const cvxg_ctx* ctx) {
 }
 // taken: the line search accepted t = 1 along s = dx, and the speculative evaluation at x1 = x + dx (bitwise the
 // x + s t of the step) is the constraint evaluation at the new x
-static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false) {
+// ahead: the prefetched assembly belongs to the next step (the end-of-step prefetch, timed in ring slot tick + 1) or
+// to this one (a step that starts without an evaluation, slot tick)
+static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false, bool ahead = true) {
   hipStream_t s = ctx->s;
   const int np = ctx->np, mp = ctx->mp;
   if (taken) {
@@ -570,12 +572,13 @@ static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false) {
     // Taken: x (= x1, swapped in by the caller) and the constraint values were final before the line search's host
     // read, so s2 needs no wait on the main stream (one event marker less in front of the assembly)
     if (!taken) HIPC(ctx, hipEventRecord(ctx->ev_w, s));
-    const int nx = (ctx->tm.tick + 1) % TRING;  // timed as phase 5 of the step that will use it
+    const int nx = (ctx->tm.tick + (ahead ? 1 : 0)) % TRING;  // timed as phase 5 of the step that will use it
     if (ctx->tm.on) HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][0], s));
     CHK(assemble_hessian(ctx, nullptr, nullptr, s));
     if (ctx->tm.on) {
       HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][1], s));
-      ctx->tm.rec[nx][5] = ctx->tm.pf5 = true;
+      ctx->tm.rec[nx][5] = true;
+      if (ahead) ctx->tm.pf5 = true;
     }
     // the second stream's wait is issued after the assembly's launches: the GPU is idle until they are (the host's
     // hipStreamWaitEvent costs ~8 us, microbench/hostcost.hip)
@@ -2102,7 +2105,7 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
     info->norm_grad = ctx->normGrad;
     return CVXG_OK;
   }
-  if (!ctx->x_eval_valid) CHK(eval_at_x(ctx, true));
+  if (!ctx->x_eval_valid) CHK(eval_at_x(ctx, true, false, /*ahead=*/false));
   const double tol = pars->tolSolver;
   info->f = ctx->f_at_x;
   info->norm_grad = ctx->normGrad;
@@ -2299,7 +2302,7 @@ int cvxg_set_timing(cvxg_ctx* ctx, int enabled) {
       for (bool& r : slot) r = false;
   }
   tm.on = enabled != 0;
-  tm.all = enabled != 1;
+  tm.all = enabled != 2;  // 1: every phase; 2: only the assembly and Cholesky phases (the bench's timed region)
   return CVXG_OK;
 }
 

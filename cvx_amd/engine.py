@@ -252,7 +252,7 @@ class Engine:
 
     def set_timing(self, on: bool, all_phases: bool = True):
         """cvxg_set_timing: all_phases=False records only the assembly and Cholesky phases (fewer event markers)."""
-        self._check(self.lib.cvxg_set_timing(self.h, (2 if all_phases else 1) if on else 0))
+        self._check(self.lib.cvxg_set_timing(self.h, (1 if all_phases else 2) if on else 0))
 
     def ruiz_lookahead(self, sweeps: int = 0) -> int:
         """cvxg_set_ruiz_lookahead: the Ruiz sweeps the next Newton step launches (0 keeps the setting); returns how

@@ -31,9 +31,11 @@ extern "C" {
 #define CVXG_E_ARG 8             /* invalid argument or call order */
 #define CVXG_E_UNSUPPORTED 9     /* configuration outside this build (e.g. n > 65472) */
 
-/* Equality rows whose KKT right-hand sides ride the factorization's fused forward solve.  Wider equality blocks
- * (any p < n) take the same KKTSystem.solveWithCholFactor sequence with the right-hand sides solved by two triangular
- * solves on the factor and the p x p Schur complement factored by dpotrf (rocBLAS / rocSOLVER). */
+/* Equality rows whose KKT right-hand sides can ride the factorization's fused forward solve (small problems).  Wider
+ * equality blocks (any p < n) take the same KKTSystem.solveWithCholFactor sequence on the engine's own kernels
+ * (k_kkt.hip): the p + 1 right-hand sides by two many-column triangular solves on the factor, and the p x p Schur
+ * complement by a one-wave dpotf2-order factorization (p <= 64) or the dataflow Cholesky (p > 64).  rocBLAS /
+ * rocSOLVER are not on any per-step path. */
 #define CVXG_MAX_EQ 8
 
 typedef struct cvxg_ctx cvxg_ctx;
@@ -285,8 +287,8 @@ int cvxg_affine_map(cvxg_ctx* dst, const double* u, double* x);
  * most the last 63), measured with HIP events on the stream each phase runs on; the steps never wait on them (only
  * this call synchronises): [0] assembly when not prefetched [1] Ruiz+scale [2] Cholesky (+fused forward solve)
  * [3] backward solve + residual [4] line search [5] the assembly SYRK alone (on its own stream when it was launched
- * behind the previous evaluation).  enabled = 1 records only the assembly and Cholesky phases ([0], [2], [5]): every
- * event record leaves the GPU idle a few microseconds between kernels; any other non-zero value records every phase. */
+ * behind the previous evaluation).  enabled = 1 records every phase; enabled = 2 records only the assembly and Cholesky
+ * phases ([0], [2], [5]) -- every event record leaves the GPU idle a few microseconds between kernels. */
 int cvxg_set_timing(cvxg_ctx* ctx, int enabled);
 int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count);
 

@@ -81,12 +81,17 @@ static void fill_params(JNIEnv* env, jdoubleArray jp, jint maxIter, cvxg_params*
 
 /* cvxg_step_info as a double[22] (CvxgNative.StepInfo in INTEGRATION.md §2 reads it by these indices). */
 #define STEP_INFO_LEN 22
+static void step_info_row(const cvxg_step_info* s, double* o) {
+  const double v[STEP_INFO_LEN] = {s->t, s->f, s->norm_grad, s->q, s->newton_decrement, s->hnorm, s->trust_radius,
+                                   s->step, s->rel_err, s->min_diag, s->norm_grad_new, s->equality_gap,
+                                   (double)s->backtracks_c, (double)s->backtracks_armijo, (double)s->fallback,
+                                   (double)s->ruiz_sweeps, (double)s->regularized, (double)s->took_step,
+                                   (double)s->done, (double)s->iter, (double)s->ls_fresh, (double)s->ls_ties};
+  for (int i = 0; i < STEP_INFO_LEN; ++i) o[i] = v[i];
+}
 static void put_step_info(JNIEnv* env, jdoubleArray out, const cvxg_step_info* s) {
-  double o[STEP_INFO_LEN] = {s->t, s->f, s->norm_grad, s->q, s->newton_decrement, s->hnorm, s->trust_radius, s->step,
-                             s->rel_err, s->min_diag, s->norm_grad_new, s->equality_gap, (double)s->backtracks_c,
-                             (double)s->backtracks_armijo, (double)s->fallback, (double)s->ruiz_sweeps,
-                             (double)s->regularized, (double)s->took_step, (double)s->done, (double)s->iter,
-                             (double)s->ls_fresh, (double)s->ls_ties};
+  double o[STEP_INFO_LEN];
+  step_info_row(s, o);
   if (out) (*env)->SetDoubleArrayRegion(env, out, 0, STEP_INFO_LEN, o);
 }
 
@@ -111,6 +116,12 @@ JNIEXPORT void JNICALL Java_cvx_gpu_CvxgNative_destroy(JNIEnv* env, jclass cls, 
 JNIEXPORT jstring JNICALL Java_cvx_gpu_CvxgNative_lastError(JNIEnv* env, jclass cls, jlong h) {
   (void)cls;
   const char* s = cvxg_last_error(CTX(h));
+  return (*env)->NewStringUTF(env, s ? s : "");
+}
+
+JNIEXPORT jstring JNICALL Java_cvx_gpu_CvxgNative_version(JNIEnv* env, jclass cls) {
+  (void)cls;
+  const char* s = cvxg_version();
   return (*env)->NewStringUTF(env, s ? s : "");
 }
 
@@ -142,6 +153,14 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_setObjectiveKL(JNIEnv* env, jclas
   dfree(pw);
   dfree(pB);
   return rc;
+}
+
+/* Dist_KL.objectiveFunction(n) (Dist_KL.scala:223-239), the KL primal objective of kl_1 / kl_2: no data beyond the
+ * outcome count n (cvxg_set_objective_kl_primal). */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_setObjectiveKLPrimal(JNIEnv* env, jclass cls, jlong h, jint nout) {
+  (void)env;
+  (void)cls;
+  return cvxg_set_objective_kl_primal(CTX(h), nout);
 }
 
 JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_setIneq(JNIEnv* env, jclass cls, jlong h, jdoubleArray A, jint ldA,
@@ -391,7 +410,68 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_batchBarrierSolve(JNIEnv* env, jc
   return rc;
 }
 
+/* batchNewtonStep(handles[k], maxIter, params[6], info[22 k], status[k]): one inner Newton iteration on each of k
+ * independent contexts concurrently (cvxg_batch_newton_step); context i's cvxg_step_info at info[22 i ..] */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_batchNewtonStep(JNIEnv* env, jclass cls, jlongArray handles,
+                                                               jint maxIter, jdoubleArray jp, jdoubleArray info,
+                                                               jintArray status) {
+  (void)cls;
+  cvxg_params p;
+  fill_params(env, jp, maxIter, &p);
+  jsize k = (*env)->GetArrayLength(env, handles);
+  jlong* hv = (jlong*)malloc((size_t)(k > 0 ? k : 1) * sizeof(jlong));
+  cvxg_ctx** cv = (cvxg_ctx**)malloc((size_t)(k > 0 ? k : 1) * sizeof(cvxg_ctx*));
+  /* zeroed: an argument error (CVXG_E_ARG) returns before any instance writes its slot */
+  cvxg_step_info* sv = (cvxg_step_info*)calloc((size_t)(k > 0 ? k : 1), sizeof(cvxg_step_info));
+  jint* st = (jint*)calloc((size_t)(k > 0 ? k : 1), sizeof(jint));
+  double* o = (double*)malloc((size_t)(k > 0 ? STEP_INFO_LEN * k : 1) * sizeof(double));
+  if (!hv || !cv || !sv || !st || !o) {
+    free(hv), free(cv), free(sv), free(st), free(o);
+    throw_oom(env);
+    return CVXG_E_ARG;
+  }
+  if (k > 0) (*env)->GetLongArrayRegion(env, handles, 0, k, hv);
+  for (jsize i = 0; i < k; ++i) cv[i] = CTX(hv[i]);
+  jint rc = cvxg_batch_newton_step(k, cv, &p, sv, (int*)st);
+  for (jsize i = 0; i < k; ++i) step_info_row(&sv[i], o + STEP_INFO_LEN * i);
+  if (k > 0) {
+    if (info) (*env)->SetDoubleArrayRegion(env, info, 0, STEP_INFO_LEN * k, o);
+    (*env)->SetIntArrayRegion(env, status, 0, k, st);
+  }
+  free(hv), free(cv), free(sv), free(st), free(o);
+  return rc;
+}
+
 /* ---- primal-dual solver --------------------------------------------------------------------------------- */
+
+/* pdDirection(h, maxIter, params[6], t, x[n], lambda[m], dx[n] (nullable), dlambda[m] (nullable), info[9]
+ * (nullable)): the PrimalDualSolver search direction (cvxg_pd_direction).  info = {t, s0, step, normResidual, relErr,
+ * backtracks, fallback, ruizSweeps, regularized} */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_pdDirection(JNIEnv* env, jclass cls, jlong h, jint maxIter,
+                                                           jdoubleArray jp, jdouble t, jdoubleArray x,
+                                                           jdoubleArray lambda, jdoubleArray dx, jdoubleArray dlambda,
+                                                           jdoubleArray info) {
+  (void)cls;
+  int ok = 1;
+  cvxg_params p;
+  cvxg_pd_step_info si;
+  fill_params(env, jp, maxIter, &p);
+  double* px = din(env, x, &ok);
+  double* pl = din(env, lambda, &ok);
+  double* pd = dout(env, dx, &ok);
+  double* pdl = dout(env, dlambda, &ok);
+  jint rc = ok ? cvxg_pd_direction(CTX(h), &p, t, px, pl, pd, pdl, &si) : CVXG_E_ARG;
+  dput(env, dlambda, pdl, rc);
+  dput(env, dx, pd, rc);
+  dfree(pl);
+  dfree(px);
+  if (rc == CVXG_OK && info) {
+    double o[9] = {si.t, si.s0, si.step, si.norm_residual, si.rel_err, (double)si.backtracks, (double)si.fallback,
+                   (double)si.ruiz_sweeps, (double)si.regularized};
+    (*env)->SetDoubleArrayRegion(env, info, 0, 9, o);
+  }
+  return rc;
+}
 
 /* pdSolve(h, maxIter, params[6], out[6]) -> PrimalDualSolver.solve on the device (cvxg_pd_solve) */
 JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_pdSolve(JNIEnv* env, jclass cls, jlong h, jint maxIter, jdoubleArray jp,

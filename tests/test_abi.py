@@ -121,9 +121,43 @@ def test_jni_glue_binds_every_scala_native_and_every_step_entry():
     scala_names = set(re.findall(r"@native def (\w+)", doc))
     assert c_names == scala_names, (c_names ^ scala_names)
     for s in ("centering", "centeringBegin", "centeringResume", "newtonStep", "newtonDirection", "barrierEval",
-              "constraintValues", "activeSet", "setQuad", "batchBarrierSolve"):
+              "constraintValues", "activeSet", "setQuad", "batchBarrierSolve", "batchNewtonStep",
+              "setObjectiveKLPrimal", "pdDirection"):
         assert s in c_names
     assert "GetPrimitiveArrayCritical" not in c_src  # no critical region spans a GPU call
+
+
+# C-ABI entry points a Scala caller has no use for: instrumentation and the host-only schedule dump
+_JNI_EXEMPT = {"cvxg_set_timing", "cvxg_get_phase_times", "cvxg_set_ruiz_lookahead", "cvxg_chol_schedule"}
+
+
+def _camel(sym):
+    """cvxg_set_objective_kl_primal -> setObjectiveKlPrimal (compared case-insensitively below)."""
+    parts = sym[len("cvxg_"):].split("_")
+    return parts[0] + "".join(p.capitalize() for p in parts[1:])
+
+
+def test_jni_binds_every_reference_facing_entry_point():
+    """Every cvxg_* the header declares has a Java_cvx_gpu_CvxgNative_* export in the glue and an @native def in
+    INTEGRATION.md (names compared case-insensitively: setObjectiveKL for cvxg_set_objective_kl), except the listed
+    diagnostics; and every export forwards to the entry point it is named after."""
+    c_src = open(os.path.join(ROOT, "jni", "cvxg_jni.c")).read()
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    c_names = {n.lower(): n for n in re.findall(r"Java_cvx_gpu_CvxgNative_(\w+)\s*\(", c_src)}
+    scala_names = {n.lower() for n in re.findall(r"@native def (\w+)", doc)}
+    missing = []
+    for sym in _header_symbols():
+        if sym in _JNI_EXEMPT:
+            continue
+        key = _camel(sym).lower()
+        if key not in c_names or key not in scala_names:
+            missing.append(sym)
+            continue
+        body = c_src[c_src.index("Java_cvx_gpu_CvxgNative_" + c_names[key] + "("):]
+        body = body[:body.index("\n}\n")]
+        assert sym + "(" in body, f"{c_names[key]} does not call {sym}"
+    assert not missing, missing
+    assert not (_JNI_EXEMPT - set(_header_symbols())), "exempt names must exist in the header"
 
 
 # Scala / Breeze names the glue uses that are not defined in the reference's own sources
