@@ -163,7 +163,27 @@ def cpu_baseline_blas(spec, steps: int = 3):
                        f"steps ({ts:.3f} s/step)")}
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
+def latest_profile(name):
+    """The newest committed profile file of that name (profiles/r04, then r03, r02)."""
+    for r in ("r04", "r03", "r02"):
+        p = os.path.join(ROOT, "profiles", r, name)
+        if os.path.exists(p):
+            return p
+    return os.path.join(ROOT, "profiles", "r04", name)
+
+
+PMC_TRAFFIC = latest_profile("pmc_traffic.json")
+# the same rooflines recomputed from the committed rocprofv3 kernel trace of `bench.py --steps 20 --warmup 5
+# --no-cpu-baseline` (scripts/trace_roofline.py: sums of kernel durations over the timed steps)
+TRACE_ROOFLINE = os.path.join(ROOT, "profiles", "r04", "trace_roofline.json")
+
+
+def trace_roofline():
+    try:
+        d = json.load(open(TRACE_ROOFLINE))
+        return d, os.path.relpath(TRACE_ROOFLINE, ROOT)
+    except (OSError, ValueError):
+        return None, None
 
 
 def pmc_traffic(kernel_prefixes, exclude=()):
@@ -346,8 +366,9 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     chol_sq = None
     if wl == "C3":  # MFMA utilisation of the Cholesky from the committed SQ counter passes (scripts/pmc_sq.sh)
         try:
-            d = json.load(open(os.path.join(ROOT, "profiles", "r02", "pmc_chol_dataflow_sq.json")))["derived"]
-            chol_sq = {"source": "profiles/r02/pmc_chol_dataflow_sq.json",
+            sq_path = latest_profile("pmc_chol_dataflow_sq.json")
+            d = json.load(open(sq_path))["derived"]
+            chol_sq = {"source": os.path.relpath(sq_path, ROOT),
                        "mfma_work_over_algorithmic": d["mfma_work_over_algorithmic"],
                        "mfma_busy_vs_clock_limited_peak": d[
                            "mfma_busy_vs_clock_limited_peak (x 0.93, the SYRK main wave's measured fraction)"]}
@@ -358,11 +379,26 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
                 "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(tf(flops_chol, chol)),
                 "traffic": chol_traffic, "traffic_unit": "bytes/factorization (algorithmic: 8 n^2 = 134 MB, the "
                 "lower triangle read and written once)", "traffic_source": chol_src, "pmc_sq": chol_sq}
-    comb_ach = tf(flops_syrk + flops_chol, syrk + chol)
-    combined = {"what": "SURVEY.md §8d: (assembly SYRK + POTRF trailing flops) / (SYRK + Cholesky kernel time)",
-                "achieved": comb_ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(comb_ach)}
     traffic, traffic_src = (pmc_traffic(("cvxg::k_syrk_direct", "cvxg::k_syrk_reduce")) if wl == "C3"
                             else (None, None))
+    assembly = {"kernel": "k_syrk_direct + k_syrk_reduce (H = tP + A'diag(w)A)", "achieved": ach,
+                "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(ach), "traffic": traffic,
+                "traffic_unit": "bytes/assembly (main wave + split-K tail + reduce)", "traffic_source": traffic_src,
+                "flops_per_launch": flops_syrk, "avg_launch_ms": syrk}
+    comb_ach = tf(flops_syrk + flops_chol, syrk + chol)
+    tr, tr_src = trace_roofline() if wl == "C3" else (None, None)
+    if tr is not None:
+        assembly["frac_trace"] = tr["assembly_frac"]
+        trailing["frac_trace"] = tr["cholesky_frac"]
+    both = (traffic + chol_traffic) if (traffic is not None and chol_traffic is not None) else None
+    # "% MFMA roofline on trailing SYRK" = (assembly SYRK + POTRF trailing flops) / (their kernel time)
+    roofline = {"bound": "mfma", "kernel": "assembly SYRK + Cholesky (SURVEY.md §8d: the SYRK-type flops of the "
+                "assembly and of the POTRF trailing updates over the two phases' kernel time)",
+                "achieved": comb_ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(comb_ach),
+                "frac_trace": tr["combined_frac"] if tr is not None else None, "trace_source": tr_src,
+                "traffic": both, "traffic_unit": "bytes/step (assembly + factorization, PMC)",
+                "flops_per_launch": flops_syrk + flops_chol, "avg_launch_ms": syrk + chol,
+                "assembly": assembly, "trailing": trailing}
     out = {
         "metric": METRIC,
         "value": value,
@@ -379,13 +415,7 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
         "config": {"workload": workload, "n": n, "m": m,
                    "parallelism": f"replicas x{world}: one independent QP per GPU (config C5), "
                                   "RCCL gather of results after the timed region"},
-        "roofline": {"bound": "mfma", "kernel": "k_syrk_direct (H = tP + A'diag(w)A)",
-                     "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": frac(ach), "traffic": traffic,
-                     "traffic_unit": "bytes/assembly (main wave + split-K tail + reduce)",
-                     "traffic_source": traffic_src,
-                     "flops_per_launch": flops_syrk, "avg_launch_ms": syrk,
-                     "trailing": trailing, "combined": combined},
+        "roofline": roofline,
         "phases_ms": {"syrk": syrk, "ruiz": float(np.mean(ruiz_ms)), "cholesky_fused_fwd": chol,
                       "bwd_solve_residual": float(np.mean(solve_ms)), "line_search": float(np.mean(ls_ms))},
         "kkt_factor_solve_per_s": 1e3 / kkt_ms if kkt_ms > 0 else None,
@@ -397,16 +427,184 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     return out, gathered
 
 
+def run_full_solve(args):
+    """--workload C3FULL ("steady state over a full barrier solve"): one complete C3 barrier solve from
+    x0 with the reference's standard parameters (SolverParams.scala:35-46: maxIter 1000 per centering), the t-loop of
+    BarrierSolver.scala:70-117 (t = 1, t *= 10 per centering until m / t < tolSolver) driven step by step through
+    cvxg_newton_step.  Solve 1 (timers off) gives Newton steps/s over the whole path; solve 2 (every phase timed, the
+    ring read every 50 steps) gives the per-phase means over the path.  Both report the Ruiz sweep histogram, the
+    regularized refactorizations, the fallbacks and the steps per centering.  One GPU, one instance."""
+    import torch
+
+    from cvx_amd.api import SolverParams
+    from cvx_amd.engine import Engine
+    torch.cuda.set_device(0)
+    n, m = args.n or 4096, args.m or 8192
+    from cvx_amd import problems as Z
+    spec = Z.random_qp(n, m, instance=0)
+    pars = SolverParams.standardParams()
+    eng = Engine(n, m, 0, device=0)
+    eng.load_problem(spec)
+
+    def solve(timed):
+        eng.set_x(spec["x0"])
+        t, steps, per_center, hist = 1.0, 0, [], {}
+        reg = fb = full = 0
+        ph_sum, ph_n = np.zeros(8), 0
+        if timed:
+            eng.set_timing(True, all_phases=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        while True:  # BarrierSolver.scala:70-117: center at t, gap = m / t, stop below tolSolver, else t *= mu
+            eng.centering_begin(t)
+            k = 0
+            while True:  # every call computes one Newton direction (a KKT solve); done ends the centering
+                st = eng.newton_step(pars)
+                k += 1
+                steps += 1
+                hist[st.ruiz_sweeps] = hist.get(st.ruiz_sweeps, 0) + 1
+                reg += st.regularized
+                fb += int(st.fallback != 0)
+                full += int(st.took_step == 1 and st.step == 1.0)
+                if timed and steps % 50 == 0:  # the timer ring holds 63 steps: read and restart it
+                    ph_sum += eng.phase_times() * 50
+                    ph_n += 50
+                    eng.set_timing(True, all_phases=True)
+                if st.done:
+                    break
+            per_center.append(k)
+            if m / t < pars.tolSolver or len(per_center) >= 100:
+                break
+            t *= 10.0
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if timed:
+            rest = steps - ph_n
+            if rest > 0:
+                ph_sum += eng.phase_times() * rest
+                ph_n += rest
+            eng.set_timing(False)
+        return dict(elapsed=el, steps=steps, per_center=per_center, hist=hist, reg=reg, fb=fb, full=full,
+                    phases=(ph_sum / max(ph_n, 1)).tolist(), x=eng.get_x())
+
+    a = solve(False)
+    b = solve(True)
+    eng.close()
+    same = bool(np.array_equal(a["x"], b["x"]))
+    ph = b["phases"]
+    out = {"metric": METRIC, "value": a["steps"] / a["elapsed"], "unit": "Newton KKT solves/s", "n_gpus": 1,
+           "steps": a["steps"], "warmup": 0, "ms_per_step": a["elapsed"] / a["steps"] * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic (seeded generators of cvx_amd/problems.py, SURVEY.md §8d)",
+           "config": {"workload": f"C3FULL: one complete barrier solve of the C3 random dense QP n={n} m={m} from x0, "
+                                  "standard parameters (maxIter 1000 per centering), t-loop to m/t < 1e-8",
+                      "n": n, "m": m},
+           "solve_s": a["elapsed"], "centerings": len(a["per_center"]), "steps_per_centering": a["per_center"],
+           "ruiz_sweep_histogram": {str(k): v for k, v in sorted(a["hist"].items())},
+           "regularized_refactorizations": a["reg"], "fallbacks": a["fb"], "line_search_full_steps": a["full"],
+           "phases_ms_timed_solve": {"assembly_prefetched": ph[5], "assembly_inline": ph[0], "ruiz": ph[1],
+                                     "cholesky_fused_fwd": ph[2], "bwd_solve_residual": ph[3], "line_search": ph[4]},
+           "timed_solve_s": b["elapsed"], "timed_solve_same_x": same}
+    return out
+
+
+def run_shared_gpu(args):
+    """--workload C3X2 (side workload, not the headline): `--instances` independent C3 problems (seeds 20261015 + i)
+    on ONE GPU, each with its own context and stream, each driven by its own host thread through cvxg_newton_step
+    (the t-loop of BarrierSolver.scala:70-117 per instance); aggregate Newton steps/s over K steps per instance
+    against one instance alone on the same box.  Shows how much of the Cholesky chain's idle workers and the
+    host/launch gaps a second independent instance reclaims (config C5's independence, one GPU).  Also times the
+    lockstep form, cvxg_batch_newton_step (one call advances every instance by one step)."""
+    import threading
+
+    import torch
+
+    from cvx_amd import problems as Z
+    from cvx_amd.api import SolverParams
+    from cvx_amd.engine import Engine, batch_newton_step
+    torch.cuda.set_device(0)
+    n, m, k = args.n or 4096, args.m or 8192, max(2, args.instances)
+    pars = SolverParams.standardParams()
+    specs = [Z.random_qp(n, m, instance=i) for i in range(k)]
+    engs = []
+    for spec in specs:
+        e = Engine(n, m, 0, device=0)
+        e.load_problem(spec)
+        engs.append(e)
+    ts = [1.0] * k
+
+    def begin(i):
+        engs[i].set_x(specs[i]["x0"])
+        ts[i] = 1.0
+        engs[i].centering_begin(1.0)
+
+    def step(i, st=None):
+        st = st if st is not None else engs[i].newton_step(pars)
+        if st.done:
+            if m / ts[i] < pars.tolSolver:
+                begin(i)
+            else:
+                ts[i] *= 10.0
+                engs[i].centering_begin(ts[i])
+
+    def run(i, steps):
+        for _ in range(steps):
+            step(i)
+
+    for i in range(k):
+        begin(i)
+        run(i, args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()  # one instance alone
+    run(0, args.steps)
+    torch.cuda.synchronize()
+    one = args.steps / (time.perf_counter() - t0)
+    th = [threading.Thread(target=run, args=(i, args.steps)) for i in range(k)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()  # all instances, one host thread each
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    agg = k * args.steps / el
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()  # lockstep: cvxg_batch_newton_step
+    for _ in range(args.steps):
+        infos, st = batch_newton_step(engs, pars)
+        assert st == [0] * k, st
+        for i in range(k):
+            step(i, infos[i])
+    torch.cuda.synchronize()
+    lock = k * args.steps / (time.perf_counter() - t0)
+    for e in engs:
+        e.close()
+    return {"metric": METRIC, "value": agg, "unit": "Newton KKT solves/s", "n_gpus": 1, "steps": args.steps * k,
+            "warmup": args.warmup, "ms_per_step": el / (k * args.steps) * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded generators of cvx_amd/problems.py, SURVEY.md §8d)",
+            "config": {"workload": f"C3X2: {k} independent C3 random dense QPs n={n} m={m} sharing one MI355X, one "
+                                   "context + stream + host thread each, full barrier Newton iterations",
+                       "n": n, "m": m, "instances": k},
+            "one_instance_steps_per_s": one, "aggregate_over_one": agg / one,
+            "lockstep_batch_steps_per_s": lock}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C3B", "C3EQ", "C4", "C4P", "C2PD", "C3PD"],
+    ap.add_argument("--workload", default="C3",
+                    choices=["C2", "C3", "C3B", "C3EQ", "C4", "C4P", "C2PD", "C3PD", "C3FULL", "C3X2"],
                     help="C3 (default, the metric's config): random dense QP n=4096 m=8192; C2: n=1024 m=2048; "
                          "C3B: C3 plus 9216 sparse bound / difference rows; C4: KL dual, 2048 outcomes, k=512; "
                          "C2PD / C3PD: the primal-dual solver (solverType PD) on C2 / C3, steps = its KKT solves; "
-                         "C3EQ: C3 with --p equality rows (KKT path); C4P: the direct KL solve, n = 2048")
+                         "C3EQ: C3 with --p equality rows (KKT path); C4P: the direct KL solve, n = 2048; "
+                         "C3FULL: one complete C3 barrier solve with standard parameters (steady state over the path); "
+                         "C3X2: --instances independent C3 problems sharing one GPU (aggregate steps/s)")
+    ap.add_argument("--instances", type=int, default=2, help="instances of C3X2")
     ap.add_argument("--p", type=int, default=64, help="equality rows of C3EQ")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--m", type=int, default=None)
@@ -416,6 +614,12 @@ def main():
 
     from cvx_amd import dist as D
     rank, _, world = D.env_rank()
+    if args.workload == "C3FULL":
+        print(json.dumps(run_full_solve(args)), flush=True)
+        return
+    if args.workload == "C3X2":
+        print(json.dumps(run_shared_gpu(args)), flush=True)
+        return
     out, _ = run_rank(args)
     if rank == 0:
         if not args.no_cpu_baseline and world == 1 and args.workload == "C3":

@@ -434,15 +434,19 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   auto code = [](const Task& x) {
     return ((unsigned)x.type << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j;
   };
+  // chain tasks (k_dataflow.hip: the chain workgroup of block b runs TRSM(b,b-2), UPDATE(b,b,b-2), UPDATE(b,b-1,b-2),
+  // then TRSM(b,b-1) and UPDATE(b,b,b-1), then POTRF(b))
   auto is_chain = [](const Task& x) {
-    return x.type == 0 || (x.type == 1 && x.i == x.k + 1) || (x.type == 2 && x.i == x.j && x.j == x.k + 1);
+    return x.type == 0 || (x.type == 1 && (x.i == x.k + 1 || x.i == x.k + 2)) ||
+           (x.type == 2 && x.i == x.k + 1 && x.j == x.i) ||
+           (x.type == 2 && x.i == x.k + 2 && (x.j == x.i || x.j == x.i - 1));
   };
-  // the worker tasks the chain's staging of block k+2 waits on -- TRSM(k+2,k), UPDATE(k+2,k+1,k), UPDATE(k+2,k+2,k)
-  // -- are emitted as soon as their last dependency is (not at their simulated start), so a worker claims them early
-  // and starts the moment their inputs land, instead of when the queue reaches them behind trailing updates.  The
-  // order stays topological: every dependency is emitted (or a chain task) before them.
+  // the worker tasks the chain's panel work on block row k+3 waits on -- TRSM(k+3,k) and the updates of tiles
+  // (k+3, k+1..k+3) with panel k -- are emitted as soon as their last dependency is (not at their simulated start), so
+  // a worker claims them early and starts the moment their inputs land, instead of when the queue reaches them behind
+  // trailing updates.  The order stays topological: every dependency is emitted (or a chain task) before them.
   auto is_eager = [](const Task& x) {
-    return (x.type == 1 && x.i == x.k + 2) || (x.type == 2 && x.i == x.k + 2 && (x.j == x.i || x.j == x.i - 1));
+    return (x.type == 1 && x.i == x.k + 3) || (x.type == 2 && x.i == x.k + 3 && x.j >= x.i - 2);
   };
   std::vector<char> emitted(T.size(), 0);
   size_t nsched = 0;
@@ -796,7 +800,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   if (ctx->hctrl->df_status != 0)
     return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
   if (ctx->df_trace) {  // instrumentation only: task order + timeline of this factorization
-    std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk));
+    std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 6 * ctx->nblk));
     std::vector<unsigned> ord(ctx->df_ntasks);
     CHK(copy_sync(ctx, tr.data(), ctx->df_trace, tr.size() * 8, hipMemcpyDeviceToHost));
     CHK(copy_sync(ctx, ord.data(), ctx->df_tasks, ord.size() * 4, hipMemcpyDeviceToHost));
@@ -1047,7 +1051,7 @@ static int kkt_alloc(cvxg_ctx* ctx, bool fused) {
       ctx->s_nblk = ps / NB;
       CHK(dalloc(ctx, &ctx->sL, (size_t)ps * ps));
       HIPC(ctx, hipMemsetAsync(ctx->sL, 0, (size_t)ps * ps * sizeof(double), ctx->s));
-      CHK(dalloc(ctx, &ctx->sLinv, (size_t)ctx->s_nblk * NB * NB));
+      CHK(dalloc(ctx, &ctx->sLinv, (size_t)ctx->s_nblk * (NB * NB + DF_LR_REC)));
       CHK(dalloc(ctx, &ctx->kzp, (size_t)ps));
       CHK(dalloc(ctx, &ctx->sw, (size_t)ps));
       std::vector<unsigned> order = chol_schedule(ctx->s_nblk, ctx->ncu);
@@ -1583,7 +1587,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   for (double** v : {&ctx->c, &ctx->d, &ctx->invd, &ctx->w, &ctx->logd, &ctx->e}) CHK(dalloc(ctx, v, std::max(mp, np)));
   CHK(dalloc(ctx, &ctx->H, np * np));
   CHK(dalloc(ctx, &ctx->L, np * np));
-  CHK(dalloc(ctx, &ctx->Linv, (size_t)ctx->nblk * NB * NB));
+  CHK(dalloc(ctx, &ctx->Linv, (size_t)ctx->nblk * (NB * NB + DF_LR_REC)));  // + the chain packages (k_dataflow.hip)
   {  // dataflow Cholesky: task order for this tile count, work words
     (void)hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device);
     ctx->ncu = std::max(ctx->ncu, 1);
@@ -1594,7 +1598,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     CHK(dalloc(ctx, &ctx->df_work, chol_dataflow_work_ints(ctx->nblk)));
     if (const char* e = getenv("CVXG_DF_TRACE")) {  // instrumentation only: the task timeline of the last factorization
       ctx->df_trace_path = e;
-      CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk)));
+      CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 6 * ctx->nblk)));
     }
   }
   CHK(dalloc(ctx, &ctx->bwd_flags, bwd_work_ints(ctx->nblk)));
@@ -2314,12 +2318,17 @@ int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count) {
   const Timer& tm = ctx->tm;
   for (int i = 0; i < count && i < NT; ++i) {
     double sum = 0.0;
+    int got = 0;
     for (int k = 1; k <= tm.steps; ++k) {  // the completed steps, newest first
       const int sl = ((tm.tick - k) % TRING + TRING) % TRING;
       float v = 0.f;
-      if (tm.rec[sl][i] && hipEventElapsedTime(&v, tm.ev[sl][i][0], tm.ev[sl][i][1]) == hipSuccess) sum += v;
+      if (tm.rec[sl][i] && hipEventElapsedTime(&v, tm.ev[sl][i][0], tm.ev[sl][i][1]) == hipSuccess) {
+        sum += v;
+        ++got;
+      }
     }
-    ms[i] = tm.steps > 0 ? sum / tm.steps : 0.0;
+    // per recorded occurrence: the first step after cvxg_set_timing may run an assembly prefetched before timing was on
+    ms[i] = got > 0 ? sum / got : 0.0;
   }
   (void)hipGetLastError();  // never leave a timing error sticky for the next launch check
   return CVXG_OK;

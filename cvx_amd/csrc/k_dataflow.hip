@@ -1,8 +1,10 @@
 // k_dataflow.hip — the whole regularized-Cholesky factorization (right-looking dpotrf('L'),
 // MatrixUtils.scala:452-461) with the fused forward solve, as ONE persistent launch over a tile DAG.
 //
-// Tiles are 64 x 64 (NB).  Tasks, in an order fixed on the host by list-scheduling the DAG with its
-// critical-path priorities (cvxg.cpp, build_chol_schedule):
+// Tiles are 64 x 64 (NB).  Two chain workgroups run the critical path: for diagonal block b, panel b-2 applied to
+// block row b (TRSM(b,b-2), UPDATE(b,b,b-2), UPDATE(b,b-1,b-2)), then TRSM(b,b-1) and UPDATE(b,b,b-1) in slices, then
+// POTRF(b).  The other tasks, in an order fixed on the host by list-scheduling the DAG with its critical-path
+// priorities (cvxg.cpp, build_chol_schedule):
 //   POTRF(k)      factor the diagonal tile, L_kk^-1 into Linv[k], forward-solve rhs block k
 //   TRSM(i,k)     L_ik = A_ik L_kk^-T (MFMA, product with L_kk^-1); rhs_i -= L_ik w_k
 //   UPDATE(i,j,k) A_ij -= L_ik L_jk^T (MFMA), k < j <= i
@@ -22,6 +24,7 @@ namespace cvxg {
 
 
 constexpr int DF_SP = NB + 2;  // LDS row stride (doubles) of a staged 64 x 64 operand: conflict-free fragments
+constexpr int DF_CH_REC = 6;  // trace records per diagonal block (the chain's stamps; CVXG_DF_TRACE)
 constexpr int DF_SMEM = 4 * NB * (NB + 2) + 2 * 16 * (NB + 2) + 512;  // doubles (~142 KB): > half the CU's LDS, so one workgroup per CU
 
 // LDS of the critical-chain workgroup: POTRF's workspace (tile, L^-1, rhs) + the TRSM tile L_k+1,k + L' w_k
@@ -384,6 +387,51 @@ __device__ __forceinline__ void ch_update(d4f (&dacc)[3], const double* Lp, int 
                                                        lf[kChJB[W][q] < 0 ? 0 : kChJB[W][q]][st], dacc[q], 0, 0, 0);
 }
 
+// D_b's lower 16 x 16 blocks of this wave (kChIB / kChJB) into MFMA accumulators, from L (or Q folded from H on the
+// tile's first touch)
+__device__ __forceinline__ void ch_load_diag(d4f (&dacc)[3], const double* src, int ld, int b, bool fold,
+                                             const QFold& qf, int wv, int lane) {
+  const Sc1Mem mD(const_cast<double*>(src) + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int ib = kChIB[wv][q], jb = kChJB[wv][q];
+    if (ib >= 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = 16 * ib + (lane >> 4) + 4 * r, cc = 16 * jb + (lane & 15);
+        const double h = mD.ld(rr * ld + cc);
+        dacc[q][r] = fold ? qf_entry(qf, b * NB + rr, b * NB + cc, h) : h;
+      }
+    }
+  }
+}
+// TRSM on the chain workgroup: acc[cb] = A[16 w.., :] X[16 cb.., :]' for the four column blocks (X = L^-1 in LDS, row
+// stride P64_SP, zero above the diagonal, so K = 16 (cb + 1)), each block one accumulation chain in K order -- df_trsm's
+// sums -- with the four chains interleaved for latency.
+__device__ __forceinline__ void ch_trsm_seq(d4f (&acc)[4], const double (&af)[16], const double* X, int lane) {
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) acc[cb] = d4f{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      if (s < 4 * (cb + 1))
+        acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s], X[(16 * cb + (lane & 15)) * P64_SP + 4 * s + (lane >> 4)],
+                                                       acc[cb], 0, 0, 0);
+}
+// acc[cb] -= A[16 rows, :] B[16 cb.., :]' over K = 64 (A: this wave's row-block, B: a 64 x 64 tile, both row stride
+// DF_SP in LDS): df_update's single accumulation chain per 16 x 16 block, in K order
+__device__ __forceinline__ void ch_gemm_nt(d4f (&acc)[4], const double* A, const double* B, int lane) {
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int kk = 4 * s + (lane >> 4);
+    const double a = -A[(lane & 15) * DF_SP + kk];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, B[(16 * cb + (lane & 15)) * DF_SP + kk], acc[cb], 0, 0, 0);
+  }
+}
+
 __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L, int ld, double* __restrict__ rhs,
                                                           int nrhs, double* __restrict__ Linv, DevCtrl* ctrl,
                                                           int* __restrict__ work, const unsigned* __restrict__ tasks,
@@ -401,6 +449,10 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   int* abortw = work + 1;
   int* state = work + 64;  // own cache lines
   int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published (0..4)
+  // rflag[2k] / rflag[2k + 1]: block k's package (Linv + nblk NB^2 + k DF_LR_REC) holds its L rows 48..63 / its last
+  // L16^-T and scales
+  int* rflag = cflag + nblk;
+  double* lrpk = Linv + (size_t)nblk * NB * NB;
   const int tid = threadIdx.x;
   const QFold qf{Hq, dq, nq, Hq ? ctrl->reg : 0.0};
   if (blockIdx.x < 2) {
@@ -413,7 +465,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     Potrf64wSmem& ps = cs.p;
     const int lane = tid & 63, wv = tid >> 6;
     auto mark = [&](int k, int step, int field) {
-      if (trace && tid == 0) trace[4 * (size_t)(ntasks + 3 * k + step) + field] = __builtin_amdgcn_s_memrealtime();
+      if (trace && tid == 0) trace[4 * (size_t)(ntasks + DF_CH_REC * k + step) + field] = __builtin_amdgcn_s_memrealtime();
     };
     auto publish = [&](int idx, int v) {
       df_drain();  // every storing wave: its sc1 stores have left
@@ -445,40 +497,141 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       } else {
         const int k = b - 1;
         mark(k, 1, 0);
-        // A_b,k and D_b with every panel < k applied (state >= k), and the rhs block b with all earlier TRSM
-        // updates: one wait for both states, then every load in flight together (minus L_b,k w_k inside POTRF(b);
-        // POTRF(b-2) of this workgroup is done with ps.B)
-        if (tid == 0)
-          s_ok = df_wait(state, df_tri(b, k), k, abortw, ctrl) && df_wait(state, df_tri(b, b), k, abortw, ctrl);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __syncthreads();
-        if (!s_ok) return;
         const Sc1Mem mA(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
         d4f dacc[NBLK16];
-        {
+        if (b == 1) {
+          // A_1,0 and D_1 (first read here: Q folded from H) and the rhs block 1: every load in flight together
+          if (!wait(state, df_tri(b, k), k)) return;
           f64x2 va[NB * NB / 512];
-          const bool fold = qf.H && k == 0;  // block 1: A_1,0 and D_1 are first read here
+          const bool fold = qf.H != nullptr;
           if (fold) qf_load(va, qf, ld, b * NB, 0);
           else df_load(va, mA, ld);
-          const Sc1Mem mD(const_cast<double*>(fold ? qf.H : L) + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
-#pragma unroll
-          for (int q = 0; q < NBLK16; ++q) {
-            const int ib = kChIB[wv][q], jb = kChJB[wv][q];
-            if (ib >= 0) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int rr = 16 * ib + (lane >> 4) + 4 * r, cc = 16 * jb + (lane & 15);
-                const double h = mD.ld(rr * ld + cc);
-                dacc[q][r] = fold ? qf_entry(qf, b * NB + rr, b * NB + cc, h) : h;
-              }
-            }
-          }
+          ch_load_diag(dacc, fold ? qf.H : L, ld, b, fold, qf, wv, lane);
           const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
           for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
           df_put(cs.Sa, va);
+        } else {
+          // Panel k2 = b - 2 is applied to block row b here, not by the workers: this workgroup factored block k2
+          // (L_k2,k2^-1 in ps.X, w_k2 in ps.W), so TRSM(b, k2), UPDATE(b, b, k2) and UPDATE(b, k, k2) cost no
+          // hand-off of their inputs -- the worker path (TRSM -> UPDATE -> staging) delivered A_b,k and D_b ~14 us
+          // into POTRF(k).  Their worker inputs (tiles (b, k2), (b, b), (b, k) with every panel < k2) are final well
+          // before this workgroup's POTRF(k2) ends, so all of them are loaded at once; only L_k,k2 (the other chain
+          // workgroup's slices, published when its POTRF(k) starts) arrives later.  The same operations in the same
+          // order as the worker tasks (df_trsm, df_update): the factor is bit-identical.
+          const int k2 = b - 2;
+          const bool fold = qf.H && k2 == 0;  // block row 2: A_2,0, D_2 and A_2,1 are first read here
+          if (tid == 0)
+            s_ok = df_wait(state, df_tri(b, k2), k2, abortw, ctrl) && df_wait(state, df_tri(b, b), k2, abortw, ctrl) &&
+                   df_wait(state, df_tri(b, k), k2, abortw, ctrl);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          __syncthreads();
+          if (!s_ok) return;
+          mark(k, 3, 0);
+          const Sc1Mem mA2(L + (size_t)b * NB * ld + (size_t)k2 * NB, tile_bytes(ld));
+          d4f aacc[4];  // A_b,k: this wave's 16 rows x 4 column blocks, MFMA accumulator layout
+          {
+            f64x2 va[NB * NB / 512];
+            if (fold) qf_load(va, qf, ld, b * NB, 0);
+            else df_load(va, mA2, ld);
+            ch_load_diag(dacc, fold ? qf.H : L, ld, b, fold, qf, wv, lane);
+            const Sc1Mem mC(const_cast<double*>(fold ? qf.H : L) + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
+                const double h = mC.ld(row * ld + col);
+                aacc[cb][r] = fold ? qf_entry(qf, b * NB + row, k * NB + col, h) : h;
+              }
+            df_put(cs.Sa, va);  // (waits for the A_b,k2 loads only: the younger D_b / A_b,k loads stay in flight)
+          }
+          __syncthreads();
+          mark(k, 3, 1);
+          // TRSM(b, k2) = A_b,k2 L_k2,k2^-T
+          {
+            double af2[16];  // this wave's row-block of A_b,k2 as MFMA A-fragments
+#pragma unroll
+            for (int q = 0; q < 16; ++q) af2[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
+            d4f acc[4];
+            ch_trsm_seq(acc, af2, ps.X, lane);
+            __syncthreads();  // every wave holds its fragments: Sa takes L_b,k2
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
+                cs.Sa[row * DF_SP + col] = acc[cb][r];
+                mA2.st(row * ld + col, acc[cb][r]);
+              }
+          }
+          // L_b,k2 stored at once (the workers' UPDATE(i, b, k2), i > b: UPDATE(b + 1, b, k2) feeds the next chain
+          // block's panel work), with a non-blocking look at L_k,k2: when it is already published, its loads go out
+          // before the diagonal update and land behind its MFMAs.  publish()'s barrier also completes L_b,k2 in Sa.
+          df_drain();
+          if (tid == 0) s_next = __hip_atomic_load(state + df_tri(k, k2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                                 k2 + 1;
+          __syncthreads();
+          if (tid == 0) __hip_atomic_store(state + df_tri(b, k2), k2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          mark(k, 3, 2);
+          const bool have_l = s_next;
+          // rhs_b -= L_b,k2 w_k2, df_trsm's sums (w_k2 = ps.W, the forward solve of this workgroup's POTRF(k2)); the
+          // rhs block b carries every TRSM(b, j < k2) update (state(b, k2) >= k2).  Its loads go out before L_k,k2's.
+          constexpr int RQ = (NB * MAX_RHS + 255) / 256;
+          double rv[RQ];
+          {
+            const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+#pragma unroll
+            for (int q = 0; q < RQ; ++q)
+              if (tid + 256 * q < NB * nrhs) rv[q] = mR.ld(tid + 256 * q);
+          }
+          const Sc1Mem mL(L + (size_t)k * NB * ld + (size_t)k2 * NB, tile_bytes(ld));
+          f64x2 vl[NB * NB / 512];
+          if (have_l) df_load(vl, mL, ld);
+#pragma unroll
+          for (int q = 0; q < RQ; ++q) {
+            const int t = tid + 256 * q;
+            if (t < NB * nrhs) {
+              const int row = t / nrhs, rho = t % nrhs;
+              double sv = 0.0;
+#pragma unroll 8
+              for (int c = 0; c < NB; ++c) sv = fma(cs.Sa[row * DF_SP + c], ps.W[c * nrhs + rho], sv);
+              ps.B[t] = rv[q] - sv;
+            }
+          }
+          // UPDATE(b, b, k2): D_b -= L_b,k2 L_b,k2' (the K order of df_update's single accumulation chain)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            switch (wv) {
+              case 0: ch_update<0>(dacc, cs.Sa, cb, lane); break;
+              case 1: ch_update<1>(dacc, cs.Sa, cb, lane); break;
+              case 2: ch_update<2>(dacc, cs.Sa, cb, lane); break;
+              default: ch_update<3>(dacc, cs.Sa, cb, lane); break;
+            }
+          }
+          mark(k, 2, 3);
+          if (!have_l) {
+            if (!wait(state, df_tri(k, k2), k2 + 1)) return;
+            df_load(vl, mL, ld);
+          }
+          df_put(ps.S, vl);  // (POTRF(k2)'s tile was stored: ps.S is free until the slices' diagonal tile)
+          __syncthreads();
+          mark(k, 3, 3);
+          // UPDATE(b, k, k2): A_b,k -= L_b,k2 L_k,k2'
+          ch_gemm_nt(aacc, cs.Sa + 16 * wv * DF_SP, ps.S, lane);
+          mark(k, 4, 0);
+          __syncthreads();  // every wave is done with L_b,k2 in Sa, which then takes A_b,k
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
+              cs.Sa[row * DF_SP + col] = aacc[cb][r];
+            }
         }
         potrf64w_reset(ps);  // the slices leave POTRF's L^-1 workspace and flags alone: clear them off the chain
-        mark(k, 1, 1);
+        if (tid == 0) ps.staged = 0;  // the waves count their blocks of D_b in at the end of the slices
+        mark(k, 1, 1);       // (the first slice's wait below is the barrier that completes Sa)
         const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
         // L_b,k, row stride DF_SP: written over A_b,k in Sa (every wave holds its row-block of A in af before the first
         // slice's barrier), where it stays for the rhs correction at the end of POTRF(b) — no copy before POTRF
@@ -501,18 +654,16 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         for (int q = 0; q < 16; ++q) af[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
         bool have_next = false;
 #pragma unroll 1
-        for (int cb = 0; cb < 4; ++cb) {
+        for (int cb = 0; cb < 3; ++cb) {  // (the last slice follows the loop)
           double* E = cs.E2[cb & 1];
-          if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
           if (cb > 0 && !have_next) {
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
           }
-          if (cb == 3) mark(k, 1, 3);  // trace: last row-block of L_kk^-1 in hand
           // non-blocking look at the next row-block: the sc1 poll is issued here and its value consumed only after
           // this slice's MFMAs, so its round trip stays off the chain
           int pollv = 0;
-          if (cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (cb < 2 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q;
@@ -534,7 +685,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               mA.st(row * ld + col, acc[r]);
             }
           }
-          if (tid == 0) s_next = (cb < 3) && pollv >= cb + 2;  // own word: read between this barrier and the next
+          if (tid == 0) s_next = (cb < 2) && pollv >= cb + 2;  // own word: read between this barrier and the next
           __syncthreads();
           have_next = s_next;
           if (have_next) eload(cb + 1);  // lands behind the diagonal update below
@@ -545,13 +696,71 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             default: ch_update<3>(dacc, Lp, cb, lane); break;
           }
         }
+        mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
+        {
+          // Last slice: L'[:, 48..63] = (A[:, 48..63] - L'[:, 0..47] L_kk[48..63, 0..47]') L16_3^-T, the forward
+          // substitution of the last column block (L' L_kk' = A) -- its inputs are POTRF(k)'s L rows 48..63 (final
+          // after the T product of its step 2) and the last sweep's L16^-T with its scales (published by wave 0 the
+          // moment the sweep ends), not row-block 3 of L_kk^-1, which the other waves finish ~2 us later.
+          const double* pk = lrpk + (size_t)k * DF_LR_REC;
+          const Sc1Mem mP(const_cast<double*>(pk), (unsigned)DF_LR_REC * 8u);
+          double* Srow = cs.E2[1];  // [16][DF_SP]: L_kk rows 48..63, columns 0..47
+          double* Eb = cs.E2[0];    // [16][P64_EP] L16^-T, then 16 scales
+          if (!wait(rflag, 2 * k, 1)) return;
+          for (int e = tid; e < 16 * 24; e += 256) {
+            const int r = e / 24, c = 2 * (e % 24);
+            *reinterpret_cast<f64x2*>(Srow + r * DF_SP + c) = mP.ld2(r * 48 + c);
+          }
+          // G = A[16 wv.., 48..63] (still in Sa: the slices overwrote columns 0..47 only)
+          d4f g;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g[r] = Lp[(16 * wv + (lane >> 4) + 4 * r) * DF_SP + 48 + (lane & 15)];
+          __syncthreads();
+#pragma unroll
+          for (int s = 0; s < 12; ++s) {  // K = 0..47 in order
+            const int kk = 4 * s + (lane >> 4);
+            g = __builtin_amdgcn_mfma_f64_16x16x4f64(-Lp[(16 * wv + (lane & 15)) * DF_SP + kk],
+                                                     Srow[(lane & 15) * DF_SP + kk], g, 0, 0, 0);
+          }
+          // G into this wave's rows of Sa (columns 48..63), read back below as the A operand of G L16^-T
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Lp[(16 * wv + (lane >> 4) + 4 * r) * DF_SP + 48 + (lane & 15)] = g[r];
+          if (!wait(rflag, 2 * k + 1, 1)) return;
+          for (int e = tid; e < 16 * 16 + 16; e += 256)
+            Eb[e < 256 ? (e >> 4) * P64_EP + (e & 15) : 16 * P64_EP + (e - 256)] = mP.ld(16 * 48 + e);
+          __syncthreads();
+          d4f acc = {0.0, 0.0, 0.0, 0.0};
+          acc = mfma16_ab(acc, Lp + 16 * wv * DF_SP + 48, DF_SP, Eb, P64_EP, 1.0, lane);
+          acc *= Eb[16 * P64_EP + (lane & 15)];  // the column scales (p64w_T's form)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * wv + (lane >> 4) + 4 * r, col = 48 + (lane & 15);
+            Lp[row * DF_SP + col] = acc[r];
+            mA.st(row * ld + col, acc[r]);
+          }
+          __syncthreads();
+          mark(k, 1, 3);  // trace: last slice's L' in Sa
+          switch (wv) {  // D -= L'[:, 3] L'[:, 3]^T on this wave's lower blocks
+            case 0: ch_update<0>(dacc, Lp, 3, lane); break;
+            case 1: ch_update<1>(dacc, Lp, 3, lane); break;
+            case 2: ch_update<2>(dacc, Lp, 3, lane); break;
+            default: ch_update<3>(dacc, Lp, 3, lane); break;
+          }
+        }
 #pragma unroll
         for (int q = 0; q < NBLK16; ++q) {
           const int ib = kChIB[wv][q], jb = kChJB[wv][q];
           if (ib >= 0) c16_store(ps.S + 16 * ib * P64_SP + 16 * jb, P64_SP, dacc[q], lane);
         }
-        publish(df_tri(b, k), k + 1);  // L_b,k stored
-        mark(k, 1, 2);
+        // hand-off without a workgroup barrier: each wave drains its sc1 stores of L_b,k and counts itself in; the
+        // last one publishes L_b,k (the next chain block's panel work waits on it).  Wave 0 owns D_00 and starts
+        // POTRF(b) at once; the other waves (and wave 0 before its first T / U) wait for all four (potrf64w_factor)
+        df_drain();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0 && __hip_atomic_fetch_add(&ps.staged, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 3) {
+          __hip_atomic_store(state + df_tri(b, k), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (trace) trace[4 * (size_t)(ntasks + DF_CH_REC * k + 1) + 2] = __builtin_amdgcn_s_memrealtime();
+        }
       }
       // POTRF(b): tile and rhs block staged in LDS; L_bb^-1 row-blocks published progressively; before the
       // forward solve, the rhs block gets its last correction  - L_b,b-1 w_b-1  (w_b-1: POTRF(b-1) done)
@@ -586,7 +795,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         potrf64w_reset(ps);
         __syncthreads();
       }  // b > 0: reset behind the staging, the tile's LDS stores behind publish()'s barrier
-      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix)) {
+      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, lrpk + (size_t)b * DF_LR_REC,
+                                   rflag + 2 * b)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
@@ -656,8 +866,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
 }
 
 // work: [0] counter, [1] abort word, [64 ..) one state word per lower tile, then one chain flag per diagonal
-// block; zeroed before every launch.
-size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + nblk; }
+// block, then two package flags per diagonal block (rflag); zeroed before every launch.
+size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + 3 * (size_t)nblk; }
 
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,

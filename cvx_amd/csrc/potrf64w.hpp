@@ -37,6 +37,7 @@ struct Potrf64wSmem {
   int fail;
   int fP, fT;                 // wave 0: steps whose P / T are published
   int cntT[4], cntU[4];       // waves 1..3 done with phase A / B of step kb
+  int staged;                 // waves whose blocks of the tile are in S (4: all; the chain counts them in)
 };
 
 __device__ __forceinline__ int p64w_load(const int* f) {
@@ -223,14 +224,17 @@ __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int
 }
 
 // The factorization of block k: tile staged in sm.S, rhs block in sm.B, flags reset (potrf64w_reset), a barrier
-// behind.  On return (uniformly true / false) sm.X = L^-1 (exact zeros above the diagonal), sm.W = w = L^-1 b (also
+// behind -- or, for the tile's blocks, sm.staged counted up to 4 by the waves that wrote them (wave 0 starts its first
+// sweep on its own block D_00 without waiting for the others).  On return (uniformly true / false) sm.X = L^-1 (exact zeros above the diagonal), sm.W = w = L^-1 b (also
 // stored to rhs block k); Linv[k] = L^-1 is stored row-block by row-block as it becomes final (wave 3), and *lflag
 // (when given) counts the stored row-blocks (sc1 hand-off: the stores drained first).  fix() runs on all threads
-// between the factorization and the forward solve (barrier behind it).  L_kk is not stored (potrf64w_store_L).
+// between the factorization and the forward solve (barrier behind it).  L_kk is not stored (potrf64w_store_L).  With
+// rfl, the package at lrk (DF_LR_REC: L rows 48..63 left of the last diagonal block, that block's L16^-T and scales)
+// is stored as its pieces become final and rfl[0] / rfl[1] raised (k_dataflow.hip: the chain's last slice).
 template <class M, class Fix = NoFix>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
-                                                Fix fix = Fix()) {
+                                                Fix fix = Fix(), double* lrk = nullptr, int* rfl = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -248,7 +252,23 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_publish(&sm.fP, kb + 1);
+      if (kb == 3 && rfl) {  // the package's last L16^-T and its scales, the moment the last sweep ends (sc1 hand-off)
+        const M mR(lrk, (unsigned)DF_LR_REC * 8u);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = lane + 64 * q;
+          mR.st(16 * 48 + e, sm.ET[3][(e >> 4) * P64_EP + (e & 15)]);
+        }
+        if (lane < 16) mR.st(16 * 48 + 256 + lane, sm.SV[3][lane]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(rfl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (kb < 3) {
+        // step 0's sweep reads only wave 0's own block D_00; T(1, 0) / U(1, 1, 0) read the other waves' blocks
+        if (kb == 0 && !p64w_wait(sm, &sm.staged, 4)) {
+          ok = false;
+          break;
+        }
         if (kb >= 1 && !p64w_wait(sm, &sm.cntU[kb - 1], 3)) {
           ok = false;
           break;
@@ -266,7 +286,8 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
   } else {
 #pragma unroll 1
     for (int kb = 0; kb < 4 && ok; ++kb) {
-      ok = p64w_wait(sm, &sm.fP, kb + 1) && (kb == 0 || p64w_wait(sm, &sm.cntU[kb - 1], 3));
+      ok = (kb > 0 || p64w_wait(sm, &sm.staged, 4)) && p64w_wait(sm, &sm.fP, kb + 1) &&
+           (kb == 0 || p64w_wait(sm, &sm.cntU[kb - 1], 3));
       if (!ok) break;
       P64_STAMP(1 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -293,6 +314,17 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       if (kb < 3) {
         ok = p64w_wait(sm, &sm.fT, kb + 1) && p64w_wait(sm, &sm.cntT[kb], 3);
         if (!ok) break;
+        if (kb == 2 && rfl && w == 3) {  // L rows 48..63 left of the last block are final (T(3,2) of wave 0): the package
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          const M mR(lrk, (unsigned)DF_LR_REC * 8u);
+#pragma unroll
+          for (int q = 0; q < 6; ++q) {
+            const int e = lane + 64 * q, r = e / 24, c = 2 * (e % 24);
+            mR.st2(r * 48 + c, *reinterpret_cast<const f64x2*>(sm.S + (48 + r) * P64_SP + c));
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_store(rfl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         P64_STAMP(3 + 4 * kb);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         p64w_phaseB(sm, kb, w, lane);
@@ -353,6 +385,7 @@ __device__ __forceinline__ void potrf64w_reset(Potrf64wSmem& sm) {
     sm.fail = 0;
     sm.fP = 0;
     sm.fT = 0;
+    sm.staged = 4;
   }
 }
 

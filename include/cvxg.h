@@ -283,9 +283,10 @@ int cvxg_affine_map(cvxg_ctx* dst, const double* u, double* x);
 
 /* ---- instrumentation ----------------------------------------------------------------------------- */
 
-/* Per-phase device time (ms), the mean per Newton step (or PD iteration) over the steps since timing was enabled (at
- * most the last 63), measured with HIP events on the stream each phase runs on; the steps never wait on them (only
- * this call synchronises): [0] assembly when not prefetched [1] Ruiz+scale [2] Cholesky (+fused forward solve)
+/* Per-phase device time (ms), the mean over the Newton steps (or PD iterations) since timing was enabled (at most the
+ * last 63) that recorded the phase -- so a step whose assembly was prefetched before timing was enabled does not count
+ * as a zero -- measured with HIP events on the stream each phase runs on; the steps never wait on them (only this call
+ * synchronises): [0] assembly when not prefetched [1] Ruiz+scale [2] Cholesky (+fused forward solve)
  * [3] backward solve + residual [4] line search [5] the assembly SYRK alone (on its own stream when it was launched
  * behind the previous evaluation).  enabled = 1 records every phase; enabled = 2 records only the assembly and Cholesky
  * phases ([0], [2], [5]) -- every event record leaves the GPU idle a few microseconds between kernels. */

@@ -5,7 +5,7 @@
 #   scripts/gpurun_wait.sh <timeout-seconds> '<command>'  > log
 T=$1
 shift
-for attempt in 1 2 3 4 5 6 7 8; do
+for attempt in $(seq 1 ${GPURUN_ATTEMPTS:-30}); do
   out=$(/usr/local/graft/bin/gpurun --timeout "$T" -- "$@" 2>&1)
   rc=$?
   echo "$out"
