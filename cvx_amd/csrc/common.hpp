@@ -10,10 +10,6 @@ constexpr int TILE = 128;     // MFMA SYRK output tile
 constexpr int KC = 16;        // SYRK contraction chunk staged per LDS buffer
 constexpr int MPAD = 64;      // inequality rows padded to a multiple of this
 constexpr int LS_TRIALS = 64; // backtracking trials evaluated per line-search batch
-// Dataflow Cholesky, per diagonal block k: the pieces the next chain block's last slice needs (k_dataflow.hip), stored
-// behind the nblk L^-1 blocks of the Linv buffer: rows 48..63 of L_kk left of its last 16 x 16 block (16 x 48), then
-// L16^-T of that block without its column scales (16 x 16) and the scales (16)
-constexpr int DF_LR_REC = 16 * 48 + 16 * 16 + 16;
 constexpr int MAX_RHS = 9;    // 1 + CVXG_MAX_EQ right-hand sides in the fused forward solve
 constexpr int RUIZ_MAX = 20;  // MatrixUtils.scala:247
 constexpr int COLDOT_ROWS = 128;  // row chunk of the A'v column reduction (partials summed in fixed order)

@@ -1051,7 +1051,7 @@ static int kkt_alloc(cvxg_ctx* ctx, bool fused) {
       ctx->s_nblk = ps / NB;
       CHK(dalloc(ctx, &ctx->sL, (size_t)ps * ps));
       HIPC(ctx, hipMemsetAsync(ctx->sL, 0, (size_t)ps * ps * sizeof(double), ctx->s));
-      CHK(dalloc(ctx, &ctx->sLinv, (size_t)ctx->s_nblk * (NB * NB + DF_LR_REC)));
+      CHK(dalloc(ctx, &ctx->sLinv, (size_t)ctx->s_nblk * NB * NB));
       CHK(dalloc(ctx, &ctx->kzp, (size_t)ps));
       CHK(dalloc(ctx, &ctx->sw, (size_t)ps));
       std::vector<unsigned> order = chol_schedule(ctx->s_nblk, ctx->ncu);
@@ -1587,7 +1587,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   for (double** v : {&ctx->c, &ctx->d, &ctx->invd, &ctx->w, &ctx->logd, &ctx->e}) CHK(dalloc(ctx, v, std::max(mp, np)));
   CHK(dalloc(ctx, &ctx->H, np * np));
   CHK(dalloc(ctx, &ctx->L, np * np));
-  CHK(dalloc(ctx, &ctx->Linv, (size_t)ctx->nblk * (NB * NB + DF_LR_REC)));  // + the chain packages (k_dataflow.hip)
+  CHK(dalloc(ctx, &ctx->Linv, (size_t)ctx->nblk * NB * NB));
   {  // dataflow Cholesky: task order for this tile count, work words
     (void)hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device);
     ctx->ncu = std::max(ctx->ncu, 1);

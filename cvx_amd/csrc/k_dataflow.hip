@@ -57,7 +57,7 @@ __device__ __forceinline__ double qf_entry(const QFold& f, int r, int c, double 
 }
 // a 64 x 64 tile's loads (df_load layout) of Q(r0.., c0..) from H
 __device__ __forceinline__ void qf_load(f64x2 (&v)[NB * NB / 512], const QFold& f, int ld, int r0, int c0) {
-  const int tid = threadIdx.x;
+  const int tid = opq_tid();
   const Sc1Mem mH(const_cast<double*>(f.H) + (size_t)r0 * ld + c0, tile_bytes(ld));
 #pragma unroll
   for (int q = 0; q < NB * NB / 512; ++q) {
@@ -98,7 +98,7 @@ __device__ bool df_wait(const int* state, int idx, int want, int* abortw, DevCtr
 
 // Stage a 64 x 64 tile (descriptor m, leading dimension ld) into LDS [64][DF_SP]: 8 x 16-B sc1 loads per thread.
 __device__ __forceinline__ void df_stage(double* __restrict__ dst, const Sc1Mem& m, int ld) {
-  const int tid = threadIdx.x;
+  const int tid = opq_tid();
   f64x2 v[NB * NB / 512];
 #pragma unroll
   for (int q = 0; q < NB * NB / 512; ++q) {
@@ -116,7 +116,7 @@ __device__ __forceinline__ void df_stage(double* __restrict__ dst, const Sc1Mem&
 
 // The two halves of df_stage, for software pipelining: loads into registers, then LDS stores.
 __device__ __forceinline__ void df_load(f64x2 (&v)[NB * NB / 512], const Sc1Mem& m, int ld) {
-  const int tid = threadIdx.x;
+  const int tid = opq_tid();
 #pragma unroll
   for (int q = 0; q < NB * NB / 512; ++q) {
     const int idx = q * 256 + tid;
@@ -124,7 +124,7 @@ __device__ __forceinline__ void df_load(f64x2 (&v)[NB * NB / 512], const Sc1Mem&
   }
 }
 __device__ __forceinline__ void df_put(double* __restrict__ dst, const f64x2 (&v)[NB * NB / 512]) {
-  const int tid = threadIdx.x;
+  const int tid = opq_tid();
 #pragma unroll
   for (int q = 0; q < NB * NB / 512; ++q) {
     const int idx = q * 256 + tid;
@@ -190,7 +190,7 @@ __device__ __forceinline__ void df_load_c(d4f (&acc)[2][2], const Sc1Mem& mC, in
 }
 
 __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, double* smem, const QFold& qf) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = opq_tid(), lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const bool active = !(i == j && wc > wr);
   const Sc1Mem mC(L + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
@@ -223,7 +223,7 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
 // UPDATE4(i,j,k0): A_ij -= sum_{k=k0}^{k0+3} L_ik L_jk^T — one read-modify-write of the tile for four panels,
 // with the operand tiles of panel k+1 loaded into registers while the MFMAs of panel k run (two LDS buffers).
 __device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0, double* smem, const QFold& qf) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = opq_tid(), lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const bool active = !(i == j && wc > wr);
   const bool diag = (i == j);
@@ -271,7 +271,7 @@ __device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0,
 __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __restrict__ rhs, int nrhs,
                         double* __restrict__ Linv, double* smem, const int* state, int* abortw, DevCtrl* ctrl,
                         int* s_ok, const QFold& qf) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = opq_tid(), lane = tid & 63, wid = tid >> 6;
   double* Pi = smem;
   double* Pj = smem + NB * DF_SP;
   const Sc1Mem mA(L + (size_t)i * NB * ld + (size_t)k * NB, tile_bytes(ld));
@@ -348,10 +348,7 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
 // TRSM slice CB: L'[16 w.., 16 CB..] = A[16 w.., :] L^-1[16 CB.., :]^T (K = 16 (CB + 1): L^-1 is lower); af = the
 // wave's row-block of A as MFMA A-fragments (loaded once per block), E = row-block CB of L^-1 (row stride DF_SP).
 template <int CB>
-__device__ __forceinline__ d4f ch_trsm(const double (&af)[16], const double* E, int lane) {
-  double xf[4 * (CB + 1)];
-#pragma unroll
-  for (int s = 0; s < 4 * (CB + 1); ++s) xf[s] = E[(lane & 15) * DF_SP + 4 * s + (lane >> 4)];
+__device__ __forceinline__ d4f ch_trsm_x(const double (&af)[16], const double* xf) {  // xf: the B-fragments
   d4f acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int s = 0; s < 4 * (CB + 1); s += 2) {
@@ -359,6 +356,13 @@ __device__ __forceinline__ d4f ch_trsm(const double (&af)[16], const double* E, 
     acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s + 1], xf[s + 1], acc1, 0, 0, 0);
   }
   return acc0 + acc1;
+}
+template <int CB>
+__device__ __forceinline__ d4f ch_trsm(const double (&af)[16], const double* E, int lane) {
+  double xf[4 * (CB + 1)];
+#pragma unroll
+  for (int s = 0; s < 4 * (CB + 1); ++s) xf[s] = E[(lane & 15) * DF_SP + 4 * s + (lane >> 4)];
+  return ch_trsm_x<CB>(af, xf);
 }
 // the 10 lower 16 x 16 blocks of a 64 x 64 tile, 3 / 3 / 2 / 2 per wave (-1: none)
 constexpr int kChIB[4][3] = {{0, 3, 3}, {1, 3, 2}, {1, 3, -1}, {2, 2, -1}};
@@ -449,10 +453,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   int* abortw = work + 1;
   int* state = work + 64;  // own cache lines
   int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published (0..4)
-  // rflag[2k] / rflag[2k + 1]: block k's package (Linv + nblk NB^2 + k DF_LR_REC) holds its L rows 48..63 / its last
-  // L16^-T and scales
-  int* rflag = cflag + nblk;
-  double* lrpk = Linv + (size_t)nblk * NB * NB;
   const int tid = threadIdx.x;
   const QFold qf{Hq, dq, nq, Hq ? ctrl->reg : 0.0};
   if (blockIdx.x < 2) {
@@ -528,22 +528,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           if (!s_ok) return;
           mark(k, 3, 0);
           const Sc1Mem mA2(L + (size_t)b * NB * ld + (size_t)k2 * NB, tile_bytes(ld));
-          d4f aacc[4];  // A_b,k: this wave's 16 rows x 4 column blocks, MFMA accumulator layout
           {
             f64x2 va[NB * NB / 512];
             if (fold) qf_load(va, qf, ld, b * NB, 0);
             else df_load(va, mA2, ld);
             ch_load_diag(dacc, fold ? qf.H : L, ld, b, fold, qf, wv, lane);
-            const Sc1Mem mC(const_cast<double*>(fold ? qf.H : L) + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
-                const double h = mC.ld(row * ld + col);
-                aacc[cb][r] = fold ? qf_entry(qf, b * NB + row, k * NB + col, h) : h;
-              }
-            df_put(cs.Sa, va);  // (waits for the A_b,k2 loads only: the younger D_b / A_b,k loads stay in flight)
+            df_put(cs.Sa, va);  // (waits for the A_b,k2 loads only: the younger D_b loads stay in flight)
           }
           __syncthreads();
           mark(k, 3, 1);
@@ -584,6 +574,19 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
 #pragma unroll
             for (int q = 0; q < RQ; ++q)
               if (tid + 256 * q < NB * nrhs) rv[q] = mR.ld(tid + 256 * q);
+          }
+          d4f aacc[4];  // A_b,k: this wave's 16 rows x 4 column blocks, MFMA accumulator layout (loaded here, not with
+                        // the others, to keep the register peak of the prefetch down; it lands behind the updates)
+          {
+            const Sc1Mem mC(const_cast<double*>(fold ? qf.H : L) + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
+                const double h = mC.ld(row * ld + col);
+                aacc[cb][r] = fold ? qf_entry(qf, b * NB + row, k * NB + col, h) : h;
+              }
           }
           const Sc1Mem mL(L + (size_t)k * NB * ld + (size_t)k2 * NB, tile_bytes(ld));
           f64x2 vl[NB * NB / 512];
@@ -647,23 +650,64 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             er[q] = mI.ld2((16 * cb + (e >> 5)) * NB + 2 * (e & 31));
           }
         };
-        if (!wait(cflag, k, 1)) return;
-        eload(0);
-        double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments (Sa staged behind the barriers above)
+        // The row-blocks of L_kk^-1 already published when the staging ends (usually all four: the panel work above
+        // ends after POTRF(k)'s last sweep) run as one batch -- staged together into ps.S (free until the diagonal
+        // tile goes there at the end), their TRSM products back to back, one barrier, their diagonal updates; the rest
+        // one slice each as they arrive.  The same MFMA sequence per output either way, so the factor is the same.
+        if (tid == 0) s_next = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();  // (also completes Sa)
+        const int nbat = min(s_next, 4);
+        double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments
 #pragma unroll
         for (int q = 0; q < 16; ++q) af[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
-        bool have_next = false;
+        if (nbat > 0) {
+          for (int e = tid; e < nbat * 512; e += 256)  // row-blocks 0 .. nbat-1 of L_kk^-1 -> ps.S rows 0 .. 16 nbat-1
+            *reinterpret_cast<f64x2*>(ps.S + (e >> 5) * P64_SP + 2 * (e & 31)) = mI.ld2((e >> 5) * NB + 2 * (e & 31));
+          __syncthreads();
+          d4f acc[4];
+          acc[0] = ch_trsm<0>(af, ps.S, lane);
+          if (nbat > 1) acc[1] = ch_trsm<1>(af, ps.S + 16 * P64_SP, lane);
+          if (nbat > 2) acc[2] = ch_trsm<2>(af, ps.S + 32 * P64_SP, lane);
+          if (nbat > 3) acc[3] = ch_trsm<3>(af, ps.S + 48 * P64_SP, lane);
+          __syncthreads();  // every wave holds its fragments of A (Sa takes L')
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb)
+            if (cb < nbat)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
+                Lp[row * DF_SP + col] = acc[cb][r];
+                mA.st(row * ld + col, acc[cb][r]);
+              }
+          __syncthreads();
+          for (int cb = 0; cb < nbat; ++cb) {
+            switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
+              case 0: ch_update<0>(dacc, Lp, cb, lane); break;
+              case 1: ch_update<1>(dacc, Lp, cb, lane); break;
+              case 2: ch_update<2>(dacc, Lp, cb, lane); break;
+              default: ch_update<3>(dacc, Lp, cb, lane); break;
+            }
+          }
+        }
+        if (nbat < 4) {
+          if (!wait(cflag, k, nbat + 1)) return;
+          eload(nbat);
+        }
+        bool have_next = nbat < 4;
 #pragma unroll 1
-        for (int cb = 0; cb < 3; ++cb) {  // (the last slice follows the loop)
+        for (int cb = nbat; cb < 4; ++cb) {
           double* E = cs.E2[cb & 1];
-          if (cb > 0 && !have_next) {
+          if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
+          if (!have_next) {
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
           }
+          if (cb == 3) mark(k, 1, 3);  // trace: last row-block of L_kk^-1 in hand
           // non-blocking look at the next row-block: the sc1 poll is issued here and its value consumed only after
           // this slice's MFMAs, so its round trip stays off the chain
           int pollv = 0;
-          if (cb < 2 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q;
@@ -685,7 +729,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               mA.st(row * ld + col, acc[r]);
             }
           }
-          if (tid == 0) s_next = (cb < 2) && pollv >= cb + 2;  // own word: read between this barrier and the next
+          if (tid == 0) s_next = (cb < 3) && pollv >= cb + 2;  // own word: read between this barrier and the next
           __syncthreads();
           have_next = s_next;
           if (have_next) eload(cb + 1);  // lands behind the diagonal update below
@@ -696,57 +740,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             default: ch_update<3>(dacc, Lp, cb, lane); break;
           }
         }
-        mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
-        {
-          // Last slice: L'[:, 48..63] = (A[:, 48..63] - L'[:, 0..47] L_kk[48..63, 0..47]') L16_3^-T, the forward
-          // substitution of the last column block (L' L_kk' = A) -- its inputs are POTRF(k)'s L rows 48..63 (final
-          // after the T product of its step 2) and the last sweep's L16^-T with its scales (published by wave 0 the
-          // moment the sweep ends), not row-block 3 of L_kk^-1, which the other waves finish ~2 us later.
-          const double* pk = lrpk + (size_t)k * DF_LR_REC;
-          const Sc1Mem mP(const_cast<double*>(pk), (unsigned)DF_LR_REC * 8u);
-          double* Srow = cs.E2[1];  // [16][DF_SP]: L_kk rows 48..63, columns 0..47
-          double* Eb = cs.E2[0];    // [16][P64_EP] L16^-T, then 16 scales
-          if (!wait(rflag, 2 * k, 1)) return;
-          for (int e = tid; e < 16 * 24; e += 256) {
-            const int r = e / 24, c = 2 * (e % 24);
-            *reinterpret_cast<f64x2*>(Srow + r * DF_SP + c) = mP.ld2(r * 48 + c);
-          }
-          // G = A[16 wv.., 48..63] (still in Sa: the slices overwrote columns 0..47 only)
-          d4f g;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) g[r] = Lp[(16 * wv + (lane >> 4) + 4 * r) * DF_SP + 48 + (lane & 15)];
-          __syncthreads();
-#pragma unroll
-          for (int s = 0; s < 12; ++s) {  // K = 0..47 in order
-            const int kk = 4 * s + (lane >> 4);
-            g = __builtin_amdgcn_mfma_f64_16x16x4f64(-Lp[(16 * wv + (lane & 15)) * DF_SP + kk],
-                                                     Srow[(lane & 15) * DF_SP + kk], g, 0, 0, 0);
-          }
-          // G into this wave's rows of Sa (columns 48..63), read back below as the A operand of G L16^-T
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Lp[(16 * wv + (lane >> 4) + 4 * r) * DF_SP + 48 + (lane & 15)] = g[r];
-          if (!wait(rflag, 2 * k + 1, 1)) return;
-          for (int e = tid; e < 16 * 16 + 16; e += 256)
-            Eb[e < 256 ? (e >> 4) * P64_EP + (e & 15) : 16 * P64_EP + (e - 256)] = mP.ld(16 * 48 + e);
-          __syncthreads();
-          d4f acc = {0.0, 0.0, 0.0, 0.0};
-          acc = mfma16_ab(acc, Lp + 16 * wv * DF_SP + 48, DF_SP, Eb, P64_EP, 1.0, lane);
-          acc *= Eb[16 * P64_EP + (lane & 15)];  // the column scales (p64w_T's form)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = 16 * wv + (lane >> 4) + 4 * r, col = 48 + (lane & 15);
-            Lp[row * DF_SP + col] = acc[r];
-            mA.st(row * ld + col, acc[r]);
-          }
-          __syncthreads();
-          mark(k, 1, 3);  // trace: last slice's L' in Sa
-          switch (wv) {  // D -= L'[:, 3] L'[:, 3]^T on this wave's lower blocks
-            case 0: ch_update<0>(dacc, Lp, 3, lane); break;
-            case 1: ch_update<1>(dacc, Lp, 3, lane); break;
-            case 2: ch_update<2>(dacc, Lp, 3, lane); break;
-            default: ch_update<3>(dacc, Lp, 3, lane); break;
-          }
-        }
+        if (nbat == 4) mark(k, 1, 3);
 #pragma unroll
         for (int q = 0; q < NBLK16; ++q) {
           const int ib = kChIB[wv][q], jb = kChJB[wv][q];
@@ -795,8 +789,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         potrf64w_reset(ps);
         __syncthreads();
       }  // b > 0: reset behind the staging, the tile's LDS stores behind publish()'s barrier
-      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, lrpk + (size_t)b * DF_LR_REC,
-                                   rflag + 2 * b)) {
+      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
@@ -866,8 +859,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
 }
 
 // work: [0] counter, [1] abort word, [64 ..) one state word per lower tile, then one chain flag per diagonal
-// block, then two package flags per diagonal block (rflag); zeroed before every launch.
-size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + 3 * (size_t)nblk; }
+// block; zeroed before every launch.
+size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + nblk; }
 
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
