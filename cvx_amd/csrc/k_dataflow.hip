@@ -455,8 +455,16 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published (0..4)
   const int tid = threadIdx.x;
   const QFold qf{Hq, dq, nq, Hq ? ctrl->reg : 0.0};
-  if (blockIdx.x < 2) {
-    // ---- workgroups 0 and 1: the critical chain, ping-pong.  Workgroup c factors the diagonal blocks b = c,
+  // Roles by residency, not by blockIdx: the first two workgroups to start run the chain.  Workgroups are not
+  // dispatched in blockIdx order across the XCDs, and with other work on the device (several contexts sharing one
+  // GPU) blockIdx 1 may wait for a free CU behind workers that wait on it; with tickets, any three resident
+  // workgroups of a launch make progress.
+  __shared__ int s_role;
+  if (tid == 0) s_role = atomicAdd(work + 2, 1);
+  __syncthreads();
+  const int role = s_role;
+  if (role < 2) {
+    // ---- roles 0 and 1: the critical chain, ping-pong.  The workgroup of role c factors the diagonal blocks b = c,
     // c + 2, ...  Before POTRF(b) it runs TRSM(b, b-1) and UPDATE(b, b, b-1) in four 16-column slices, each
     // started as soon as the other workgroup's POTRF(b-1) has published that row-block of L_b-1^-1
     // (chain flags), so the next factorization starts ~one slice after the previous one ends.  The updated
@@ -479,7 +487,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       return s_ok;
     };
     constexpr int NBLK16 = 3;  // (kChIB / kChJB: this wave's lower 16 x 16 blocks)
-    for (int b = blockIdx.x; b < nblk; b += 2) {
+    for (int b = role; b < nblk; b += 2) {
       if (b == 0) {
         if (qf.H) {
           f64x2 v[NB * NB / 512];
@@ -499,6 +507,29 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         mark(k, 1, 0);
         const Sc1Mem mA(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
         d4f dacc[NBLK16];
+        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
+        // The row-blocks of L_kk^-1 already published when the staging ends (usually three or four: the panel work
+        // ends late in POTRF(k)) run as one batch -- loaded together into ps.S (free until the diagonal tile goes there
+        // at the end), their TRSM products back to back, one barrier, their diagonal updates; the rest one slice each
+        // as they arrive.  The same MFMA sequence per output either way, so the factor is the same.  The flag is read
+        // before the staging's last MFMAs and the row-block loads all go out before the staging's LDS stores, so
+        // neither round trip is paid on the chain.
+        int nbat = 0;
+        f64x2 vb[8];
+        auto bload = [&]() {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int e = opq_tid() + 256 * q;
+            if (q < 2 * nbat) vb[q] = mI.ld2((e >> 5) * NB + 2 * (e & 31));
+          }
+        };
+        auto bput = [&]() {  // row-blocks 0 .. nbat-1 of L_kk^-1 -> ps.S rows 0 .. 16 nbat-1
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int e = opq_tid() + 256 * q;
+            if (q < 2 * nbat) *reinterpret_cast<f64x2*>(ps.S + (e >> 5) * P64_SP + 2 * (e & 31)) = vb[q];
+          }
+        };
         if (b == 1) {
           // A_1,0 and D_1 (first read here: Q folded from H) and the rhs block 1: every load in flight together
           if (!wait(state, df_tri(b, k), k)) return;
@@ -510,6 +541,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
           for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
           df_put(cs.Sa, va);
+          if (tid == 0) s_next = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          __syncthreads();
+          nbat = min(s_next, 4);
+          bload();
+          bput();
         } else {
           // Panel k2 = b - 2 is applied to block row b here, not by the workers: this workgroup factored block k2
           // (L_k2,k2^-1 in ps.X, w_k2 in ps.W), so TRSM(b, k2), UPDATE(b, b, k2) and UPDATE(b, k, k2) cost no
@@ -520,9 +557,13 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           // order as the worker tasks (df_trsm, df_update): the factor is bit-identical.
           const int k2 = b - 2;
           const bool fold = qf.H && k2 == 0;  // block row 2: A_2,0, D_2 and A_2,1 are first read here
-          if (tid == 0)
-            s_ok = df_wait(state, df_tri(b, k2), k2, abortw, ctrl) && df_wait(state, df_tri(b, b), k2, abortw, ctrl) &&
-                   df_wait(state, df_tri(b, k), k2, abortw, ctrl);
+          if (tid == 0) {  // (the three polls in flight together: usually all three inputs are final already)
+            const int v0 = df_poll(state + df_tri(b, k2)), v1 = df_poll(state + df_tri(b, b)),
+                      v2 = df_poll(state + df_tri(b, k));
+            s_ok = (v0 >= k2 || df_wait(state, df_tri(b, k2), k2, abortw, ctrl)) &&
+                   (v1 >= k2 || df_wait(state, df_tri(b, b), k2, abortw, ctrl)) &&
+                   (v2 >= k2 || df_wait(state, df_tri(b, k), k2, abortw, ctrl));
+          }
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           __syncthreads();
           if (!s_ok) return;
@@ -620,10 +661,16 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           df_put(ps.S, vl);  // (POTRF(k2)'s tile was stored: ps.S is free until the slices' diagonal tile)
           __syncthreads();
           mark(k, 3, 3);
-          // UPDATE(b, k, k2): A_b,k -= L_b,k2 L_k,k2'
+          // UPDATE(b, k, k2): A_b,k -= L_b,k2 L_k,k2'  (the L_kk^-1 flag read goes out ahead of it)
+          int pv = 0;
+          if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           ch_gemm_nt(aacc, cs.Sa + 16 * wv * DF_SP, ps.S, lane);
           mark(k, 4, 0);
-          __syncthreads();  // every wave is done with L_b,k2 in Sa, which then takes A_b,k
+          if (tid == 0) s_next = pv;  // (have_l was read before the barrier above)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          __syncthreads();  // every wave is done with L_b,k2 in Sa (which then takes A_b,k) and with ps.S
+          nbat = min(s_next, 4);
+          bload();
 #pragma unroll
           for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -631,11 +678,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
               cs.Sa[row * DF_SP + col] = aacc[cb][r];
             }
+          bput();
         }
         potrf64w_reset(ps);  // the slices leave POTRF's L^-1 workspace and flags alone: clear them off the chain
         if (tid == 0) ps.staged = 0;  // the waves count their blocks of D_b in at the end of the slices
         mark(k, 1, 1);       // (the first slice's wait below is the barrier that completes Sa)
-        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
         // L_b,k, row stride DF_SP: written over A_b,k in Sa (every wave holds its row-block of A in af before the first
         // slice's barrier), where it stays for the rhs correction at the end of POTRF(b) — no copy before POTRF
         double* Lp = cs.Sa;
@@ -646,25 +693,15 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         auto eload = [&](int cb) {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
-            const int e = tid + 256 * q;
+            const int e = opq_tid() + 256 * q;  // (opaque: the addresses are not kept live across the chain loop)
             er[q] = mI.ld2((16 * cb + (e >> 5)) * NB + 2 * (e & 31));
           }
         };
-        // The row-blocks of L_kk^-1 already published when the staging ends (usually all four: the panel work above
-        // ends after POTRF(k)'s last sweep) run as one batch -- staged together into ps.S (free until the diagonal
-        // tile goes there at the end), their TRSM products back to back, one barrier, their diagonal updates; the rest
-        // one slice each as they arrive.  The same MFMA sequence per output either way, so the factor is the same.
-        if (tid == 0) s_next = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __syncthreads();  // (also completes Sa)
-        const int nbat = min(s_next, 4);
+        __syncthreads();  // completes Sa and the batch's row-blocks in ps.S
         double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments
 #pragma unroll
         for (int q = 0; q < 16; ++q) af[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
         if (nbat > 0) {
-          for (int e = tid; e < nbat * 512; e += 256)  // row-blocks 0 .. nbat-1 of L_kk^-1 -> ps.S rows 0 .. 16 nbat-1
-            *reinterpret_cast<f64x2*>(ps.S + (e >> 5) * P64_SP + 2 * (e & 31)) = mI.ld2((e >> 5) * NB + 2 * (e & 31));
-          __syncthreads();
           d4f acc[4];
           acc[0] = ch_trsm<0>(af, ps.S, lane);
           if (nbat > 1) acc[1] = ch_trsm<1>(af, ps.S + 16 * P64_SP, lane);
@@ -690,6 +727,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             }
           }
         }
+        if (tid == 0 && trace) trace[4 * (size_t)(ntasks + DF_CH_REC * k + 4) + 3] = nbat;
+        mark(k, 4, 2);  // trace: batch done
         if (nbat < 4) {
           if (!wait(cflag, k, nbat + 1)) return;
           eload(nbat);
@@ -700,6 +739,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           double* E = cs.E2[cb & 1];
           if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
           if (!have_next) {
+            if (cb == 3) mark(k, 4, 1);  // trace: waiting for the last row-block
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
           }
@@ -746,9 +786,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           const int ib = kChIB[wv][q], jb = kChJB[wv][q];
           if (ib >= 0) c16_store(ps.S + 16 * ib * P64_SP + 16 * jb, P64_SP, dacc[q], lane);
         }
+        mark(b, 0, 3);  // trace: D_b in LDS (before the drain)
         // hand-off without a workgroup barrier: each wave drains its sc1 stores of L_b,k and counts itself in; the
-        // last one publishes L_b,k (the next chain block's panel work waits on it).  Wave 0 owns D_00 and starts
-        // POTRF(b) at once; the other waves (and wave 0 before its first T / U) wait for all four (potrf64w_factor)
+        // last one publishes L_b,k (the next chain block's panel work waits on it: publishing it only after POTRF(b)'s
+        // first sweep, to spare wave 0 the drain, measured slower).  Wave 0 owns D_00 and starts POTRF(b) at once;
+        // the other waves (and wave 0 before its first T / U) wait for all four (potrf64w_factor)
         df_drain();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0 && __hip_atomic_fetch_add(&ps.staged, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 3) {
@@ -789,7 +831,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         potrf64w_reset(ps);
         __syncthreads();
       }  // b > 0: reset behind the staging, the tile's LDS stores behind publish()'s barrier
-      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix)) {
+      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix,
+                                   trace ? trace + 4 * (size_t)(ntasks + DF_CH_REC * b + 5) : nullptr)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
@@ -800,7 +843,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     }
     return;
   }
-  // ---- workgroups 2..: claim the remaining tasks in the host-built order ---------------------------
+  // ---- roles 2..: claim the remaining tasks in the host-built order ---------------------------
   int my_idx = -1;  // thread 0: claimed task index (trace)
   for (;;) {
     if (tid == 0) {

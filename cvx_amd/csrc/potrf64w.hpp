@@ -237,7 +237,7 @@ __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int
 template <class M, class Fix = NoFix>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
-                                                Fix fix = Fix()) {
+                                                Fix fix = Fix(), unsigned long long* lstamp = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -284,14 +284,14 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       if (!ok) break;
       P64_STAMP(1 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      p64w_phaseA(sm, kb, w, lane, T3);
+      p64w_phaseA(sm, kb, w, opq_tid() & 63, T3);
       P64_STAMP(2 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_add(&sm.cntT[kb]);
       if (lflag) {
         // row-block kb of L^-1: each wave stores the blocks X_kb,j its phase A just formed (the upper blocks of Linv
-        // stay the zeros they were allocated with), drains, and counts itself in; the last of the three raises the
-        // flag (an agent-scope max: the flags of consecutive steps may be raised by different waves)
+        // stay the zeros they were allocated with), later drains and counts itself in (count_in); the last of the
+        // three raises the flag (an agent-scope max: the flags of consecutive steps may be raised by different waves)
         const int j0 = (kb == 0) ? ((w == 3) ? 0 : -1) : (kb == 1) ? ((w == 1) ? -1 : w - 2) : w - 1;
         const int nj = (kb == 3 && w == 3) ? 2 : (j0 >= 0 ? 1 : 0);
         const int r = lane >> 2, c = 4 * (lane & 3);
@@ -300,24 +300,32 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
           mI.st2(rr * NB + cc, *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc));
           mI.st2(rr * NB + cc + 2, *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc + 2));
         }
-        if (lflag != PUBLISH_ONLY) {
+      }
+      // the drain and count of row-block kb: at once for the last one, behind phase B otherwise (the stores complete
+      // during its MFMAs instead of holding up the next sweep's inputs)
+      auto count_in = [&]() {
+        if (lflag && lflag != PUBLISH_ONLY) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (lane == 0 &&
-              __hip_atomic_fetch_add(&sm.cntL[kb], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 2)
+              __hip_atomic_fetch_add(&sm.cntL[kb], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 2) {
             __hip_atomic_fetch_max(lflag, kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lstamp) lstamp[kb] = __builtin_amdgcn_s_memrealtime();  // (trace: row-block kb's flag raised)
+          }
         }
-      }
+      };
+      if (kb == 3) count_in();
       if (kb < 3) {
         ok = p64w_wait(sm, &sm.fT, kb + 1) && p64w_wait(sm, &sm.cntT[kb], 3);
         if (!ok) break;
         P64_STAMP(3 + 4 * kb);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        p64w_phaseB(sm, kb, w, lane);
-        if (kb == 2) T3 = p64w_Xpre(sm, 3, w - 1, lane);  // L_3,m (m < 3) and X_m,j (m <= 2) are final here
+        p64w_phaseB(sm, kb, w, opq_tid() & 63);
+        if (kb == 2) T3 = p64w_Xpre(sm, 3, w - 1, opq_tid() & 63);  // L_3,m (m < 3) and X_m,j (m <= 2) are final here
         P64_STAMP(4 + 4 * kb);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_add(&sm.cntU[kb]);
+      if (kb < 3) count_in();
     }
   }
   P64_STAMP(17);

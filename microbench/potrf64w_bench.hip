@@ -1,15 +1,20 @@
 // Microbenchmark of the wave-specialised 64x64 diagonal-block Cholesky (potrf64w.hpp) in isolation: correctness against a
 // host Cholesky / inverse / forward solve, kernel time via hipEvents over many launches on fresh copies,
 // and per-wave phase stamps (built with -DPOTRF_STAMPS).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPOTRF_STAMPS microbench/potrf_bench.hip -o microbench/potrf_bench
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPOTRF_STAMPS microbench/potrf64w_bench.hip -o microbench/potrf64w_bench
+// -DWITH_LFLAG: progressive L^-1 stores + flag (the chain's form); -DPOTRF_HDR='"ab_old/potrf64w.hpp"': another version
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 
 #include <vector>
 
-#include "../cvx_amd/csrc/potrf64w.hpp"
+#ifndef POTRF_HDR
+#define POTRF_HDR "../cvx_amd/csrc/potrf64w.hpp"
+#endif
+#include POTRF_HDR
 namespace cvxg {
+__device__ int g_lflag;  // -DWITH_LFLAG: the progressive L^-1 row-block stores and flag of the chain's POTRF
 __device__ double* g_src;  // pristine copy of the tile (warm-I$ repetition)
 __device__ int g_reps = 1;
 __global__ __launch_bounds__(256) void k_p64(double* L, int ld, int k, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl) {
@@ -27,7 +32,11 @@ __global__ __launch_bounds__(256) void k_p64(double* L, int ld, int k, double* r
     potrf64w_stage<PlainMem>(L, ld, (size_t)k * NB * ld + (size_t)k * NB, rhs, k, nrhs, sm);
     potrf64w_reset(sm);
     __syncthreads();
+#ifdef WITH_LFLAG
+    if (potrf64w_factor<Sc1Mem>(k, rhs, nrhs, Linv, ctrl, sm, &g_lflag)) potrf64w_store_L<Sc1Mem>(L, ld, k, sm);
+#else
     if (potrf64w_factor<PlainMem>(k, rhs, nrhs, Linv, ctrl, sm)) potrf64w_store_L<PlainMem>(L, ld, k, sm);
+#endif
     __syncthreads();
   }
 }

@@ -50,3 +50,15 @@ if ch.shape[1] >= 5 and ch[2:nb-2, 3, 0].min() > 0:
     vals = np.array(vals)
     for i, l in enumerate(lab):
         print(f"panel {l:22s} med {np.median(vals[:, i]):7.2f} mean {vals[:, i].mean():7.2f}")
+# L^-1 row-block hand-offs: flags raised by POTRF(k)'s waves (record 5), the consumer's batch / wait for the last one
+if ch[2:nb-2, 5, 3].min() > 0:
+    v = np.array([[(ch[k, 5, f] - ch[k, 0, 0]) / 100.0 for f in range(4)] for k in range(2, nb - 2)])
+    for f in range(4):
+        print(f"rb{f} flag raised        med {np.median(v[:, f]):7.2f} mean {v[:, f].mean():7.2f}")
+    nbat = ch[2:nb-2, 4, 3]
+    print("batch sizes", {int(x): int((nbat == x).sum()) for x in np.unique(nbat)})
+    bd = np.array([(ch[k, 4, 2] - ch[k, 0, 0]) / 100.0 for k in range(2, nb - 2)])
+    print(f"batch done             med {np.median(bd):7.2f} mean {bd.mean():7.2f}")
+    w = [(ch[k, 4, 1] - ch[k, 0, 0]) / 100.0 for k in range(2, nb - 2) if ch[k, 4, 1] > ch[k, 0, 0]]
+    if w:
+        print(f"wait for rb3 begins    med {np.median(w):7.2f} mean {np.mean(w):7.2f} (n={len(w)})")
