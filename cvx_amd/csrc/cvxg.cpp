@@ -434,19 +434,15 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   auto code = [](const Task& x) {
     return ((unsigned)x.type << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j;
   };
-  // chain tasks (k_dataflow.hip: the chain workgroup of block b runs TRSM(b,b-2), UPDATE(b,b,b-2), UPDATE(b,b-1,b-2),
-  // then TRSM(b,b-1) and UPDATE(b,b,b-1), then POTRF(b))
   auto is_chain = [](const Task& x) {
-    return x.type == 0 || (x.type == 1 && (x.i == x.k + 1 || x.i == x.k + 2)) ||
-           (x.type == 2 && x.i == x.k + 1 && x.j == x.i) ||
-           (x.type == 2 && x.i == x.k + 2 && (x.j == x.i || x.j == x.i - 1));
+    return x.type == 0 || (x.type == 1 && x.i == x.k + 1) || (x.type == 2 && x.i == x.j && x.j == x.k + 1);
   };
-  // the worker tasks the chain's panel work on block row k+3 waits on -- TRSM(k+3,k) and the updates of tiles
-  // (k+3, k+1..k+3) with panel k -- are emitted as soon as their last dependency is (not at their simulated start), so
-  // a worker claims them early and starts the moment their inputs land, instead of when the queue reaches them behind
-  // trailing updates.  The order stays topological: every dependency is emitted (or a chain task) before them.
+  // the worker tasks the chain's staging of block k+2 waits on -- TRSM(k+2,k), UPDATE(k+2,k+1,k), UPDATE(k+2,k+2,k)
+  // -- are emitted as soon as their last dependency is (not at their simulated start), so a worker claims them early
+  // and starts the moment their inputs land, instead of when the queue reaches them behind trailing updates.  The
+  // order stays topological: every dependency is emitted (or a chain task) before them.
   auto is_eager = [](const Task& x) {
-    return (x.type == 1 && x.i == x.k + 3) || (x.type == 2 && x.i == x.k + 3 && x.j >= x.i - 2);
+    return (x.type == 1 && x.i == x.k + 2) || (x.type == 2 && x.i == x.k + 2 && (x.j == x.i || x.j == x.i - 1));
   };
   std::vector<char> emitted(T.size(), 0);
   size_t nsched = 0;
@@ -800,7 +796,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   if (ctx->hctrl->df_status != 0)
     return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
   if (ctx->df_trace) {  // instrumentation only: task order + timeline of this factorization
-    std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 6 * ctx->nblk));
+    std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk));
     std::vector<unsigned> ord(ctx->df_ntasks);
     CHK(copy_sync(ctx, tr.data(), ctx->df_trace, tr.size() * 8, hipMemcpyDeviceToHost));
     CHK(copy_sync(ctx, ord.data(), ctx->df_tasks, ord.size() * 4, hipMemcpyDeviceToHost));
@@ -1598,7 +1594,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     CHK(dalloc(ctx, &ctx->df_work, chol_dataflow_work_ints(ctx->nblk)));
     if (const char* e = getenv("CVXG_DF_TRACE")) {  // instrumentation only: the task timeline of the last factorization
       ctx->df_trace_path = e;
-      CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 6 * ctx->nblk)));
+      CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk)));
     }
   }
   CHK(dalloc(ctx, &ctx->bwd_flags, bwd_work_ints(ctx->nblk)));

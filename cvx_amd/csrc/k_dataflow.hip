@@ -1,10 +1,8 @@
 // k_dataflow.hip — the whole regularized-Cholesky factorization (right-looking dpotrf('L'),
 // MatrixUtils.scala:452-461) with the fused forward solve, as ONE persistent launch over a tile DAG.
 //
-// Tiles are 64 x 64 (NB).  Two chain workgroups run the critical path: for diagonal block b, panel b-2 applied to
-// block row b (TRSM(b,b-2), UPDATE(b,b,b-2), UPDATE(b,b-1,b-2)), then TRSM(b,b-1) and UPDATE(b,b,b-1) in slices, then
-// POTRF(b).  The other tasks, in an order fixed on the host by list-scheduling the DAG with its critical-path
-// priorities (cvxg.cpp, build_chol_schedule):
+// Tiles are 64 x 64 (NB).  Tasks, in an order fixed on the host by list-scheduling the DAG with its
+// critical-path priorities (cvxg.cpp, build_chol_schedule):
 //   POTRF(k)      factor the diagonal tile, L_kk^-1 into Linv[k], forward-solve rhs block k
 //   TRSM(i,k)     L_ik = A_ik L_kk^-T (MFMA, product with L_kk^-1); rhs_i -= L_ik w_k
 //   UPDATE(i,j,k) A_ij -= L_ik L_jk^T (MFMA), k < j <= i
@@ -24,7 +22,6 @@ namespace cvxg {
 
 
 constexpr int DF_SP = NB + 2;  // LDS row stride (doubles) of a staged 64 x 64 operand: conflict-free fragments
-constexpr int DF_CH_REC = 6;  // trace records per diagonal block (the chain's stamps; CVXG_DF_TRACE)
 constexpr int DF_SMEM = 4 * NB * (NB + 2) + 2 * 16 * (NB + 2) + 512;  // doubles (~142 KB): > half the CU's LDS, so one workgroup per CU
 
 // LDS of the critical-chain workgroup: POTRF's workspace (tile, L^-1, rhs) + the TRSM tile L_k+1,k + L' w_k
@@ -57,7 +54,7 @@ __device__ __forceinline__ double qf_entry(const QFold& f, int r, int c, double 
 }
 // a 64 x 64 tile's loads (df_load layout) of Q(r0.., c0..) from H
 __device__ __forceinline__ void qf_load(f64x2 (&v)[NB * NB / 512], const QFold& f, int ld, int r0, int c0) {
-  const int tid = opq_tid();
+  const int tid = threadIdx.x;
   const Sc1Mem mH(const_cast<double*>(f.H) + (size_t)r0 * ld + c0, tile_bytes(ld));
 #pragma unroll
   for (int q = 0; q < NB * NB / 512; ++q) {
@@ -98,7 +95,7 @@ __device__ bool df_wait(const int* state, int idx, int want, int* abortw, DevCtr
 
 // Stage a 64 x 64 tile (descriptor m, leading dimension ld) into LDS [64][DF_SP]: 8 x 16-B sc1 loads per thread.
 __device__ __forceinline__ void df_stage(double* __restrict__ dst, const Sc1Mem& m, int ld) {
-  const int tid = opq_tid();
+  const int tid = threadIdx.x;
   f64x2 v[NB * NB / 512];
 #pragma unroll
   for (int q = 0; q < NB * NB / 512; ++q) {
@@ -116,7 +113,7 @@ __device__ __forceinline__ void df_stage(double* __restrict__ dst, const Sc1Mem&
 
 // The two halves of df_stage, for software pipelining: loads into registers, then LDS stores.
 __device__ __forceinline__ void df_load(f64x2 (&v)[NB * NB / 512], const Sc1Mem& m, int ld) {
-  const int tid = opq_tid();
+  const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < NB * NB / 512; ++q) {
     const int idx = q * 256 + tid;
@@ -124,7 +121,7 @@ __device__ __forceinline__ void df_load(f64x2 (&v)[NB * NB / 512], const Sc1Mem&
   }
 }
 __device__ __forceinline__ void df_put(double* __restrict__ dst, const f64x2 (&v)[NB * NB / 512]) {
-  const int tid = opq_tid();
+  const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < NB * NB / 512; ++q) {
     const int idx = q * 256 + tid;
@@ -190,7 +187,7 @@ __device__ __forceinline__ void df_load_c(d4f (&acc)[2][2], const Sc1Mem& mC, in
 }
 
 __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, double* smem, const QFold& qf) {
-  const int tid = opq_tid(), lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const bool active = !(i == j && wc > wr);
   const Sc1Mem mC(L + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
@@ -223,7 +220,7 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
 // UPDATE4(i,j,k0): A_ij -= sum_{k=k0}^{k0+3} L_ik L_jk^T — one read-modify-write of the tile for four panels,
 // with the operand tiles of panel k+1 loaded into registers while the MFMAs of panel k run (two LDS buffers).
 __device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0, double* smem, const QFold& qf) {
-  const int tid = opq_tid(), lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const bool active = !(i == j && wc > wr);
   const bool diag = (i == j);
@@ -271,7 +268,7 @@ __device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0,
 __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __restrict__ rhs, int nrhs,
                         double* __restrict__ Linv, double* smem, const int* state, int* abortw, DevCtrl* ctrl,
                         int* s_ok, const QFold& qf) {
-  const int tid = opq_tid(), lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   double* Pi = smem;
   double* Pj = smem + NB * DF_SP;
   const Sc1Mem mA(L + (size_t)i * NB * ld + (size_t)k * NB, tile_bytes(ld));
@@ -348,7 +345,10 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
 // TRSM slice CB: L'[16 w.., 16 CB..] = A[16 w.., :] L^-1[16 CB.., :]^T (K = 16 (CB + 1): L^-1 is lower); af = the
 // wave's row-block of A as MFMA A-fragments (loaded once per block), E = row-block CB of L^-1 (row stride DF_SP).
 template <int CB>
-__device__ __forceinline__ d4f ch_trsm_x(const double (&af)[16], const double* xf) {  // xf: the B-fragments
+__device__ __forceinline__ d4f ch_trsm(const double (&af)[16], const double* E, int lane) {
+  double xf[4 * (CB + 1)];
+#pragma unroll
+  for (int s = 0; s < 4 * (CB + 1); ++s) xf[s] = E[(lane & 15) * DF_SP + 4 * s + (lane >> 4)];
   d4f acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int s = 0; s < 4 * (CB + 1); s += 2) {
@@ -356,13 +356,6 @@ __device__ __forceinline__ d4f ch_trsm_x(const double (&af)[16], const double* x
     acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s + 1], xf[s + 1], acc1, 0, 0, 0);
   }
   return acc0 + acc1;
-}
-template <int CB>
-__device__ __forceinline__ d4f ch_trsm(const double (&af)[16], const double* E, int lane) {
-  double xf[4 * (CB + 1)];
-#pragma unroll
-  for (int s = 0; s < 4 * (CB + 1); ++s) xf[s] = E[(lane & 15) * DF_SP + 4 * s + (lane >> 4)];
-  return ch_trsm_x<CB>(af, xf);
 }
 // the 10 lower 16 x 16 blocks of a 64 x 64 tile, 3 / 3 / 2 / 2 per wave (-1: none)
 constexpr int kChIB[4][3] = {{0, 3, 3}, {1, 3, 2}, {1, 3, -1}, {2, 2, -1}};
@@ -389,51 +382,6 @@ __device__ __forceinline__ void ch_update(d4f (&dacc)[3], const double* Lp, int 
       if (kChIB[W][q] >= 0)
         dacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-lf[kChIB[W][q] < 0 ? 0 : kChIB[W][q]][st],
                                                        lf[kChJB[W][q] < 0 ? 0 : kChJB[W][q]][st], dacc[q], 0, 0, 0);
-}
-
-// D_b's lower 16 x 16 blocks of this wave (kChIB / kChJB) into MFMA accumulators, from L (or Q folded from H on the
-// tile's first touch)
-__device__ __forceinline__ void ch_load_diag(d4f (&dacc)[3], const double* src, int ld, int b, bool fold,
-                                             const QFold& qf, int wv, int lane) {
-  const Sc1Mem mD(const_cast<double*>(src) + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int ib = kChIB[wv][q], jb = kChJB[wv][q];
-    if (ib >= 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rr = 16 * ib + (lane >> 4) + 4 * r, cc = 16 * jb + (lane & 15);
-        const double h = mD.ld(rr * ld + cc);
-        dacc[q][r] = fold ? qf_entry(qf, b * NB + rr, b * NB + cc, h) : h;
-      }
-    }
-  }
-}
-// TRSM on the chain workgroup: acc[cb] = A[16 w.., :] X[16 cb.., :]' for the four column blocks (X = L^-1 in LDS, row
-// stride P64_SP, zero above the diagonal, so K = 16 (cb + 1)), each block one accumulation chain in K order -- df_trsm's
-// sums -- with the four chains interleaved for latency.
-__device__ __forceinline__ void ch_trsm_seq(d4f (&acc)[4], const double (&af)[16], const double* X, int lane) {
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) acc[cb] = d4f{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int s = 0; s < 16; ++s)
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-      if (s < 4 * (cb + 1))
-        acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s], X[(16 * cb + (lane & 15)) * P64_SP + 4 * s + (lane >> 4)],
-                                                       acc[cb], 0, 0, 0);
-}
-// acc[cb] -= A[16 rows, :] B[16 cb.., :]' over K = 64 (A: this wave's row-block, B: a 64 x 64 tile, both row stride
-// DF_SP in LDS): df_update's single accumulation chain per 16 x 16 block, in K order
-__device__ __forceinline__ void ch_gemm_nt(d4f (&acc)[4], const double* A, const double* B, int lane) {
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int kk = 4 * s + (lane >> 4);
-    const double a = -A[(lane & 15) * DF_SP + kk];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, B[(16 * cb + (lane & 15)) * DF_SP + kk], acc[cb], 0, 0, 0);
-  }
 }
 
 __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L, int ld, double* __restrict__ rhs,
@@ -473,7 +421,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     Potrf64wSmem& ps = cs.p;
     const int lane = tid & 63, wv = tid >> 6;
     auto mark = [&](int k, int step, int field) {
-      if (trace && tid == 0) trace[4 * (size_t)(ntasks + DF_CH_REC * k + step) + field] = __builtin_amdgcn_s_memrealtime();
+      if (trace && tid == 0) trace[4 * (size_t)(ntasks + 3 * k + step) + field] = __builtin_amdgcn_s_memrealtime();
     };
     auto publish = [&](int idx, int v) {
       df_drain();  // every storing wave: its sc1 stores have left
@@ -505,184 +453,41 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       } else {
         const int k = b - 1;
         mark(k, 1, 0);
+        // A_b,k and D_b with every panel < k applied (state >= k), and the rhs block b with all earlier TRSM
+        // updates: one wait for both states, then every load in flight together (minus L_b,k w_k inside POTRF(b);
+        // POTRF(b-2) of this workgroup is done with ps.B)
+        if (tid == 0)
+          s_ok = df_wait(state, df_tri(b, k), k, abortw, ctrl) && df_wait(state, df_tri(b, b), k, abortw, ctrl);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        if (!s_ok) return;
         const Sc1Mem mA(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
         d4f dacc[NBLK16];
-        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
-        // The row-blocks of L_kk^-1 already published when the staging ends (usually three or four: the panel work
-        // ends late in POTRF(k)) run as one batch -- loaded together into ps.S (free until the diagonal tile goes there
-        // at the end), their TRSM products back to back, one barrier, their diagonal updates; the rest one slice each
-        // as they arrive.  The same MFMA sequence per output either way, so the factor is the same.  The flag is read
-        // before the staging's last MFMAs and the row-block loads all go out before the staging's LDS stores, so
-        // neither round trip is paid on the chain.
-        int nbat = 0;
-        f64x2 vb[8];
-        auto bload = [&]() {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int e = opq_tid() + 256 * q;
-            if (q < 2 * nbat) vb[q] = mI.ld2((e >> 5) * NB + 2 * (e & 31));
-          }
-        };
-        auto bput = [&]() {  // row-blocks 0 .. nbat-1 of L_kk^-1 -> ps.S rows 0 .. 16 nbat-1
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int e = opq_tid() + 256 * q;
-            if (q < 2 * nbat) *reinterpret_cast<f64x2*>(ps.S + (e >> 5) * P64_SP + 2 * (e & 31)) = vb[q];
-          }
-        };
-        if (b == 1) {
-          // A_1,0 and D_1 (first read here: Q folded from H) and the rhs block 1: every load in flight together
-          if (!wait(state, df_tri(b, k), k)) return;
+        {
           f64x2 va[NB * NB / 512];
-          const bool fold = qf.H != nullptr;
+          const bool fold = qf.H && k == 0;  // block 1: A_1,0 and D_1 are first read here
           if (fold) qf_load(va, qf, ld, b * NB, 0);
           else df_load(va, mA, ld);
-          ch_load_diag(dacc, fold ? qf.H : L, ld, b, fold, qf, wv, lane);
+          const Sc1Mem mD(const_cast<double*>(fold ? qf.H : L) + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
+#pragma unroll
+          for (int q = 0; q < NBLK16; ++q) {
+            const int ib = kChIB[wv][q], jb = kChJB[wv][q];
+            if (ib >= 0) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int rr = 16 * ib + (lane >> 4) + 4 * r, cc = 16 * jb + (lane & 15);
+                const double h = mD.ld(rr * ld + cc);
+                dacc[q][r] = fold ? qf_entry(qf, b * NB + rr, b * NB + cc, h) : h;
+              }
+            }
+          }
           const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
           for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
           df_put(cs.Sa, va);
-          if (tid == 0) s_next = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          __syncthreads();
-          nbat = min(s_next, 4);
-          bload();
-          bput();
-        } else {
-          // Panel k2 = b - 2 is applied to block row b here, not by the workers: this workgroup factored block k2
-          // (L_k2,k2^-1 in ps.X, w_k2 in ps.W), so TRSM(b, k2), UPDATE(b, b, k2) and UPDATE(b, k, k2) cost no
-          // hand-off of their inputs -- the worker path (TRSM -> UPDATE -> staging) delivered A_b,k and D_b ~14 us
-          // into POTRF(k).  Their worker inputs (tiles (b, k2), (b, b), (b, k) with every panel < k2) are final well
-          // before this workgroup's POTRF(k2) ends, so all of them are loaded at once; only L_k,k2 (the other chain
-          // workgroup's slices, published when its POTRF(k) starts) arrives later.  The same operations in the same
-          // order as the worker tasks (df_trsm, df_update): the factor is bit-identical.
-          const int k2 = b - 2;
-          const bool fold = qf.H && k2 == 0;  // block row 2: A_2,0, D_2 and A_2,1 are first read here
-          if (tid == 0) {  // (the three polls in flight together: usually all three inputs are final already)
-            const int v0 = df_poll(state + df_tri(b, k2)), v1 = df_poll(state + df_tri(b, b)),
-                      v2 = df_poll(state + df_tri(b, k));
-            s_ok = (v0 >= k2 || df_wait(state, df_tri(b, k2), k2, abortw, ctrl)) &&
-                   (v1 >= k2 || df_wait(state, df_tri(b, b), k2, abortw, ctrl)) &&
-                   (v2 >= k2 || df_wait(state, df_tri(b, k), k2, abortw, ctrl));
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          __syncthreads();
-          if (!s_ok) return;
-          mark(k, 3, 0);
-          const Sc1Mem mA2(L + (size_t)b * NB * ld + (size_t)k2 * NB, tile_bytes(ld));
-          {
-            f64x2 va[NB * NB / 512];
-            if (fold) qf_load(va, qf, ld, b * NB, 0);
-            else df_load(va, mA2, ld);
-            ch_load_diag(dacc, fold ? qf.H : L, ld, b, fold, qf, wv, lane);
-            df_put(cs.Sa, va);  // (waits for the A_b,k2 loads only: the younger D_b loads stay in flight)
-          }
-          __syncthreads();
-          mark(k, 3, 1);
-          // TRSM(b, k2) = A_b,k2 L_k2,k2^-T
-          {
-            double af2[16];  // this wave's row-block of A_b,k2 as MFMA A-fragments
-#pragma unroll
-            for (int q = 0; q < 16; ++q) af2[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
-            d4f acc[4];
-            ch_trsm_seq(acc, af2, ps.X, lane);
-            __syncthreads();  // every wave holds its fragments: Sa takes L_b,k2
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
-                cs.Sa[row * DF_SP + col] = acc[cb][r];
-                mA2.st(row * ld + col, acc[cb][r]);
-              }
-          }
-          // L_b,k2 stored at once (the workers' UPDATE(i, b, k2), i > b: UPDATE(b + 1, b, k2) feeds the next chain
-          // block's panel work), with a non-blocking look at L_k,k2: when it is already published, its loads go out
-          // before the diagonal update and land behind its MFMAs.  publish()'s barrier also completes L_b,k2 in Sa.
-          df_drain();
-          if (tid == 0) s_next = __hip_atomic_load(state + df_tri(k, k2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                                 k2 + 1;
-          __syncthreads();
-          if (tid == 0) __hip_atomic_store(state + df_tri(b, k2), k2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          mark(k, 3, 2);
-          const bool have_l = s_next;
-          // rhs_b -= L_b,k2 w_k2, df_trsm's sums (w_k2 = ps.W, the forward solve of this workgroup's POTRF(k2)); the
-          // rhs block b carries every TRSM(b, j < k2) update (state(b, k2) >= k2).  Its loads go out before L_k,k2's.
-          constexpr int RQ = (NB * MAX_RHS + 255) / 256;
-          double rv[RQ];
-          {
-            const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-#pragma unroll
-            for (int q = 0; q < RQ; ++q)
-              if (tid + 256 * q < NB * nrhs) rv[q] = mR.ld(tid + 256 * q);
-          }
-          d4f aacc[4];  // A_b,k: this wave's 16 rows x 4 column blocks, MFMA accumulator layout (loaded here, not with
-                        // the others, to keep the register peak of the prefetch down; it lands behind the updates)
-          {
-            const Sc1Mem mC(const_cast<double*>(fold ? qf.H : L) + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
-                const double h = mC.ld(row * ld + col);
-                aacc[cb][r] = fold ? qf_entry(qf, b * NB + row, k * NB + col, h) : h;
-              }
-          }
-          const Sc1Mem mL(L + (size_t)k * NB * ld + (size_t)k2 * NB, tile_bytes(ld));
-          f64x2 vl[NB * NB / 512];
-          if (have_l) df_load(vl, mL, ld);
-#pragma unroll
-          for (int q = 0; q < RQ; ++q) {
-            const int t = tid + 256 * q;
-            if (t < NB * nrhs) {
-              const int row = t / nrhs, rho = t % nrhs;
-              double sv = 0.0;
-#pragma unroll 8
-              for (int c = 0; c < NB; ++c) sv = fma(cs.Sa[row * DF_SP + c], ps.W[c * nrhs + rho], sv);
-              ps.B[t] = rv[q] - sv;
-            }
-          }
-          // UPDATE(b, b, k2): D_b -= L_b,k2 L_b,k2' (the K order of df_update's single accumulation chain)
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb) {
-            switch (wv) {
-              case 0: ch_update<0>(dacc, cs.Sa, cb, lane); break;
-              case 1: ch_update<1>(dacc, cs.Sa, cb, lane); break;
-              case 2: ch_update<2>(dacc, cs.Sa, cb, lane); break;
-              default: ch_update<3>(dacc, cs.Sa, cb, lane); break;
-            }
-          }
-          mark(k, 2, 3);
-          if (!have_l) {
-            if (!wait(state, df_tri(k, k2), k2 + 1)) return;
-            df_load(vl, mL, ld);
-          }
-          df_put(ps.S, vl);  // (POTRF(k2)'s tile was stored: ps.S is free until the slices' diagonal tile)
-          __syncthreads();
-          mark(k, 3, 3);
-          // UPDATE(b, k, k2): A_b,k -= L_b,k2 L_k,k2'  (the L_kk^-1 flag read goes out ahead of it)
-          int pv = 0;
-          if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ch_gemm_nt(aacc, cs.Sa + 16 * wv * DF_SP, ps.S, lane);
-          mark(k, 4, 0);
-          if (tid == 0) s_next = pv;  // (have_l was read before the barrier above)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          __syncthreads();  // every wave is done with L_b,k2 in Sa (which then takes A_b,k) and with ps.S
-          nbat = min(s_next, 4);
-          bload();
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
-              cs.Sa[row * DF_SP + col] = aacc[cb][r];
-            }
-          bput();
         }
         potrf64w_reset(ps);  // the slices leave POTRF's L^-1 workspace and flags alone: clear them off the chain
-        if (tid == 0) ps.staged = 0;  // the waves count their blocks of D_b in at the end of the slices
-        mark(k, 1, 1);       // (the first slice's wait below is the barrier that completes Sa)
+        mark(k, 1, 1);
+        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
         // L_b,k, row stride DF_SP: written over A_b,k in Sa (every wave holds its row-block of A in af before the first
         // slice's barrier), where it stays for the rhs correction at the end of POTRF(b) — no copy before POTRF
         double* Lp = cs.Sa;
@@ -693,53 +498,21 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         auto eload = [&](int cb) {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
-            const int e = opq_tid() + 256 * q;  // (opaque: the addresses are not kept live across the chain loop)
+            const int e = tid + 256 * q;
             er[q] = mI.ld2((16 * cb + (e >> 5)) * NB + 2 * (e & 31));
           }
         };
-        __syncthreads();  // completes Sa and the batch's row-blocks in ps.S
-        double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments
+        if (!wait(cflag, k, 1)) return;
+        eload(0);
+        double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments (Sa staged behind the barriers above)
 #pragma unroll
         for (int q = 0; q < 16; ++q) af[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
-        if (nbat > 0) {
-          d4f acc[4];
-          acc[0] = ch_trsm<0>(af, ps.S, lane);
-          if (nbat > 1) acc[1] = ch_trsm<1>(af, ps.S + 16 * P64_SP, lane);
-          if (nbat > 2) acc[2] = ch_trsm<2>(af, ps.S + 32 * P64_SP, lane);
-          if (nbat > 3) acc[3] = ch_trsm<3>(af, ps.S + 48 * P64_SP, lane);
-          __syncthreads();  // every wave holds its fragments of A (Sa takes L')
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb)
-            if (cb < nbat)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
-                Lp[row * DF_SP + col] = acc[cb][r];
-                mA.st(row * ld + col, acc[cb][r]);
-              }
-          __syncthreads();
-          for (int cb = 0; cb < nbat; ++cb) {
-            switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
-              case 0: ch_update<0>(dacc, Lp, cb, lane); break;
-              case 1: ch_update<1>(dacc, Lp, cb, lane); break;
-              case 2: ch_update<2>(dacc, Lp, cb, lane); break;
-              default: ch_update<3>(dacc, Lp, cb, lane); break;
-            }
-          }
-        }
-        if (tid == 0 && trace) trace[4 * (size_t)(ntasks + DF_CH_REC * k + 4) + 3] = nbat;
-        mark(k, 4, 2);  // trace: batch done
-        if (nbat < 4) {
-          if (!wait(cflag, k, nbat + 1)) return;
-          eload(nbat);
-        }
-        bool have_next = nbat < 4;
+        bool have_next = false;
 #pragma unroll 1
-        for (int cb = nbat; cb < 4; ++cb) {
+        for (int cb = 0; cb < 4; ++cb) {
           double* E = cs.E2[cb & 1];
           if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
-          if (!have_next) {
-            if (cb == 3) mark(k, 4, 1);  // trace: waiting for the last row-block
+          if (cb > 0 && !have_next) {
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
           }
@@ -780,23 +553,13 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             default: ch_update<3>(dacc, Lp, cb, lane); break;
           }
         }
-        if (nbat == 4) mark(k, 1, 3);
 #pragma unroll
         for (int q = 0; q < NBLK16; ++q) {
           const int ib = kChIB[wv][q], jb = kChJB[wv][q];
           if (ib >= 0) c16_store(ps.S + 16 * ib * P64_SP + 16 * jb, P64_SP, dacc[q], lane);
         }
-        mark(b, 0, 3);  // trace: D_b in LDS (before the drain)
-        // hand-off without a workgroup barrier: each wave drains its sc1 stores of L_b,k and counts itself in; the
-        // last one publishes L_b,k (the next chain block's panel work waits on it: publishing it only after POTRF(b)'s
-        // first sweep, to spare wave 0 the drain, measured slower).  Wave 0 owns D_00 and starts POTRF(b) at once;
-        // the other waves (and wave 0 before its first T / U) wait for all four (potrf64w_factor)
-        df_drain();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0 && __hip_atomic_fetch_add(&ps.staged, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 3) {
-          __hip_atomic_store(state + df_tri(b, k), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (trace) trace[4 * (size_t)(ntasks + DF_CH_REC * k + 1) + 2] = __builtin_amdgcn_s_memrealtime();
-        }
+        publish(df_tri(b, k), k + 1);  // L_b,k stored
+        mark(k, 1, 2);
       }
       // POTRF(b): tile and rhs block staged in LDS; L_bb^-1 row-blocks published progressively; before the
       // forward solve, the rhs block gets its last correction  - L_b,b-1 w_b-1  (w_b-1: POTRF(b-1) done)
@@ -831,8 +594,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         potrf64w_reset(ps);
         __syncthreads();
       }  // b > 0: reset behind the staging, the tile's LDS stores behind publish()'s barrier
-      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix,
-                                   trace ? trace + 4 * (size_t)(ntasks + DF_CH_REC * b + 5) : nullptr)) {
+      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }

@@ -18,15 +18,6 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int AUX_SC1 = 16;  // cache-policy bits of a buffer access: sc1 (L1 bypass, write-through)
 
-// threadIdx.x behind an empty volatile asm: the index arithmetic derived from it at one site is neither hoisted to the
-// kernel entry nor shared with other sites, so the persistent dataflow kernel (one register allocation for the chain
-// and the workers, at the 512-register cap) does not hold every site's addresses live for its whole lifetime.
-__device__ __forceinline__ int opq_tid() {
-  int t = threadIdx.x;
-  asm volatile("" : "+v"(t));
-  return t;
-}
-
 __device__ __forceinline__ double rsqrt_nr(double p) {
   double y = __builtin_amdgcn_rsq(p);
   const double h = 0.5 * p;

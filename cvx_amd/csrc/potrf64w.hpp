@@ -37,8 +37,6 @@ struct Potrf64wSmem {
   int fail;
   int fP, fT;                 // wave 0: steps whose P / T are published
   int cntT[4], cntU[4];       // waves 1..3 done with phase A / B of step kb
-  int cntL[4];                // waves 1..3 whose blocks of L^-1 row-block kb are stored (the last raises the flag)
-  int staged;                 // waves whose blocks of the tile are in S (4: all; the chain counts them in)
 };
 
 __device__ __forceinline__ int p64w_load(const int* f) {
@@ -66,7 +64,7 @@ __device__ __forceinline__ bool p64w_wait(Potrf64wSmem& sm, const int* f, int wa
 template <class M>
 __device__ __forceinline__ void potrf64w_stage(const double* L, int ld, size_t off, const double* rhs, int k, int nrhs,
                                                Potrf64wSmem& sm) {
-  const int tid = opq_tid();
+  const int tid = threadIdx.x;
   const M mL(const_cast<double*>(L) + off, tile_bytes(ld));
   f64x2 v[NB * NB / 512];
 #pragma unroll
@@ -98,15 +96,10 @@ __device__ __forceinline__ void p64w_U(Potrf64wSmem& sm, int ib, int jb, int kb,
                    lane);
   c16_store(C, P64_SP, acc, lane);
 }
-// X_kb,j = -L16_kb^-1 T with T = sum_{m=j}^{kb-1} L_kb,m X_m,j (j < kb): p64w_Xpre forms T (it needs no part of step kb's
-// sweep, so step 3's runs while wave 0 sweeps), p64w_Xfin the rest
-__device__ __forceinline__ d4f p64w_Xpre(const Potrf64wSmem& sm, int kb, int j, int lane) {
+__device__ __forceinline__ void p64w_X(Potrf64wSmem& sm, int kb, int j, int lane) {  // X_kb,j, j < kb
   d4f T = {0.0, 0.0, 0.0, 0.0};
   for (int m = j; m < kb; ++m)
     T = mfma16_ab(T, sm.S + 16 * kb * P64_SP + 16 * m, P64_SP, sm.X + 16 * m * P64_SP + 16 * j, P64_SP, 1.0, lane);
-  return T;
-}
-__device__ __forceinline__ void p64w_Xfin(Potrf64wSmem& sm, int kb, int j, d4f T, int lane) {
   const double* ET = sm.ET[kb];
   d4f acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -115,9 +108,6 @@ __device__ __forceinline__ void p64w_Xfin(Potrf64wSmem& sm, int kb, int j, d4f T
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] *= sm.SV[kb][(lane >> 4) + 4 * i];  // row scales (C layout: row (lane>>4) + 4i)
   c16_store(sm.X + 16 * kb * P64_SP + 16 * j, P64_SP, acc, lane);
-}
-__device__ __forceinline__ void p64w_X(Potrf64wSmem& sm, int kb, int j, int lane) {  // X_kb,j, j < kb
-  p64w_Xfin(sm, kb, j, p64w_Xpre(sm, kb, j, lane), lane);
 }
 // X_kb,kb = (L16^-T)' with the column scales, and the scales of the L16 block of S (L16 = L~16 diag(s))
 __device__ __forceinline__ void p64w_Xdiag(Potrf64wSmem& sm, int kb, int lane) {
@@ -193,7 +183,7 @@ __device__ __forceinline__ bool p64w_eliminate(Potrf64wSmem& sm, int kb, int bas
 }
 
 // Phase A / B work of waves 1..3 at step kb (static assignment, see the header).
-__device__ __forceinline__ void p64w_phaseA(Potrf64wSmem& sm, int kb, int w, int lane, d4f T3) {
+__device__ __forceinline__ void p64w_phaseA(Potrf64wSmem& sm, int kb, int w, int lane) {
   if (kb == 0) {
     if (w == 1) p64w_T(sm, 2, 0, lane);
     if (w == 2) p64w_T(sm, 3, 0, lane);
@@ -206,9 +196,13 @@ __device__ __forceinline__ void p64w_phaseA(Potrf64wSmem& sm, int kb, int w, int
     if (w == 1) p64w_X(sm, 2, 0, lane);
     if (w == 2) p64w_X(sm, 2, 1, lane);
     if (w == 3) p64w_Xdiag(sm, 2, lane);
-  } else {  // X_3,w-1 from the T formed during step 2 (p64w_Xpre)
-    p64w_Xfin(sm, 3, w - 1, T3, lane);
-    if (w == 3) p64w_Xdiag(sm, 3, lane);
+  } else {
+    if (w == 1) p64w_X(sm, 3, 0, lane);
+    if (w == 2) p64w_X(sm, 3, 1, lane);
+    if (w == 3) {
+      p64w_X(sm, 3, 2, lane);
+      p64w_Xdiag(sm, 3, lane);
+    }
   }
 }
 __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int lane) {
@@ -229,15 +223,14 @@ __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int
 }
 
 // The factorization of block k: tile staged in sm.S, rhs block in sm.B, flags reset (potrf64w_reset), a barrier
-// behind -- or, for the tile's blocks, sm.staged counted up to 4 by the waves that wrote them (wave 0 starts its first
-// sweep on its own block D_00 without waiting for the others).  On return (uniformly true / false) sm.X = L^-1 (exact zeros above the diagonal), sm.W = w = L^-1 b (also
+// behind.  On return (uniformly true / false) sm.X = L^-1 (exact zeros above the diagonal), sm.W = w = L^-1 b (also
 // stored to rhs block k); Linv[k] = L^-1 is stored row-block by row-block as it becomes final (wave 3), and *lflag
 // (when given) counts the stored row-blocks (sc1 hand-off: the stores drained first).  fix() runs on all threads
 // between the factorization and the forward solve (barrier behind it).  L_kk is not stored (potrf64w_store_L).
 template <class M, class Fix = NoFix>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
-                                                Fix fix = Fix(), unsigned long long* lstamp = nullptr) {
+                                                Fix fix = Fix()) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -256,11 +249,6 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_publish(&sm.fP, kb + 1);
       if (kb < 3) {
-        // step 0's sweep reads only wave 0's own block D_00; T(1, 0) / U(1, 1, 0) read the other waves' blocks
-        if (kb == 0 && !p64w_wait(sm, &sm.staged, 4)) {
-          ok = false;
-          break;
-        }
         if (kb >= 1 && !p64w_wait(sm, &sm.cntU[kb - 1], 3)) {
           ok = false;
           break;
@@ -276,56 +264,42 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       }
     }
   } else {
-    d4f T3 = {0.0, 0.0, 0.0, 0.0};  // the T of X_3,w-1, formed in step 2's (otherwise empty) phase-B slot
 #pragma unroll 1
     for (int kb = 0; kb < 4 && ok; ++kb) {
-      ok = (kb > 0 || p64w_wait(sm, &sm.staged, 4)) && p64w_wait(sm, &sm.fP, kb + 1) &&
-           (kb == 0 || p64w_wait(sm, &sm.cntU[kb - 1], 3));
+      ok = p64w_wait(sm, &sm.fP, kb + 1) && (kb == 0 || p64w_wait(sm, &sm.cntU[kb - 1], 3));
       if (!ok) break;
       P64_STAMP(1 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      p64w_phaseA(sm, kb, w, opq_tid() & 63, T3);
+      p64w_phaseA(sm, kb, w, lane);
       P64_STAMP(2 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_add(&sm.cntT[kb]);
-      if (lflag) {
-        // row-block kb of L^-1: each wave stores the blocks X_kb,j its phase A just formed (the upper blocks of Linv
-        // stay the zeros they were allocated with), later drains and counts itself in (count_in); the last of the
-        // three raises the flag (an agent-scope max: the flags of consecutive steps may be raised by different waves)
-        const int j0 = (kb == 0) ? ((w == 3) ? 0 : -1) : (kb == 1) ? ((w == 1) ? -1 : w - 2) : w - 1;
-        const int nj = (kb == 3 && w == 3) ? 2 : (j0 >= 0 ? 1 : 0);
-        const int r = lane >> 2, c = 4 * (lane & 3);
-        for (int jj = 0; jj < nj; ++jj) {
-          const int rr = 16 * kb + r, cc = 16 * (j0 + jj) + c;
+      if (lflag && w == 3) {  // row-block kb of L^-1 is final once every wave's phase A is
+        if (!p64w_wait(sm, &sm.cntT[kb], 3)) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int e = lane + 64 * q, rr = 16 * kb + (e >> 5), cc = 2 * (e & 31);
           mI.st2(rr * NB + cc, *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc));
-          mI.st2(rr * NB + cc + 2, *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc + 2));
+        }
+        if (lflag != PUBLISH_ONLY) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_store(lflag, kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-      // the drain and count of row-block kb: at once for the last one, behind phase B otherwise (the stores complete
-      // during its MFMAs instead of holding up the next sweep's inputs)
-      auto count_in = [&]() {
-        if (lflag && lflag != PUBLISH_ONLY) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == 0 &&
-              __hip_atomic_fetch_add(&sm.cntL[kb], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 2) {
-            __hip_atomic_fetch_max(lflag, kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (lstamp) lstamp[kb] = __builtin_amdgcn_s_memrealtime();  // (trace: row-block kb's flag raised)
-          }
-        }
-      };
-      if (kb == 3) count_in();
       if (kb < 3) {
         ok = p64w_wait(sm, &sm.fT, kb + 1) && p64w_wait(sm, &sm.cntT[kb], 3);
         if (!ok) break;
         P64_STAMP(3 + 4 * kb);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        p64w_phaseB(sm, kb, w, opq_tid() & 63);
-        if (kb == 2) T3 = p64w_Xpre(sm, 3, w - 1, opq_tid() & 63);  // L_3,m (m < 3) and X_m,j (m <= 2) are final here
+        p64w_phaseB(sm, kb, w, lane);
         P64_STAMP(4 + 4 * kb);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_add(&sm.cntU[kb]);
-      if (kb < 3) count_in();
     }
   }
   P64_STAMP(17);
@@ -365,7 +339,7 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
 // Before potrf64w_factor: zero the upper blocks of L^-1 (read by callers' MFMAs) and the flags (a barrier must
 // follow).
 __device__ __forceinline__ void potrf64w_reset(Potrf64wSmem& sm) {
-  const int tid = opq_tid();
+  const int tid = threadIdx.x;
   for (int t = tid; t < 6 * 256; t += 256) {
     const int b = t >> 8, e = t & 255;
     const int ib = (b < 3) ? 0 : ((b < 5) ? 1 : 2), jb = (b < 3) ? 1 + b : ((b < 5) ? b - 1 : 3);
@@ -374,13 +348,11 @@ __device__ __forceinline__ void potrf64w_reset(Potrf64wSmem& sm) {
   if (tid < 4) {
     sm.cntT[tid] = 0;
     sm.cntU[tid] = 0;
-    sm.cntL[tid] = 0;
   }
   if (tid == 0) {
     sm.fail = 0;
     sm.fP = 0;
     sm.fT = 0;
-    sm.staged = 4;
   }
 }
 

@@ -4,8 +4,9 @@ POTRF(k+1) start, the fix hook of POTRF(k+1); then the worker tasks feeding bloc
 import sys, numpy as np
 raw=open(sys.argv[1],'rb').read()
 nq,nb=(int(v) for v in np.frombuffer(raw[:8],dtype=np.int32))
-tr=np.frombuffer(raw[8+4*nq:8+4*nq+32*(nq+6*nb)],dtype=np.uint64).reshape(nq+6*nb,4).astype(np.int64)
-ch=tr[nq:].reshape(nb,6,4)
+R=((len(raw)-8-4*nq)//32-nq)//nb  # chain records per block (k_dataflow.hip: 3, or 6 with the panel / row-block stamps)
+tr=np.frombuffer(raw[8+4*nq:8+4*nq+32*(nq+R*nb)],dtype=np.uint64).reshape(nq+R*nb,4).astype(np.int64)
+ch=tr[nq:].reshape(nb,R,4)
 us=lambda v:v/100.0
 rows=[]
 for k in range(2,nb-2):
@@ -41,7 +42,7 @@ for i,l in enumerate(lab):
 print('staged', np.median(res[:,-1]))
 # which is last before staging?
 # the chain's own panel work on block row k+1 (TRSM(k+1,k-1), UPDATE(k+1,k+1,k-1), UPDATE(k+1,k,k-1)), when stamped
-if ch.shape[1] >= 5 and ch[2:nb-2, 3, 0].min() > 0:
+if R >= 5 and ch[2:nb-2, 3, 0].min() > 0:
     lab = ['inputs ready', 'loads landed', 'L_k+1,k-1 published', 'L_k,k-1 in LDS', 'updates done']
     vals = []
     for k in range(2, nb - 2):
@@ -51,7 +52,7 @@ if ch.shape[1] >= 5 and ch[2:nb-2, 3, 0].min() > 0:
     for i, l in enumerate(lab):
         print(f"panel {l:22s} med {np.median(vals[:, i]):7.2f} mean {vals[:, i].mean():7.2f}")
 # L^-1 row-block hand-offs: flags raised by POTRF(k)'s waves (record 5), the consumer's batch / wait for the last one
-if ch[2:nb-2, 5, 3].min() > 0:
+if R >= 6 and ch[2:nb-2, 5, 3].min() > 0:
     v = np.array([[(ch[k, 5, f] - ch[k, 0, 0]) / 100.0 for f in range(4)] for k in range(2, nb - 2)])
     for f in range(4):
         print(f"rb{f} flag raised        med {np.median(v[:, f]):7.2f} mean {v[:, f].mean():7.2f}")

@@ -28,10 +28,7 @@ def _order(nblk, workers=256):
 
 
 def _is_chain(typ, k, i, j):
-    """The chain workgroup of block b runs TRSM(b,b-2), UPDATE(b,b,b-2), UPDATE(b,b-1,b-2), TRSM(b,b-1), UPDATE(b,b,b-1)
-    and POTRF(b)."""
-    return (typ == 1 and i in (k + 1, k + 2)) or (typ == 2 and i == j == k + 1) or \
-        (typ == 2 and i == k + 2 and j in (i, i - 1))
+    return (typ == 1 and i == k + 1) or (typ == 2 and i == j == k + 1)
 
 
 @pytest.mark.parametrize("nblk", [2, 4, 10, 16, 64])
@@ -54,9 +51,9 @@ def test_schedule_covers_every_task_once_in_dependency_order(nblk):
     # coverage
     for k in range(nblk):
         for i in range(k + 1, nblk):
-            assert (i, k) in pos_trsm or _is_chain(1, k, i, k)
+            assert (i, k) in pos_trsm or i == k + 1
             for j in range(k + 1, i + 1):
-                assert (i, j, k) in pos_upd or _is_chain(2, k, i, j), (i, j, k)
+                assert (i, j, k) in pos_upd or (i == j == k + 1), (i, j, k)
     # order: TRSM(i,k) after the update of tile (i,k) with panel k-1; UPDATE(i,j,k) after TRSM(i,k), TRSM(j,k)
     # and after the update of tile (i,j) with panel k-1
     for (i, k), p in pos_trsm.items():
@@ -71,27 +68,3 @@ def test_schedule_covers_every_task_once_in_dependency_order(nblk):
             q = pos_upd.get((i, j, k - 1))
             assert q is None or q <= p
     assert len(order) == len(set(order))
-
-
-@pytest.mark.parametrize("nblk", [4, 10, 16, 64])
-def test_chain_inputs_precede_the_consumers_of_chain_outputs(nblk):
-    """Deadlock freedom across the chain: the chain workgroup of block b waits on the worker updates of block row b
-    with panel b-3 (tiles (b, b-2), (b, b-1), (b, b)); a listed task that consumes an output of chain blocks <= b
-    (L_b,b-2, L_b,b-1 or L_bb^-1) must come after every such input, or the workers could all block on the chain while
-    the chain waits on a task nobody has claimed."""
-    order = _order(nblk)
-    pos = {}
-    for p, (typ, k, i, j) in enumerate(order):
-        cnt = 4 if typ == 3 else 1
-        for kk in range(k, k + cnt):
-            pos[(typ if typ == 1 else 2, i, j if typ != 1 else kk, kk)] = p
-    need = [-1] * nblk  # latest position of a worker input of chain blocks <= b
-    for b in range(nblk):
-        ins = [pos.get((2, b, j, b - 3), -1) for j in (b - 2, b - 1, b)] if b >= 3 else []
-        need[b] = max([need[b - 1] if b > 0 else -1] + ins)
-    for p, (typ, k, i, j) in enumerate(order):
-        # chain outputs consumed: TRSM(i,k) reads L_kk^-1 (block k); UPDATE(i,j,k) reads L_ik, L_jk, chain outputs when
-        # i or j is k + 1 or k + 2
-        blocks = [k] if typ == 1 else [r for r in (i, j) if r - k in (1, 2)]
-        for b in blocks:
-            assert need[b] < p, (typ, k, i, j, b)
