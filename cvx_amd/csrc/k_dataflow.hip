@@ -456,12 +456,20 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         // A_b,k and D_b with every panel < k applied (state >= k), and the rhs block b with all earlier TRSM
         // updates: one wait for both states, then every load in flight together (minus L_b,k w_k inside POTRF(b);
         // POTRF(b-2) of this workgroup is done with ps.B)
-        if (tid == 0)
-          s_ok = df_wait(state, df_tri(b, k), k, abortw, ctrl) && df_wait(state, df_tri(b, b), k, abortw, ctrl);
+        if (tid == 0) {  // (both polls in flight together: usually the second input is final when the first is)
+          const int v0 = df_poll(state + df_tri(b, k)), v1 = df_poll(state + df_tri(b, b));
+          s_ok = (v0 >= k || df_wait(state, df_tri(b, k), k, abortw, ctrl)) &&
+                 (v1 >= k || df_wait(state, df_tri(b, b), k, abortw, ctrl));
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
         if (!s_ok) return;
         const Sc1Mem mA(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
+        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
+        // the row-blocks of L_kk^-1 already published (cflag, read while the tile loads are in flight) are loaded
+        // at once into ps.S (free until the diagonal tile goes there at the end of the slices) and applied as one
+        // batch below
+        int pv = 0;
         d4f dacc[NBLK16];
         {
           f64x2 va[NB * NB / 512];
@@ -481,13 +489,30 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               }
             }
           }
+          if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
           for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
           df_put(cs.Sa, va);
         }
+        if (tid == 0) s_next = pv;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        const int nbat = min(s_next, 4);
+        {
+          f64x2 vb[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int e = tid + 256 * q;
+            if (q < 2 * nbat) vb[q] = mI.ld2((e >> 5) * NB + 2 * (e & 31));
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int e = tid + 256 * q;
+            if (q < 2 * nbat) *reinterpret_cast<f64x2*>(ps.S + (e >> 5) * P64_SP + 2 * (e & 31)) = vb[q];
+          }
+        }
         potrf64w_reset(ps);  // the slices leave POTRF's L^-1 workspace and flags alone: clear them off the chain
         mark(k, 1, 1);
-        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
         // L_b,k, row stride DF_SP: written over A_b,k in Sa (every wave holds its row-block of A in af before the first
         // slice's barrier), where it stays for the rhs correction at the end of POTRF(b) — no copy before POTRF
         double* Lp = cs.Sa;
@@ -502,17 +527,47 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             er[q] = mI.ld2((16 * cb + (e >> 5)) * NB + 2 * (e & 31));
           }
         };
-        if (!wait(cflag, k, 1)) return;
-        eload(0);
-        double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments (Sa staged behind the barriers above)
+        __syncthreads();  // Sa and the batch's row-blocks in ps.S complete
+        double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments
 #pragma unroll
         for (int q = 0; q < 16; ++q) af[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
-        bool have_next = false;
+        if (nbat > 0) {
+          // the batch: the same MFMA sequence per output as the per-slice form below, so the same bits
+          d4f acc[4];
+          acc[0] = ch_trsm<0>(af, ps.S, lane);
+          if (nbat > 1) acc[1] = ch_trsm<1>(af, ps.S + 16 * P64_SP, lane);
+          if (nbat > 2) acc[2] = ch_trsm<2>(af, ps.S + 32 * P64_SP, lane);
+          if (nbat > 3) acc[3] = ch_trsm<3>(af, ps.S + 48 * P64_SP, lane);
+          __syncthreads();  // every wave holds its fragments of A (Sa takes L')
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb)
+            if (cb < nbat)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
+                Lp[row * DF_SP + col] = acc[cb][r];
+                mA.st(row * ld + col, acc[cb][r]);
+              }
+          __syncthreads();
+          for (int cb = 0; cb < nbat; ++cb) {
+            switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
+              case 0: ch_update<0>(dacc, Lp, cb, lane); break;
+              case 1: ch_update<1>(dacc, Lp, cb, lane); break;
+              case 2: ch_update<2>(dacc, Lp, cb, lane); break;
+              default: ch_update<3>(dacc, Lp, cb, lane); break;
+            }
+          }
+        }
+        if (nbat < 4) {
+          if (!wait(cflag, k, nbat + 1)) return;
+          eload(nbat);
+        }
+        bool have_next = nbat < 4;
 #pragma unroll 1
-        for (int cb = 0; cb < 4; ++cb) {
+        for (int cb = nbat; cb < 4; ++cb) {
           double* E = cs.E2[cb & 1];
           if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
-          if (cb > 0 && !have_next) {
+          if (!have_next) {
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
           }
