@@ -266,7 +266,7 @@ __device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0,
 // starts once all of Linv_kk is published (chain flag) and waits for w_k (state(k,k) == k + 1, the end of POTRF(k))
 // only before the rhs update, so the L tile is not held back by POTRF's forward solve.  False: the launch aborted.
 __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __restrict__ rhs, int nrhs,
-                        double* __restrict__ Linv, double* smem, const int* state, int* abortw, DevCtrl* ctrl,
+                        double* __restrict__ Linv, double* smem, int* state, int* rhscnt, int* abortw, DevCtrl* ctrl,
                         int* s_ok, const QFold& qf) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   double* Pi = smem;
@@ -322,8 +322,18 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
         mA.st(row * ld + col, acc[mi][t][r]);
         Pi[row * DF_SP + col] = acc[mi][t][r];
       }
-  if (tid == 0) *s_ok = df_wait(state, df_tri(k, k), k + 1, abortw, ctrl);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the w_k loads behind the poll
+  // L_ik is published before the rhs update: its consumers (the updates of row i and column i) start a rhs update
+  // earlier.  The rhs updates of block row i stay in panel order through rhscnt[i] (applied TRSM(i, .) updates):
+  // this one waits for w_k and for rhscnt[i] == k, and the chain's staging of block i waits for rhscnt[i] == i - 1.
+  df_drain();
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(state + df_tri(i, k), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int v0 = df_poll(state + df_tri(k, k)), v1 = df_poll(rhscnt + i);
+    *s_ok = (v0 >= k + 1 || df_wait(state, df_tri(k, k), k + 1, abortw, ctrl)) &&
+            (v1 >= k || df_wait(rhscnt, i, k, abortw, ctrl));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the w_k and rhs loads behind the polls
   __syncthreads();
   if (!*s_ok) return false;
   double* wk = Pj;  // [64][nrhs]
@@ -336,6 +346,9 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
     for (int c = 0; c < NB; ++c) s = fma(Pi[row * DF_SP + c], wk[c * nrhs + rho], s);
     mR.st(t, mR.ld(t) - s);
   }
+  df_drain();
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(rhscnt + i, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
 
@@ -401,6 +414,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   int* abortw = work + 1;
   int* state = work + 64;  // own cache lines
   int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published (0..4)
+  int* rhscnt = cflag + nblk;  // rhscnt[i]: worker TRSM(i, .) rhs updates applied to rhs block i (in panel order)
   const int tid = threadIdx.x;
   const QFold qf{Hq, dq, nq, Hq ? ctrl->reg : 0.0};
   // Roles by residency, not by blockIdx: the first two workgroups to start run the chain.  Workgroups are not
@@ -456,10 +470,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         // A_b,k and D_b with every panel < k applied (state >= k), and the rhs block b with all earlier TRSM
         // updates: one wait for both states, then every load in flight together (minus L_b,k w_k inside POTRF(b);
         // POTRF(b-2) of this workgroup is done with ps.B)
-        if (tid == 0) {  // (both polls in flight together: usually the second input is final when the first is)
-          const int v0 = df_poll(state + df_tri(b, k)), v1 = df_poll(state + df_tri(b, b));
+        if (tid == 0) {  // (the polls in flight together: usually the other inputs are final when the first is)
+          const int v0 = df_poll(state + df_tri(b, k)), v1 = df_poll(state + df_tri(b, b)), v2 = df_poll(rhscnt + b);
           s_ok = (v0 >= k || df_wait(state, df_tri(b, k), k, abortw, ctrl)) &&
-                 (v1 >= k || df_wait(state, df_tri(b, b), k, abortw, ctrl));
+                 (v1 >= k || df_wait(state, df_tri(b, b), k, abortw, ctrl)) &&
+                 (v2 >= k || df_wait(rhscnt, b, k, abortw, ctrl));  // the rhs block has TRSM(b, j < k)'s updates
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
@@ -696,7 +711,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     if (!s_ok) break;
     int done_idx, done_val = k + 1;
     if (type == 1) {
-      if (!df_trsm(L, ld, i, k, rhs, nrhs, Linv, smem, state, abortw, ctrl, &s_ok, qf)) break;
+      if (!df_trsm(L, ld, i, k, rhs, nrhs, Linv, smem, state, rhscnt, abortw, ctrl, &s_ok, qf)) break;
       done_idx = df_tri(i, k);
     } else if (type == 3) {
       df_update4(L, ld, i, j, k, smem, qf);
@@ -718,9 +733,9 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   }
 }
 
-// work: [0] counter, [1] abort word, [64 ..) one state word per lower tile, then one chain flag per diagonal
-// block; zeroed before every launch.
-size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + nblk; }
+// work: [0] counter, [1] abort word, [2] role ticket, [64 ..) one state word per lower tile, then one chain flag and
+// one rhs counter per diagonal block; zeroed before every launch.
+size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + 2 * (size_t)nblk; }
 
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
