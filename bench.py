@@ -387,15 +387,21 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
                 "flops_per_launch": flops_syrk, "avg_launch_ms": syrk}
     comb_ach = tf(flops_syrk + flops_chol, syrk + chol)
     tr, tr_src = trace_roofline() if wl == "C3" else (None, None)
-    if tr is not None:
-        assembly["frac_trace"] = tr["assembly_frac"]
-        trailing["frac_trace"] = tr["cholesky_frac"]
+    # the same fractions recomputed from a COMMITTED rocprofv3 kernel trace of this command (not this run): a
+    # cross-check of the event timing, labelled with its source so it is never mistaken for a live measurement
+    committed = None if tr is None else {
+        "source": tr_src, "note": "kernel-trace durations of a committed profile of `bench.py --steps 20 --warmup 5 "
+        "--no-cpu-baseline`, not measured by this run", "combined_frac": tr["combined_frac"],
+        "assembly_frac": tr["assembly_frac"], "cholesky_frac": tr["cholesky_frac"]}
     both = (traffic + chol_traffic) if (traffic is not None and chol_traffic is not None) else None
     # "% MFMA roofline on trailing SYRK" = (assembly SYRK + POTRF trailing flops) / (their kernel time)
     roofline = {"bound": "mfma", "kernel": "assembly SYRK + Cholesky (SURVEY.md §8d: the SYRK-type flops of the "
                 "assembly and of the POTRF trailing updates over the two phases' kernel time)",
                 "achieved": comb_ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": frac(comb_ach),
-                "frac_trace": tr["combined_frac"] if tr is not None else None, "trace_source": tr_src,
+                "frac_definition": "combined: (assembly SYRK + Cholesky) flops / (their HIP-event kernel time) / peak "
+                                   "(since round 4; round 1-3 lines carried the assembly SYRK alone, now in "
+                                   "roofline.assembly)",
+                "committed_trace": committed,
                 "traffic": both, "traffic_unit": "bytes/step (assembly + factorization, PMC)",
                 "flops_per_launch": flops_syrk + flops_chol, "avg_launch_ms": syrk + chol,
                 "assembly": assembly, "trailing": trailing}
@@ -427,6 +433,14 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     return out, gathered
 
 
+def _hist(v):
+    """{value: count} of a list of ints, keys as strings (JSON)."""
+    out = {}
+    for x in v:
+        out[str(x)] = out.get(str(x), 0) + 1
+    return dict(sorted(out.items(), key=lambda kv: int(kv[0])))
+
+
 def run_full_solve(args):
     """--workload C3FULL ("steady state over a full barrier solve"): one complete C3 barrier solve from
     x0 with the reference's standard parameters (SolverParams.scala:35-46: maxIter 1000 per centering), the t-loop of
@@ -450,7 +464,8 @@ def run_full_solve(args):
         eng.set_x(spec["x0"])
         t, steps, per_center, hist = 1.0, 0, [], {}
         reg = fb = full = 0
-        ph_sum, ph_n = np.zeros(8), 0
+        small_piv = []  # regularized steps: the row block where the first attempt stopped (0: it ran to the end)
+        ph_sum, ph_cnt = np.zeros(8), np.zeros(8)  # per phase: summed ms over its occurrences, occurrences
         if timed:
             eng.set_timing(True, all_phases=True)
         torch.cuda.synchronize()
@@ -464,11 +479,14 @@ def run_full_solve(args):
                 steps += 1
                 hist[st.ruiz_sweeps] = hist.get(st.ruiz_sweeps, 0) + 1
                 reg += st.regularized
+                if st.regularized:
+                    small_piv.append(int(st.small_pivot))
                 fb += int(st.fallback != 0)
                 full += int(st.took_step == 1 and st.step == 1.0)
                 if timed and steps % 50 == 0:  # the timer ring holds 63 steps: read and restart it
-                    ph_sum += eng.phase_times() * 50
-                    ph_n += 50
+                    ms, cnt = eng.phase_stats()
+                    ph_sum += ms * cnt
+                    ph_cnt += cnt
                     eng.set_timing(True, all_phases=True)
                 if st.done:
                     break
@@ -479,19 +497,22 @@ def run_full_solve(args):
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         if timed:
-            rest = steps - ph_n
-            if rest > 0:
-                ph_sum += eng.phase_times() * rest
-                ph_n += rest
+            ms, cnt = eng.phase_stats()
+            ph_sum += ms * cnt
+            ph_cnt += cnt
             eng.set_timing(False)
+        # per step: a phase's total time over the solve / the steps (the inline assembly runs on few steps); per
+        # occurrence: its mean duration when it runs
         return dict(elapsed=el, steps=steps, per_center=per_center, hist=hist, reg=reg, fb=fb, full=full,
-                    phases=(ph_sum / max(ph_n, 1)).tolist(), x=eng.get_x())
+                    phases=(ph_sum / max(steps, 1)).tolist(),
+                    phases_occ=(ph_sum / np.maximum(ph_cnt, 1)).tolist(), occ=ph_cnt.tolist(), x=eng.get_x(),
+                    small_piv=small_piv)
 
     a = solve(False)
     b = solve(True)
     eng.close()
     same = bool(np.array_equal(a["x"], b["x"]))
-    ph = b["phases"]
+    ph, po = b["phases"], b["phases_occ"]
     out = {"metric": METRIC, "value": a["steps"] / a["elapsed"], "unit": "Newton KKT solves/s", "n_gpus": 1,
            "steps": a["steps"], "warmup": 0, "ms_per_step": a["elapsed"] / a["steps"] * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
@@ -502,8 +523,15 @@ def run_full_solve(args):
            "solve_s": a["elapsed"], "centerings": len(a["per_center"]), "steps_per_centering": a["per_center"],
            "ruiz_sweep_histogram": {str(k): v for k, v in sorted(a["hist"].items())},
            "regularized_refactorizations": a["reg"], "fallbacks": a["fb"], "line_search_full_steps": a["full"],
-           "phases_ms_timed_solve": {"assembly_prefetched": ph[5], "assembly_inline": ph[0], "ruiz": ph[1],
-                                     "cholesky_fused_fwd": ph[2], "bwd_solve_residual": ph[3], "line_search": ph[4]},
+           "phases_ms_per_step_timed_solve": {"assembly_prefetched": ph[5], "assembly_inline": ph[0], "ruiz": ph[1],
+                                              "cholesky_fused_fwd": ph[2], "bwd_solve_residual": ph[3],
+                                              "line_search": ph[4]},
+           "phases_ms_per_occurrence_timed_solve": {"assembly_prefetched": po[5], "assembly_inline": po[0],
+                                                    "ruiz": po[1], "cholesky_fused_fwd": po[2],
+                                                    "bwd_solve_residual": po[3], "line_search": po[4]},
+           "phase_occurrences_timed_solve": {"assembly_prefetched": b["occ"][5], "assembly_inline": b["occ"][0],
+                                             "cholesky_fused_fwd": b["occ"][2]},
+           "first_attempt_stop_rows": _hist(a["small_piv"]),
            "timed_solve_s": b["elapsed"], "timed_solve_same_x": same}
     return out
 

@@ -42,7 +42,8 @@ class cvxg_step_info(C.Structure):
                 ("norm_grad_new", C.c_double), ("equality_gap", C.c_double),
                 ("backtracks_c", C.c_int), ("backtracks_armijo", C.c_int), ("fallback", C.c_int),
                 ("ruiz_sweeps", C.c_int), ("regularized", C.c_int), ("took_step", C.c_int), ("done", C.c_int),
-                ("iter", C.c_int), ("ls_fresh", C.c_int), ("ls_ties", C.c_int)]
+                ("iter", C.c_int), ("ls_fresh", C.c_int), ("ls_ties", C.c_int),
+                ("small_pivot", C.c_int)]
 
 
 class cvxg_centering_info(C.Structure):
@@ -109,6 +110,7 @@ SIGNATURES = {
     "cvxg_affine_map": (C.c_int, [_P, _D, _D]),
     "cvxg_set_timing": (C.c_int, [_P, C.c_int]),
     "cvxg_get_phase_times": (C.c_int, [_P, _D, C.c_int]),
+    "cvxg_get_phase_stats": (C.c_int, [_P, _D, C.POINTER(C.c_int), C.c_int]),
     "cvxg_chol_schedule": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_uint), C.c_int]),
     "cvxg_set_ruiz_lookahead": (C.c_int, [_P, C.c_int, C.POINTER(C.c_longlong)]),
 }

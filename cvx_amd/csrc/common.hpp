@@ -30,6 +30,9 @@ struct DevCtrl {
   double sc[40];                  // reduced scalars, see SC_* below
   int spec_infeasible;            // the speculative evaluation at x + s (k_ls_setup_eval): its infeasible / not_strict
   int spec_not_strict;
+  int small_piv;                  // k_chol_dataflow with early_min > 0 (regularizedCholesky's first attempt): 1-based
+                                  // first row of the 16-column block where it stopped on min diag(L) <= early_min
+                                  // (min_diag holds that block's value); 0 = it did not stop
 };
 
 enum {

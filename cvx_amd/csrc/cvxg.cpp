@@ -108,6 +108,8 @@ struct cvxg_ctx {
   // Sparse constraint rows (<= SPARSE_NNZ nonzeros: bounds, phase-I bound rows, box rows).  Their Hessian
   // terms are per-entry sums (k_sparse_hess); only the dense rows, packed into As, go through the SYRK.
   int sparse_rows = 1;          // CVXG_SPARSE_ROWS=0 disables the split (A/B)
+  int early_abort = 1;          // regularizedCholesky's first attempt stops at min diag(L) <= 1e-7 (CVXG_EARLY_ABORT=0: off)
+  int small_piv = 0;            // the last first attempt's stop row (DevCtrl::small_piv)
   int have_sparse = 0;          // set_ineq found sparse rows: the SYRK runs over As / wd / mdp
   int ndense = 0, mdp = 0;      // dense rows, padded to MPAD (>= MPAD)
   double *As = nullptr, *wd = nullptr;
@@ -194,7 +196,7 @@ struct cvxg_ctx {
 // helpers
 // ------------------------------------------------------------------------------------------------
 static int set_err(cvxg_ctx* ctx, int code, const char* fmt, ...) {
-  char buf[512];
+  char buf[1024];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof(buf), fmt, ap);
@@ -769,8 +771,11 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   fill_rhs();
   // the whole factorization as one persistent launch over the 64 x 64 tile DAG (k_dataflow.hip); Q = (d d') o H
   // (+ reg I) is formed as each tile is first read (no separate k_form_q pass)
+  // the first attempt (reg = 0) stops at the first block with min diag(L) <= 1e-7: its factor would be discarded
+  // anyway (MatrixUtils.scala:458-460 refactors Q + 1e-10 I), so only the retry's L is ever used
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
-                       ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending);
+                       ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending,
+                       (reg == 0.0 && ctx->early_abort) ? 1e-7 : 0.0);
   ctx->spec_launched = false;
   after();
   HIPC(ctx, hipGetLastError());
@@ -823,6 +828,7 @@ template <class F, class G>
 static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regularized, double* mind, G after) {
   CHK(factor_attempt(ctx, 0.0, nrhs, fill_rhs, after));
   *regularized = 0;
+  ctx->small_piv = ctx->hctrl->small_piv;  // where the first attempt stopped on min diag(L) <= 1e-7 (0: it did not)
   if (ctx->hctrl->chol_info == 0 && min_diag_of(*ctx->hctrl) > 1e-7) {
     *mind = min_diag_of(*ctx->hctrl);
     return CVXG_OK;
@@ -891,6 +897,7 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
   info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
   if (info->ruiz_sweeps >= 0) ruiz_learn(ctx, info->ruiz_sweeps);
   info->regularized = reg;
+  info->small_pivot = reg ? ctx->small_piv : 0;
   info->min_diag = mind;
   if (rc != CVXG_OK) return rc;
   const double nb = ctx->normGrad;
@@ -1094,6 +1101,7 @@ static int kkt_solve_pd(cvxg_ctx* ctx, const double* qv, const double* bv, doubl
   tstop(ctx, 2);
   info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
   info->regularized = reg;
+  info->small_pivot = reg ? ctx->small_piv : 0;
   info->min_diag = mind;
   if (rc != CVXG_OK) return rc;
   tstart(ctx, 3);
@@ -1472,6 +1480,8 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
   if (it == 100) return set_err(ctx, CVXG_E_LINESEARCH, "Line search: backtracking into the set C failed.");
   *k_c = it;
   // while (objF.valueAt(x + s*t) > f + alpha*t*q && it < limit) { t *= beta; it += 1 }
+  double last_fv = 0.0, last_thr = 0.0;  // (diagnostics of a failed search)
+  const int ties0 = *ties;
   while (it < limit) {
     CHK(ensure(it));
     const int j = it - b.k0;
@@ -1492,11 +1502,18 @@ static int line_search(cvxg_ctx* ctx, const cvxg_params* pars, double q, int lim
     }
     if (npos > 0)
       return set_err(ctx, CVXG_E_INFEASIBLE_X, "barrierFunction: x not strictly feasible in line search");
+    last_fv = fv;
+    last_thr = thr;
     if (!(fv > thr)) break;
     tcur *= beta;
     ++it;
   }
-  if (it == 100) return set_err(ctx, CVXG_E_LINESEARCH, "Line search: sufficient decrease not reached");
+  if (it == 100)
+    return set_err(ctx, CVXG_E_LINESEARCH,
+                   "Line search: sufficient decrease not reached (barrier t = %.17g, inner iteration %d, f = %.17g, "
+                   "q = %.17g, %d halvings into C, last trial step %.17g: f(x + s t) = %.17g > f + alpha t q = %.17g; "
+                   "%d of the Armijo decisions inside the rounding band of f)",
+                   tb, ctx->iter, f, q, *k_c, tcur / beta, last_fv, last_thr, *ties - ties0);
   *k_a = it - *k_c;
   *t_out = tcur;
   return CVXG_OK;
@@ -1608,6 +1625,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   const int slots = 2 * std::max(ncu, 1);
   ctx->slots = slots;
   if (const char* e = getenv("CVXG_SPARSE_ROWS")) ctx->sparse_rows = atoi(e) != 0;
+  if (const char* e = getenv("CVXG_EARLY_ABORT")) ctx->early_abort = atoi(e) != 0;
   // the fused forward solve carries the KKT columns only on small problems: at C3 (64 blocks) the many-column solves
   // cost less than the 9-column chain (C3EQ8: 204.5 vs 191.5 solves/s)
   ctx->kkt_fused_rhs = ctx->nblk < 8 ? MAX_RHS : 1;
@@ -2306,7 +2324,9 @@ int cvxg_set_timing(cvxg_ctx* ctx, int enabled) {
   return CVXG_OK;
 }
 
-int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count) {
+int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count) { return cvxg_get_phase_stats(ctx, ms, nullptr, count); }
+
+int cvxg_get_phase_stats(cvxg_ctx* ctx, double* ms, int* occurrences, int count) {
   if (!ctx || !ms) return CVXG_E_ARG;
   HIPC(ctx, hipSetDevice(ctx->dev));
   HIPC(ctx, hipStreamSynchronize(ctx->s));
@@ -2325,6 +2345,7 @@ int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count) {
     }
     // per recorded occurrence: the first step after cvxg_set_timing may run an assembly prefetched before timing was on
     ms[i] = got > 0 ? sum / got : 0.0;
+    if (occurrences) occurrences[i] = got;
   }
   (void)hipGetLastError();  // never leave a timing error sticky for the next launch check
   return CVXG_OK;

@@ -402,7 +402,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
                                                           int* __restrict__ work, const unsigned* __restrict__ tasks,
                                                           int ntasks, int nblk, unsigned long long* __restrict__ trace,
                                                           const double* __restrict__ Hq, const double* __restrict__ dq,
-                                                          int nq, int ruiz_gate) {
+                                                          int nq, int ruiz_gate, double early_min) {
   // the Ruiz loop launched ahead of the factorization without a host read may still be open (k_ruiz_final: -1): then
   // the launch is void and the host finishes the loop and factors again
   if (ruiz_gate && ctrl->ruiz_sweeps < 0) return;
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         potrf64w_reset(ps);
         __syncthreads();
       }  // b > 0: reset behind the staging, the tile's LDS stores behind publish()'s barrier
-      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix)) {
+      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
@@ -740,10 +740,10 @@ size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1)
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace, bool zero_work, const double* Hq, const double* dq, int nq,
-                          bool ruiz_gate) {
+                          bool ruiz_gate, double early_min) {
   if (zero_work) (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
   k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq,
-                                      ruiz_gate ? 1 : 0);
+                                      ruiz_gate ? 1 : 0, early_min);
 }
 
 }  // namespace cvxg

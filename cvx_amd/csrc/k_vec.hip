@@ -804,45 +804,38 @@ void launch_klp_eval(hipStream_t s, const double* x, int n, int np, double nd, d
 
 // KL primal objective at the LS_TRIALS trial points xt = x + s*t_k (t_k = tbase beta^k by repeated products, as the
 // host's backtracking; x + s*t with two roundings, as Breeze's x + s*t): per trial {sum_j xt_j log(xt_j n),
-// sum_j |xt_j log(xt_j n)| + |xt_j|}; per-block partials, then a fixed-order sum over the blocks.  A trial outside
-// the domain (some xt_j <= 0) gives a NaN / -inf sum; the backtracking into C has rejected it before Armijo reads it.
-__global__ __launch_bounds__(256) void k_ls_klp(const double* __restrict__ x, const double* __restrict__ sdir, int n,
-                                                double nd, double tbase, double beta, double* __restrict__ part) {
-  __shared__ double sred[2][4][LS_TRIALS];
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const bool valid = j < n;
-  const double xj = valid ? x[j] : 0.0, sj = valid ? sdir[j] : 0.0;
+// sum_j |xt_j log(xt_j n)| + |xt_j|}.  One 1024-thread block per trial, and the value sum is formed exactly as the
+// objective at x is (k_dots' DOT_FMA over x and log(n x): fma(xt_j, log(xt_j n), acc) per thread over j = tid +
+// 1024 i, then block_sum), so a trial point equal to x gives bitwise the f(x) the Armijo test compares with -- as in
+// the reference, where both sides are objF.valueAt (EqualityConstrainedSolver.scala:52, 88).  (A different summation
+// order left f(x + s t) a few ulps of t f0 above f(x) at every small t: late in the path, where one ulp of f exceeds
+// the decrease alpha t q, no trial could pass and the line search threw at it == 100.)  A trial outside the domain
+// (some xt_j <= 0) gives a NaN / -inf sum; the backtracking into C has rejected it before Armijo reads it.
+__global__ __launch_bounds__(1024) void k_ls_klp(const double* __restrict__ x, const double* __restrict__ sdir, int n,
+                                                 double nd, double tbase, double beta, double* __restrict__ out) {
+  __shared__ double red[16];
+  const int k = blockIdx.x;
   double t = tbase;
-  for (int k = 0; k < LS_TRIALS; ++k) {
-    double v = 0.0, a = 0.0;
-    if (valid) {
-      const double st = sj * t;
-      const double xt = xj + st;
-      const double l = log(xt * nd);
-      v = xt * l;
-      a = fabs(v) + fabs(xt);
-    }
-    const double sv = wave_sum(v), sa = wave_sum(a);
-    if (lane == 0) {
-      sred[0][wid][k] = sv;
-      sred[1][wid][k] = sa;
-    }
-    t *= beta;
+  for (int q = 0; q < k; ++q) t *= beta;
+  double v = 0.0, a = 0.0;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {  // (j >= n: x = s = 0 adds exact zeros to the dot at x)
+    const double xt = x[j] + sdir[j] * t;
+    const double l = log(xt * nd);
+    v = fma(xt, l, v);
+    a += fabs(xt * l) + fabs(xt);
   }
-  __syncthreads();
-  if (threadIdx.x < 2 * LS_TRIALS) {
-    const int q = threadIdx.x / LS_TRIALS, k = threadIdx.x % LS_TRIALS;
-    part[(size_t)blockIdx.x * 2 * LS_TRIALS + q * LS_TRIALS + k] =
-        ((sred[q][0][k] + sred[q][1][k]) + sred[q][2][k]) + sred[q][3][k];
+  v = block_sum(v, red);
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) {
+    out[k] = v;
+    out[LS_TRIALS + k] = a;
   }
 }
 int ls_klp_blocks(int n) { return (n + 255) / 256; }
 void launch_ls_klp(hipStream_t s, const double* x, const double* sdir, int n, double nd, double tbase, double beta,
                    double* part, double* out) {
-  const int nb = ls_klp_blocks(n);
-  k_ls_klp<<<nb, 256, 0, s>>>(x, sdir, n, nd, tbase, beta, part);
-  k_sum_chunks<<<1, 2 * LS_TRIALS, 0, s>>>(part, nb, 2 * LS_TRIALS, out);
+  (void)part;
+  k_ls_klp<<<LS_TRIALS, 1024, 0, s>>>(x, sdir, n, nd, tbase, beta, out);
 }
 
 // KL dual at z (v = B'z given): y_j = R exp(-v_j) for j < nout (Dist_KL.scala:163, 170), 0 on the padding
@@ -909,6 +902,7 @@ __global__ void k_factor_prep(DevCtrl* ctrl, double reg, int* __restrict__ work,
   if (i < nwork) work[i] = 0;
   if (i == 0) {
     ctrl->reg = reg;
+    ctrl->small_piv = 0;
     ctrl->chol_info = 0;
     ctrl->df_status = 0;
     ctrl->min_diag = (unsigned long long)__double_as_longlong(__builtin_inf());

@@ -139,7 +139,9 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                                                         formed as each tile is first read; L is then output only */,
                           const double* dq = nullptr, int nq = 0,
                           bool ruiz_gate = false /* true: every workgroup leaves at once when ctrl->ruiz_sweeps < 0
-                                                    (a short Ruiz lookahead, cvxg.cpp: factor_attempt) */);
+                                                    (a short Ruiz lookahead, cvxg.cpp: factor_attempt) */,
+                          double early_min = 0.0 /* > 0: stop (abort word, min_diag and small_piv set) at the first
+                                                    16-column block whose min diag(L) <= early_min */);
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
 size_t bwd_work_ints(int nblk);  // flag words + the data-tagged u granules of k_bwd_dataflow
 // Optional epilogue (nrhs = 1): dx = d :* u; with s, also s = dx and x1 = x + s (the speculative line search's

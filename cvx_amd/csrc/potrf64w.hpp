@@ -126,7 +126,7 @@ __device__ __forceinline__ void p64w_Xdiag(Potrf64wSmem& sm, int kb, int lane) {
 // wave 0: eliminate D_kb (S diagonal block kb, all panels < kb applied) -> L16 into S, L16^-T into ET[kb].
 // Returns false on a non-positive pivot (chol_info recorded).
 __device__ __forceinline__ bool p64w_eliminate(Potrf64wSmem& sm, int kb, int base, DevCtrl* ctrl, double& mind,
-                                               int lane) {
+                                               int lane, double early_min) {
   const int o = 16 * kb, r = lane & 15;
   double a[16];
   {
@@ -161,7 +161,8 @@ __device__ __forceinline__ bool p64w_eliminate(Potrf64wSmem& sm, int kb, int bas
 #pragma unroll
     for (int c = j + 1; c < 16; ++c) a[c] = fma(-t, lc[c], a[c]);
   }
-  mind = fmin(mind, pmin * rsqrt_nr(pmin));
+  const double bmin = pmin * rsqrt_nr(pmin);  // this block's min diag(L) (the value min_diag would take)
+  mind = fmin(mind, bmin);
   // L~16 (lanes 0-15) and L~16^-T (lanes 16-31) without their column scales; lanes 0-15 publish s_r = p_r^-1/2 (the
   // consumers scale: p64w_T, p64w_X, p64w_Xdiag)
   if (lane < 16) sm.SV[kb][r] = rsqrt_nr(mypiv);
@@ -177,6 +178,16 @@ __device__ __forceinline__ bool p64w_eliminate(Potrf64wSmem& sm, int kb, int bas
   }
   if (firstbad >= 0) {
     if (lane == 0) atomicCAS(&ctrl->chol_info, 0, base + o + firstbad + 1);
+    return false;
+  }
+  // regularizedCholesky's first attempt (MatrixUtils.scala:458-460): once some diag(L) <= 1e-7 the factor is discarded
+  // and chol(Q + 1e-10 I) taken instead, so the rest of this factorization cannot matter -- stop here.  The test is on
+  // the same value min_diag accumulates, so the host's decision (min_diag <= 1e-7) is the one the full attempt gives.
+  if (early_min > 0.0 && !(bmin > early_min)) {
+    if (lane == 0) {
+      atomic_min_pos(&ctrl->min_diag, bmin);
+      atomicCAS(&ctrl->small_piv, 0, base + o + 1);
+    }
     return false;
   }
   return true;
@@ -230,7 +241,7 @@ __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int
 template <class M, class Fix = NoFix>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
-                                                Fix fix = Fix()) {
+                                                Fix fix = Fix(), double early_min = 0.0) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -240,7 +251,7 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
 #pragma unroll 1
     for (int kb = 0; kb < 4 && ok; ++kb) {
       P64_STAMP(1 + 4 * kb);
-      ok = p64w_eliminate(sm, kb, base, ctrl, mind, lane);
+      ok = p64w_eliminate(sm, kb, base, ctrl, mind, lane, early_min);
       P64_STAMP(2 + 4 * kb);
       if (!ok) {
         if (lane == 0) __hip_atomic_store(&sm.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

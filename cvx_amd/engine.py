@@ -266,10 +266,16 @@ class Engine:
         return self.lib.cvxg_last_error(self.h).decode()
 
     def phase_times(self) -> np.ndarray:
-        """cvxg_get_phase_times: per-step mean device time (ms) of each phase since set_timing(True)."""
+        """cvxg_get_phase_times: per phase, the mean device time (ms) over the steps since set_timing(True) that
+        recorded it (a per-occurrence mean: a phase not every step runs is not averaged over the steps)."""
+        return self.phase_stats()[0]
+
+    def phase_stats(self):
+        """cvxg_get_phase_stats: (per-occurrence mean ms, occurrence count) per phase since set_timing(True)."""
         ms = np.zeros(8)
-        self._check(self.lib.cvxg_get_phase_times(self.h, _dp(ms), 8))
-        return ms
+        cnt = (C.c_int * 8)()
+        self._check(self.lib.cvxg_get_phase_stats(self.h, _dp(ms), cnt, 8))
+        return ms, np.array(list(cnt), dtype=np.int64)
 
 
 def batch_barrier_solve(engines, pars, termination: int = 0):

@@ -75,6 +75,9 @@ typedef struct cvxg_step_info {
   int iter;                 /* inner iteration index */
   int ls_fresh;             /* line-search feasibility trials evaluated fresh (margin inside the rounding band) */
   int ls_ties;              /* Armijo decisions inside the rounding band of the barrier value (rounding noise) */
+  int small_pivot;          /* regularized: 1-based first row of the 16-column block where the first attempt stopped
+                               on min diag(L) <= 1e-7 (MatrixUtils.scala:458-460); 0 = it ran to the end (a failed
+                               pivot, or not regularized) */
 } cvxg_step_info;
 
 /* UnconstrainedSolver / EqualityConstrainedSolver result (Solution.scala:32-43). */
@@ -292,6 +295,9 @@ int cvxg_affine_map(cvxg_ctx* dst, const double* u, double* x);
  * phases ([0], [2], [5]) -- every event record leaves the GPU idle a few microseconds between kernels. */
 int cvxg_set_timing(cvxg_ctx* ctx, int enabled);
 int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count);
+/* cvxg_get_phase_times plus, per phase, the number of recorded occurrences its mean is over (occurrences may be NULL):
+ * a phase that not every step runs (the inline assembly [0]) is then weighted by its occurrences, not by steps. */
+int cvxg_get_phase_stats(cvxg_ctx* ctx, double* ms, int* occurrences, int count);
 
 /* The Newton step's Ruiz lookahead (cholesky_solve, MatrixUtils.scala:240-268 as restated in k_vec.hip): the next
  * step first launches `sweeps` Ruiz sweeps (the last step's count + 1 by default, RUIZ_MAX = 20 on a fresh

@@ -79,14 +79,15 @@ static void fill_params(JNIEnv* env, jdoubleArray jp, jint maxIter, cvxg_params*
   p->delta = v[5];
 }
 
-/* cvxg_step_info as a double[22] (CvxgNative.StepInfo in INTEGRATION.md §2 reads it by these indices). */
-#define STEP_INFO_LEN 22
+/* cvxg_step_info as a double[23] (CvxgNative.StepInfo in INTEGRATION.md §2 reads it by these indices). */
+#define STEP_INFO_LEN 23
 static void step_info_row(const cvxg_step_info* s, double* o) {
   const double v[STEP_INFO_LEN] = {s->t, s->f, s->norm_grad, s->q, s->newton_decrement, s->hnorm, s->trust_radius,
                                    s->step, s->rel_err, s->min_diag, s->norm_grad_new, s->equality_gap,
                                    (double)s->backtracks_c, (double)s->backtracks_armijo, (double)s->fallback,
                                    (double)s->ruiz_sweeps, (double)s->regularized, (double)s->took_step,
-                                   (double)s->done, (double)s->iter, (double)s->ls_fresh, (double)s->ls_ties};
+                                   (double)s->done, (double)s->iter, (double)s->ls_fresh, (double)s->ls_ties,
+                                   (double)s->small_pivot};
   for (int i = 0; i < STEP_INFO_LEN; ++i) o[i] = v[i];
 }
 static void put_step_info(JNIEnv* env, jdoubleArray out, const cvxg_step_info* s) {
@@ -283,7 +284,7 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_activeSet(JNIEnv* env, jclass cls
 
 /* ---- the hot path: one Newton direction, one inner iteration, one centering ------------------------------ */
 
-/* newtonDirection(h, maxIter, params[6], t, x, grad (nullable), dx, w (nullable), info[22] (nullable)) */
+/* newtonDirection(h, maxIter, params[6], t, x, grad (nullable), dx, w (nullable), info[23] (nullable)) */
 JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_newtonDirection(JNIEnv* env, jclass cls, jlong h, jint maxIter,
                                                                jdoubleArray jp, jdouble t, jdoubleArray x,
                                                                jdoubleArray grad, jdoubleArray dx, jdoubleArray w,
@@ -325,7 +326,7 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_centeringResume(JNIEnv* env, jcla
   return rc;
 }
 
-/* newtonStep(h, maxIter, params[6], info[22]): one inner iteration on the device-resident iterate
+/* newtonStep(h, maxIter, params[6], info[23]): one inner iteration on the device-resident iterate
  * (UnconstrainedSolver.scala:47-134 / EqualityConstrainedSolver.scala:60-111); info[18] = done */
 JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_newtonStep(JNIEnv* env, jclass cls, jlong h, jint maxIter,
                                                           jdoubleArray jp, jdoubleArray info) {
@@ -410,8 +411,8 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_batchBarrierSolve(JNIEnv* env, jc
   return rc;
 }
 
-/* batchNewtonStep(handles[k], maxIter, params[6], info[22 k], status[k]): one inner Newton iteration on each of k
- * independent contexts concurrently (cvxg_batch_newton_step); context i's cvxg_step_info at info[22 i ..] */
+/* batchNewtonStep(handles[k], maxIter, params[6], info[23 k], status[k]): one inner Newton iteration on each of k
+ * independent contexts concurrently (cvxg_batch_newton_step); context i's cvxg_step_info at info[23 i ..] */
 JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_batchNewtonStep(JNIEnv* env, jclass cls, jlongArray handles,
                                                                jint maxIter, jdoubleArray jp, jdoubleArray info,
                                                                jintArray status) {

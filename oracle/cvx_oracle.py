@@ -265,12 +265,19 @@ def barrier_hessian(pb: Problem, t: float, x: np.ndarray, literal: bool = True) 
 
     ``literal=True`` keeps every temporary of the reference (G*G.t, /(d*d), zeros, /d, two sums) —
     that is the CPU-baseline cost model.  ``literal=False`` drops only the +zeros/d term, which adds
-    exact zeros (bit-identical result for d > 0).
+    exact zeros (bit-identical result for d > 0), and updates a linear row's G*G.t/(d*d) only on the
+    row's support: every entry outside it would receive (G_p G_q)/(d*d) = +-0.0, which leaves a finite
+    sum bitwise unchanged (0.0 + -0.0 = 0.0), so the result is the dense fold's, bit for bit
+    (``tests/test_oracle_known_answers.py::test_support_fold_is_the_dense_fold``).  It makes the fold
+    O(sum of squared row supports): the KL primal's positivity rows and phase-I rows touch 1-2 entries.
     """
     if isinstance(pb, AffineView):  # BarrierSolver.scala:229-230 — (F.t * self.hessianBarrierFunction(t, z0 + F u)) * F
         return (pb.F.T @ barrier_hessian(pb.pb, t, pb.x_of(x), literal)) @ pb.F
     if literal == "blas":
         return _barrier_hessian_blas(pb, t, x)
+    if literal is False:
+        return _barrier_hessian_support(pb, t, x)
+    literal = literal is True  # "dense": the literal=False fold over whole n x n outer products
     n = pb.n
     s = objective_hessian(pb, x) * t
     for i in range(pb.m):
@@ -287,6 +294,27 @@ def barrier_hessian(pb: Problem, t: float, x: np.ndarray, literal: bool = True) 
             s = s + GGt / (d * d) + Hc / d
         else:
             s = s + GGt / (d * d)
+    return s
+
+
+def _barrier_hessian_support(pb: Problem, t: float, x: np.ndarray) -> np.ndarray:
+    """barrier_hessian(literal=False) restricted to each linear row's support (see there): bitwise the same fold."""
+    s = np.array(objective_hessian(pb, x) * t, dtype=np.float64, copy=True)
+    for i in range(pb.m):
+        d = pb.ub[i] - constraint_value(pb, i, x)
+        if d <= 0:
+            raise NotStrictlyFeasible(f"hessianBarrierFunction: x not strictly feasible, d = {d}")
+        G = constraint_gradient(pb, i, x)
+        Hq = constraint_hessian(pb, i)
+        if Hq is not None:
+            s = s + np.outer(G, G) / (d * d) + Hq / d
+            continue
+        sup = np.flatnonzero(G)
+        if sup.size == 0:
+            continue
+        Gs = G[sup]
+        blk = np.ix_(sup, sup)
+        s[blk] = s[blk] + np.outer(Gs, Gs) / (d * d)
     return s
 
 

@@ -10,9 +10,11 @@ def main(path, blocks=(2, 3, 10, 30, 50, 61)):
     raw = open(path, "rb").read()
     nq, nb = (int(v) for v in np.frombuffer(raw[:8], dtype=np.int32))
     order = np.frombuffer(raw[8:8 + 4 * nq], dtype=np.uint32)
-    n = nq + 6 * nb
+    # chain records per block, from the file size (k_dataflow.hip writes 3: POTRF(k), the staging of k+1, the fix hook)
+    R = ((len(raw) - 8 - 4 * nq) // 32 - nq) // nb
+    n = nq + R * nb
     tr = np.frombuffer(raw[8 + 4 * nq:8 + 4 * nq + 32 * n], dtype=np.uint64).reshape(n, 4).astype(np.int64)
-    ch = tr[nq:].reshape(nb, 6, 4)
+    ch = tr[nq:].reshape(nb, R, 4)
     t0 = ch[0, 0, 0]
     us = lambda v: (v - t0) / 100.0
     per = (ch[nb - 1, 0, 0] - ch[1, 0, 0]) / 100.0 / (nb - 2)

@@ -1,8 +1,8 @@
 """Analyse a dataflow-Cholesky task timeline written with CVXG_DF_TRACE=<file> (k_dataflow.hip).
 
-File: int32 ntasks, int32 nblk, uint32 order[ntasks] (encoded queue tasks), uint64 trace[ntasks + 6 nblk][4]
-= {claim, ready, done, wg} in s_memrealtime ticks (100 MHz) for the worker tasks; the last 6 nblk records hold the
-chain workgroups' stamps.  Prints per-type durations of the worker tasks and the
+File: int32 ntasks, int32 nblk, uint32 order[ntasks] (encoded queue tasks), uint64 trace[ntasks + 3 nblk][4]
+= {claim, ready, done, wg} in s_memrealtime ticks (100 MHz) for the worker tasks; the last 3 nblk records hold the
+chain workgroups' stamps (cvxg.cpp writes 4 (ntasks + 3 nblk) words).  Prints per-type durations of the worker tasks and the
 fraction of workgroup time spent busy / waiting (the chain's stamps: scripts/chain_offsets.py).
 """
 import sys

@@ -1445,6 +1445,45 @@ def test_regularized_cholesky_retry_branch(mods):
     assert np.linalg.norm(dx - dref) <= 64 * u * (w[-1] / w[0]) * np.linalg.norm(dref)
 
 
+def test_regularized_first_attempt_stops_early(mods, monkeypatch):
+    """regularizedCholesky (MatrixUtils.scala:452-461) discards chol(Q) as soon as min diag(L) <= 1e-7 and factors
+    Q + 1e-10 I, so the engine stops its first attempt at the first 16-column block with such a pivot
+    (k_chol_dataflow's early_min) instead of running it to the end.  A mid-matrix small pivot -- columns 300 and 301 of
+    A nearly parallel, n = 600 (10 Cholesky blocks) -- stops it in the block of rows 289..304 (small_pivot = 289);
+    with the stop disabled (CVXG_EARLY_ABORT=0) the attempt runs to the end (small_pivot = 0).  Both give bitwise the
+    same dx, min diag(L) and regularization flag (the oracle's), and a whole Newton step from there the same x."""
+    Z, SP, Engine, O = mods
+    n, m = 600, 1200
+    rng = np.random.default_rng(11)
+    A = rng.uniform(-1, 1, (m, n))
+    A[:, 301] = A[:, 300] * (1 + 1e-7 * rng.uniform(-1, 1, m))
+    spec = dict(a0=rng.uniform(-1, 1, n), r0=0.0, P=None, A=A, r=np.zeros(m), ub=rng.uniform(0.1, 0.2, m),
+                Aeq=None, beq=None)
+    pb = _opb(O, spec)
+    x = np.zeros(n)
+    pars = SP.standardParams()
+    g = O.barrier_gradient(pb, 1.0, x)
+    rec = O.NewtonStepRecord(x=x, grad=g, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
+    O.newton_direction(pb, 1.0, x, g, pars.tolEqSolve, rec)
+    assert rec.regularized == 1 and rec.fallback == 0
+    out = {}
+    for early in ("1", "0"):
+        monkeypatch.setenv("CVXG_EARLY_ABORT", early)
+        eng = _engine(Engine, spec)
+        dx, _, info = eng.newton_direction(pars, 1.0, x, grad=g)
+        eng.set_x(x)
+        eng.centering_begin(1.0)
+        st = eng.newton_step(pars)
+        out[early] = (dx, info.regularized, info.min_diag, info.small_pivot, st.small_pivot, st.step, eng.get_x())
+        eng.close()
+    a, b = out["1"], out["0"]
+    print(f"early stop at row {a[3]} (full attempt: {b[3]}), min diag(L) {a[2]:.3e}, oracle {np.min(rec.diagL):.3e}")
+    assert a[3] == 289 and a[4] == 289 and b[3] == 0 and b[4] == 0
+    assert np.array_equal(a[0], b[0]) and a[1] == b[1] == 1 and a[2] == b[2] and a[5] == b[5]
+    assert np.array_equal(a[6], b[6])
+    assert abs(a[2] - np.min(rec.diagL)) <= 1e-6 * np.min(rec.diagL)
+
+
 def test_batch_barrier_solve_matches_single_contexts(mods):
     """cvxg_batch_barrier_solve / cvxg_batch_newton_step (config C5 from one host process, one thread per context):
     three independent instances solved concurrently give bitwise the x, step counts and gaps of three one-at-a-time
@@ -1541,9 +1580,13 @@ def test_batch_full_size_contexts_share_one_gpu(mods):
 def test_full_c3_solve_standard_params(mods):
     """A complete C3 barrier solve with the reference's standard parameters (SolverParams.scala:35-46: maxIter 1000
     per centering, tolSolver 1e-8) on the GPU -- the t-loop of BarrierSolver.scala:70-117 from x0 at t = 1 until
-    m / t < 1e-8 -- once alone and once through cvxg_batch_barrier_solve beside an n = 600 instance on the same GPU:
-    the two runs give bitwise the same x, step count and gap (config C5's independence), the gap meets the criterion,
-    x is strictly feasible and the objective is the lowest of the path's centred points."""
+    m / t < 1e-8 -- once alone, driven centering by centering from the host (cvxg_centering per t, as the reference's
+    t-loop calls its inner solver), and once through cvxg_batch_barrier_solve beside an n = 600 instance on the same
+    GPU: the two runs give bitwise the same x, step count and gap (config C5's independence), the gap meets the
+    criterion, x is strictly feasible and its objective is below the starting point's.  The per-centering step counts
+    follow the documented pattern: the centerings at t <= 1e9 converge (fewer than maxIter steps) and
+    the C3 solve's last three (t = 1e10 .. 1e12, where Armijo's decrease is below one ulp of f) run to maxIter = 1000
+    (maxedOut); the counts sum to the solve's Newton steps."""
     Z, SP, Engine, O = mods
     from cvx_amd.engine import batch_barrier_solve
     pars = SP.standardParams()
@@ -1552,10 +1595,20 @@ def test_full_c3_solve_standard_params(mods):
     for spec in specs:
         e = _engine(Engine, spec)
         e.set_x(spec["x0"])
+        m = spec["A"].shape[0]
+        t, per, maxed = 1.0, [], []
         t0 = time.perf_counter()
-        s = e.barrier_solve(pars, 0)
+        while True:  # BarrierSolver.scala:70-117 with CvxUtils.standardTerminationCriterion
+            ci = e.centering(pars, t)
+            per.append(ci.iter)
+            maxed.append(ci.maxed_out)
+            if m / t < pars.tolSolver:
+                break
+            t *= 10.0
         dt = time.perf_counter() - t0
-        ref.append((e.get_x(), s.newton_steps, s.outer_iters, s.duality_gap, s.objective, dt))
+        x = e.get_x()
+        obj = float(spec["a0"] @ x + 0.5 * x @ spec["P"] @ x + spec["r0"])
+        ref.append((x, sum(per), len(per), m / t, obj, dt, per, maxed))
         e.close()
     engs = [_engine(Engine, spec) for spec in specs]
     for e, spec in zip(engs, specs):
@@ -1563,7 +1616,7 @@ def test_full_c3_solve_standard_params(mods):
     sols, st = batch_barrier_solve(engs, pars, 0)
     assert st == [0, 0], [e.last_error() for e in engs]
     for i, (e, s) in enumerate(zip(engs, sols)):
-        x, steps, outer, gap, obj, dt = ref[i]
+        x, steps, outer, gap, obj, dt, per, maxed = ref[i]
         assert np.array_equal(e.get_x(), x), i
         assert (s.newton_steps, s.outer_iters, s.duality_gap) == (steps, outer, gap), i
         assert gap < pars.tolSolver and outer == 13, (gap, outer)
@@ -1572,8 +1625,12 @@ def test_full_c3_solve_standard_params(mods):
         assert np.all(d > 0), "the solution is strictly feasible"
         f0 = float(spec["a0"] @ spec["x0"] + 0.5 * spec["x0"] @ spec["P"] @ spec["x0"] + spec["r0"])
         assert obj < f0
-        print(f"instance {i} (n={spec['a0'].shape[0]}): {steps} Newton steps in {outer} centerings, gap {gap:.2e}, "
-              f"objective {obj:.12e}, single-context solve {dt:.2f} s ({steps / dt:.1f} steps/s), min slack {d.min():.2e}")
+        assert all(k < pars.maxIter and not mo for k, mo in zip(per[:10], maxed[:10])), per
+        if i == 0:  # C3: the last three centerings hit maxIter
+            assert per[10:] == [pars.maxIter] * 3 and all(maxed[10:]), per
+        print(f"instance {i} (n={spec['a0'].shape[0]}): {steps} Newton steps in {outer} centerings {per}, gap "
+              f"{gap:.2e}, objective {obj:.12e}, single-context solve {dt:.2f} s ({steps / dt:.1f} steps/s), min "
+              f"slack {d.min():.2e}")
     for e in engs:
         e.close()
 

@@ -344,3 +344,33 @@ def test_reduced_barrier_matches_kkt_path_many_equalities():
     xr = view.x_of(sol.x)
     assert np.linalg.norm(xr - sol_kkt.x) / np.linalg.norm(sol_kkt.x) < 1e-8
     assert np.abs(spec["Aeq"] @ xr - spec["beq"]).max() < 1e-12
+
+
+@pytest.mark.parametrize("case", ["kl_1", "kl_2", "qp", "phase_I", "quad"])
+def test_support_fold_is_the_dense_fold(case):
+    """The oracle's Hessian fold (BarrierSolver.scala:303-315) updates a linear row's G G'/(d d) only on the row's
+    support: every other entry would receive +-0.0, which leaves the sum's bits unchanged.  Bitwise (as int64) the
+    dense fold over whole n x n outer products, on the KL primal rows, a random QP, its phase-I problem (dense rows plus
+    a -1 column) and a problem with QuadraticConstraint rows (dense update kept for those)."""
+    if case in ("kl_1", "kl_2"):
+        spec = Z.kl_primal_spec(40, case)
+        pb = O.Problem(a0=spec["a0"], A=spec["A"], r=spec["r"], ub=spec["ub"], Aeq=spec["Aeq"], beq=spec["beq"],
+                       klp_n=40)
+        xs = [spec["x0"]]
+    elif case == "quad":
+        spec = Z.random_qp_quad(12, 20, 3, instance=5)
+        pb = O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"],
+                       qrows=spec["qrows"], qP=spec["qP"])
+        xs = [spec["x0"]]
+    else:
+        spec = Z.random_qp(30, 60, instance=3)
+        pb = O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"])
+        xs = [spec["x0"]]
+        if case == "phase_I":
+            pb, fp = O.phase_I_problem(pb, np.zeros(30))
+            xs = [fp]
+    for x in xs:
+        for t in (1.0, 1e4, 1e12):
+            a = O.barrier_hessian(pb, t, x, literal=False)
+            b = O.barrier_hessian(pb, t, x, literal="dense")
+            assert np.array_equal(a.view(np.int64), b.view(np.int64)), (case, t)
