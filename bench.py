@@ -344,6 +344,8 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
         ph = [ph[i] if i in (0, 2, 5) else ph_all[i] for i in range(len(ph))]
     record(ph)
     eng.set_timing(False)
+    # (the late-path state is the default C3 instance's: instance 0, n = 4096, m = 8192)
+    steady = steady_state(eng, pars, sync) if (wl == "C3" and rank == 0 and (n, m) == (4096, 8192)) else None
 
     stats = np.array([rank, steps, elapsed, t_final], dtype=np.float64)
     gathered = D.gather_results(x_final, stats, device)
@@ -428,6 +430,7 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
         "cholesky_tflops": tf(n ** 3 / 3, chol),
         "ruiz_lookahead_reruns": ruiz_reruns,
         "ls_full_steps": full_steps,
+        "steady_state": steady,
         "gathered_ranks": len(gathered),
     }
     return out, gathered
@@ -439,6 +442,45 @@ def _hist(v):
     for x in v:
         out[str(x)] = out.get(str(x), 0) + 1
     return dict(sorted(out.items(), key=lambda kv: int(kv[0])))
+
+
+LATE_FIXTURE = os.path.join(ROOT, "tests", "golden", "big", "C3late_n4096_m8192.npz")
+
+
+def steady_state(eng, pars, sync, t_late=1e11, steps=50, detail=10):
+    """The late path, where a full C3 solve spends 96 % of its Newton steps (t = 1e10 .. 1e12, three centerings that
+    run to maxIter; bench_c3full): `steps` Newton steps of the centering at t = 1e11 from the engine's own iterate
+    entering it (the committed state of tests/golden/big/C3late_n4096_m8192.npz, recorded by scripts/c3_late_states.py),
+    wall-clocked like the headline window, then `detail` more with every phase timed.  A side figure: `value` stays the
+    t = 1 window.  None when the fixture is absent."""
+    try:
+        fx = np.load(LATE_FIXTURE)
+        k = [i for i in range(fx["t"].shape[0]) if float(fx["t"][i]) == t_late and int(fx["it_n"][i]) == 0][0]
+        x = np.array(fx["x"][k])
+    except (OSError, IndexError, KeyError):
+        return None
+    eng.set_x(x)
+    eng.centering_begin(t_late)
+    eng.newton_step(pars)  # (the first step: its assembly is not prefetched)
+    sync()
+    t0 = time.perf_counter()
+    reg = 0
+    for _ in range(steps):
+        st = eng.newton_step(pars)
+        reg += st.regularized
+    sync()
+    el = time.perf_counter() - t0
+    eng.set_timing(True, all_phases=True)
+    for _ in range(detail):
+        reg += eng.newton_step(pars).regularized
+    ms, cnt = eng.phase_stats()
+    eng.set_timing(False)
+    return {"t": t_late, "steps": steps, "steps_per_s": steps / el, "ms_per_step": el / steps * 1e3,
+            "regularized_steps": reg, "x_source": os.path.relpath(LATE_FIXTURE, ROOT) + f" (state {k})",
+            "phases_ms": {"syrk": float(ms[5]), "ruiz": float(ms[1]), "cholesky_fused_fwd": float(ms[2]),
+                          "bwd_solve_residual": float(ms[3]), "line_search": float(ms[4])},
+            "note": "late-path window (t = 1e11 centering, which runs to maxIter in a full solve); value is the t = 1 "
+                    "window"}
 
 
 def run_full_solve(args):

@@ -27,7 +27,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     # reference evaluates as separate Breeze operations (x + s*t, d*d, t*(a + Px) + ...) keep its roundings;
     # the dot products and MFMA accumulations use explicit fma / MFMA builtins.
     cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall",
-           "-Wno-pass-failed", "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + [
+           "-Wno-pass-failed", "-Wl,-z,defs", "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + [
         "-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)

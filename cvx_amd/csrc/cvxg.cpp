@@ -109,7 +109,13 @@ struct cvxg_ctx {
   // terms are per-entry sums (k_sparse_hess); only the dense rows, packed into As, go through the SYRK.
   int sparse_rows = 1;          // CVXG_SPARSE_ROWS=0 disables the split (A/B)
   int early_abort = 1;          // regularizedCholesky's first attempt stops at min diag(L) <= 1e-7 (CVXG_EARLY_ABORT=0: off)
-  int small_piv = 0;            // the last first attempt's stop row (DevCtrl::small_piv)
+  // The Newton-step assembly with p == 0 stores H's lower triangle (and its diagonal tiles whole) only: Ruiz, the
+  // Cholesky and the residual (a lower-triangle symv) read nothing else; consumers of the full matrix (eigen fallback,
+  // KKT paths, cvxg_barrier_eval, the primal-dual solver) mirror it first (ensure_h_full).  CVXG_H_LOWER=0: always mirror
+  int h_lower = 1;
+  bool h_full = true;           // the current H holds its upper triangle too
+  double* hsv_part = nullptr;   // symv partials (nblk x np)
+  int small_piv = 0;            // the last first attempt's stop row (DevCtrl::small_piv, or chol_info)
   int have_sparse = 0;          // set_ineq found sparse rows: the SYRK runs over As / wd / mdp
   int ndense = 0, mdp = 0;      // dense rows, padded to MPAD (>= MPAD)
   double *As = nullptr, *wd = nullptr;
@@ -541,7 +547,10 @@ static void constraint_eval_all(cvxg_ctx* ctx) {
 
 // Barrier value / gradient pieces at the current x and ctrl->t (BarrierSolver.scala:280-301):
 // c, d, w, invd, logd, Px, y, eqDiff, and sc[A0X, XPX, SUMLOG, GG, EQ2].
-static int assemble_hessian(cvxg_ctx* ctx, const double* wts, const double* qw, hipStream_t st);
+static int assemble_hessian(cvxg_ctx* ctx, const double* wts, const double* qw, hipStream_t st, bool full);
+constexpr int ROWDOT_BESIDE_WG = 64;
+// the Newton step's assembly: lower-only when nothing but Ruiz, the Cholesky and the symv residual reads H
+static bool step_h_full(const cvxg_ctx* ctx) { return !(ctx->p == 0 && ctx->h_lower); }
 // The setup sweep of a speculative line search also evaluates the constraints at x + dx (k_ls_setup_eval): linear
 // rows, certified line search.
 static bool spec_eval_ok(const cvxg_ctx* ctx) {
@@ -576,7 +585,7 @@ static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false, b
     if (!taken) HIPC(ctx, hipEventRecord(ctx->ev_w, s));
     const int nx = (ctx->tm.tick + (ahead ? 1 : 0)) % TRING;  // timed as phase 5 of the step that will use it
     if (ctx->tm.on) HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][0], s));
-    CHK(assemble_hessian(ctx, nullptr, nullptr, s));
+    CHK(assemble_hessian(ctx, nullptr, nullptr, s, step_h_full(ctx)));
     if (ctx->tm.on) {
       HIPC(ctx, hipEventRecord(ctx->tm.ev[nx][5][1], s));
       ctx->tm.rec[nx][5] = true;
@@ -591,7 +600,9 @@ static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false, b
   const bool quad = ctx->hasP && !ctx->kl;
   const bool cert = ls_certified(ctx);
   if (quad) {
-    if (cert) launch_rowdot_abs(s, ctx->P, np, np, np, ctx->x, ctx->Px, ctx->Pxa);
+    // beside the prefetched assembly (s2) on a bounded grid: 64 workgroups loop over the rows instead of 512 queueing
+    // for the SYRK's CU slots (the same sums, bitwise)
+    if (cert) launch_rowdot_abs(s, ctx->P, np, np, np, ctx->x, ctx->Px, ctx->Pxa, prefetch ? ROWDOT_BESIDE_WG : 0);
     else launch_rowdot(s, ctx->P, np, np, np, ctx->x, ctx->Px);
   }
   if (ctx->kl) {  // v = B'z, y = R exp(-v), -B y (the KL dual gradient is w - B y), sum_j y_j
@@ -668,7 +679,7 @@ static double objective_at_x(cvxg_ctx* ctx) { return objective_from_ctrl(ctx, *c
 // ctx->w = 1/d^2 and qw = 1/d for the barrier Hessian (BarrierSolver.scala:314), or the primal-dual KKT weights
 // lambda/d and qw = lambda (kktMatrix_noEqs, PrimalDualSolver.scala:226-238; then ctrl->t = 1).
 static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr, const double* qw = nullptr,
-                            hipStream_t st = nullptr) {
+                            hipStream_t st = nullptr, bool full = true) {
   const bool own = st == nullptr;  // on ctx->s (timed here as phase 5); otherwise the prefetch on s2 (timed there)
   if (own) st = ctx->s;
   if (own) tstart(ctx, 5);
@@ -699,11 +710,12 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr, const do
   const double* Pd = ctx->klp ? ctx->klp_hd : nullptr;  // the KL primal's diag(1/x) * t
   if (ctx->ntiles_main > 0)
     launch_syrk_assemble(st, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
-                         TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->spart, Pd);
+                         TileList{ctx->tiles, ctx->ntiles_main}, 1, ctx->spart, Pd, full);
   if (ctx->ntiles > ctx->ntiles_main)
     launch_syrk_assemble(st, A, ctx->np, w, rows, P, ctx->ctrl, ctx->H, ctx->np,
                          TileList{ctx->tiles + ctx->ntiles_main, ctx->ntiles - ctx->ntiles_main}, ctx->nsplit,
-                         ctx->spart, Pd);
+                         ctx->spart, Pd, full);
+  ctx->h_full = full;
   if (ctx->have_sparse)
     launch_sparse_hess(st, ctx->sp_ptr, ctx->sp_pq, ctx->sp_row, ctx->sp_coef, wsrc, ctx->sp_T, ctx->H, ctx->np);
   if (ctx->nq > 0)  // + hessianAt/d = P_k / d_k  (BarrierSolver.scala:314), or grad2_gi * l_i (PrimalDualSolver.scala:236)
@@ -828,7 +840,8 @@ template <class F, class G>
 static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regularized, double* mind, G after) {
   CHK(factor_attempt(ctx, 0.0, nrhs, fill_rhs, after));
   *regularized = 0;
-  ctx->small_piv = ctx->hctrl->small_piv;  // where the first attempt stopped on min diag(L) <= 1e-7 (0: it did not)
+  // where the first attempt stopped: its non-positive pivot, or the block where min diag(L) <= 1e-7 (0: it did not)
+  ctx->small_piv = ctx->hctrl->small_piv ? ctx->hctrl->small_piv : ctx->hctrl->chol_info;
   if (ctx->hctrl->chol_info == 0 && min_diag_of(*ctx->hctrl) > 1e-7) {
     *mind = min_diag_of(*ctx->hctrl);
     return CVXG_OK;
@@ -877,7 +890,8 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
     }
     backward_solve(ctx, 1, epi);
     // relativeSize(H*x - b, b, tol), b = -grad  (MatrixUtils.scala:437-442, 496)
-    launch_rowdot_add(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->dx, ctx->y, ctx->vtmp);  // H x + grad = H x - b
+    if (ctx->h_full) launch_rowdot_add(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->dx, ctx->y, ctx->vtmp);  // H x + grad
+    else launch_symv_lower_add(s, ctx->H, ctx->np, ctx->n, ctx->dx, ctx->y, ctx->vtmp, ctx->hsv_part);
     DotBatch db{};
     db.add(DOT_FMA, ctx->vtmp, nullptr, ctx->n, SC_RES2);
     db.add(DOT_FMA, ctx->dx, ctx->y, ctx->np, SC_Q);
@@ -967,6 +981,13 @@ static int sym_solve(cvxg_ctx* ctx, const double* Mat, int n2, const double* bde
   return CVXG_OK;
 }
 
+// The full symmetric H for a consumer that reads its upper triangle (after a lower-only assembly).
+static void ensure_h_full(cvxg_ctx* ctx) {
+  if (ctx->h_full) return;
+  launch_mirror_lower(ctx->s, ctx->H, ctx->np, ctx->n);
+  ctx->h_full = true;
+}
+
 // UnconstrainedSolver Newton direction with its fallback chain (UnconstrainedSolver.scala:54-67).
 static int newton_direction_p0(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* info) {
   int rc = cholesky_solve(ctx, pars->tolEqSolve, info);
@@ -984,6 +1005,7 @@ static int newton_direction_p0(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step
   ctx->spec_have = false;  // (the speculative line-search setup belonged to a rejected direction)
   ctx->spec_eval_have = false;
   // symSolve(H, -y) (UnconstrainedSolver.scala:64)
+  ensure_h_full(ctx);
   CHK(eig_alloc(ctx));
   HIPC(ctx, hipMemsetAsync(ctx->eig_b, 0, (size_t)ctx->eig_ldm * sizeof(double), ctx->s));
   launch_axpy(ctx->s, ctx->eig_b, ctx->y, -1.0, ctx->n, ctx->eig_b);
@@ -1182,7 +1204,7 @@ static int newton_direction(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_in
   if (ctx->h_valid && ctx->x_eval_valid) {  // assembled on s2 behind this x's evaluation (s already waits on it)
   } else {
     tstart(ctx, 0);
-    CHK(assemble_hessian(ctx));
+    CHK(assemble_hessian(ctx, nullptr, nullptr, nullptr, step_h_full(ctx)));
     tstop(ctx, 0);
   }
   ctx->h_valid = false;
@@ -1626,6 +1648,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   ctx->slots = slots;
   if (const char* e = getenv("CVXG_SPARSE_ROWS")) ctx->sparse_rows = atoi(e) != 0;
   if (const char* e = getenv("CVXG_EARLY_ABORT")) ctx->early_abort = atoi(e) != 0;
+  if (const char* e = getenv("CVXG_H_LOWER")) ctx->h_lower = atoi(e) != 0;
   // the fused forward solve carries the KKT columns only on small problems: at C3 (64 blocks) the many-column solves
   // cost less than the 9-column chain (C3EQ8: 204.5 vs 191.5 solves/s)
   ctx->kkt_fused_rhs = ctx->nblk < 8 ? MAX_RHS : 1;
@@ -1640,6 +1663,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   if (ctx->nsplit > 1)
     part = std::max(part, (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE);
   CHK(dalloc(ctx, &ctx->part, part));
+  CHK(dalloc(ctx, &ctx->hsv_part, (size_t)ctx->nblk * np));
   CHK(dalloc(ctx, &ctx->spart,
              ctx->nsplit > 1 ? (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE : (size_t)1));
   HIPC(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
@@ -1676,7 +1700,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
   void* ptrs[] = {ctx->P, ctx->a0, ctx->A, ctx->r, ctx->ub, ctx->Aeq, ctx->beq, ctx->x, ctx->y, ctx->dx, ctx->sdir,
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
-                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
+                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
                   ctx->ls_log, ctx->ls_pcnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,

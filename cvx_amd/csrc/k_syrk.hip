@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk_direct(const double* __restrict
                                                         double* __restrict__ H, int ldh,
                                                         const int* __restrict__ tiles, int ntiles, int nsplit,
                                                         double* __restrict__ partials,
-                                                        const double* __restrict__ Pd) {
+                                                        const double* __restrict__ Pd, int mirror) {
   const int tile = blockIdx.x, split = blockIdx.y;
   const int ij = tiles[tile];
   const int I = ij >> 16, J = ij & 0xffff;
@@ -114,15 +114,16 @@ __global__ __launch_bounds__(256, 2) void k_syrk_direct(const double* __restrict
         const int gi = I * TILE + li, gj = J * TILE + lj;
         const double v = (P ? P[(size_t)gi * ldh + gj] * t : (Pd && gi == gj ? Pd[gi] * t : 0.0)) + acc[mi][nj][r];
         H[(size_t)gi * ldh + gj] = v;
-        if (gi != gj) H[(size_t)gj * ldh + gi] = v;
+        if (gi != gj && (mirror || diag)) H[(size_t)gj * ldh + gi] = v;
       }
 }
 
-// Split-K reduce: H = t*P + sum_splits partial (fixed split order), lower entries mirrored.
+// Split-K reduce: H = t*P + sum_splits partial (fixed split order), lower entries mirrored (all, or those of diagonal
+// tiles only).
 __global__ __launch_bounds__(TILE) void k_syrk_reduce(const double* __restrict__ partials, int ntiles, int nsplit,
                                                       const int* __restrict__ tiles, const double* __restrict__ P,
                                                       const DevCtrl* ctrl, double* __restrict__ H, int ldh,
-                                                      const double* __restrict__ Pd) {
+                                                      const double* __restrict__ Pd, int mirror) {
   const int tile = blockIdx.x, li = blockIdx.y, lj = threadIdx.x;
   const int ij = tiles[tile];
   const int I = ij >> 16, J = ij & 0xffff;
@@ -132,17 +133,18 @@ __global__ __launch_bounds__(TILE) void k_syrk_reduce(const double* __restrict__
   const int gi = I * TILE + li, gj = J * TILE + lj;
   const double v = (P ? P[(size_t)gi * ldh + gj] * ctrl->t : (Pd && gi == gj ? Pd[gi] * ctrl->t : 0.0)) + s;
   H[(size_t)gi * ldh + gj] = v;
-  if (gi != gj) H[(size_t)gj * ldh + gi] = v;
+  if (gi != gj && (mirror || I == J)) H[(size_t)gj * ldh + gi] = v;
 }
 
 void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double* w, int mp, const double* P,
                           const DevCtrl* ctrl, double* H, int ldh, TileList tiles, int nsplit, double* partials,
-                          const double* Pd) {
+                          const double* Pd, bool mirror) {
   dim3 grid(tiles.count, nsplit);
-  k_syrk_direct<4><<<grid, 256, 0, s>>>(A, lda, w, mp, P, ctrl, H, ldh, tiles.ij, tiles.count, nsplit, partials, Pd);
+  k_syrk_direct<4><<<grid, 256, 0, s>>>(A, lda, w, mp, P, ctrl, H, ldh, tiles.ij, tiles.count, nsplit, partials, Pd,
+                                        mirror ? 1 : 0);
   if (nsplit > 1) {
     dim3 g2(tiles.count, TILE);
-    k_syrk_reduce<<<g2, TILE, 0, s>>>(partials, tiles.count, nsplit, tiles.ij, P, ctrl, H, ldh, Pd);
+    k_syrk_reduce<<<g2, TILE, 0, s>>>(partials, tiles.count, nsplit, tiles.ij, P, ctrl, H, ldh, Pd, mirror ? 1 : 0);
   }
 }
 

@@ -120,17 +120,18 @@ __global__ __launch_bounds__(256) void k_rowdot(const double* __restrict__ M, in
                                                 const double* __restrict__ v, const double* __restrict__ add,
                                                 double* __restrict__ y, double* __restrict__ yabs) {
   const int lane = threadIdx.x & 63;
-  const int row = 2 * (blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (row >= rows) return;
-  const bool two = row + 1 < rows;
-  double dot[2], adot[2];
-  row_dot2_wave<ABS>(M + (size_t)row * ld, M + (size_t)(two ? row + 1 : row) * ld, two, v, cols, lane, dot, adot);
-  if (lane == 0) {
+  // one wave per row pair; a grid smaller than the pairs loops (the same per-row sums: bitwise the full grid)
+  for (int row = 2 * (blockIdx.x * 4 + (threadIdx.x >> 6)); row < rows; row += 2 * 4 * gridDim.x) {
+    const bool two = row + 1 < rows;
+    double dot[2], adot[2];
+    row_dot2_wave<ABS>(M + (size_t)row * ld, M + (size_t)(two ? row + 1 : row) * ld, two, v, cols, lane, dot, adot);
+    if (lane == 0) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (q == 1 && !two) break;
-      y[row + q] = add ? dot[q] + add[row + q] : dot[q];
-      if (ABS) yabs[row + q] = adot[q];
+      for (int q = 0; q < 2; ++q) {
+        if (q == 1 && !two) break;
+        y[row + q] = add ? dot[q] + add[row + q] : dot[q];
+        if (ABS) yabs[row + q] = adot[q];
+      }
     }
   }
 }
@@ -144,8 +145,116 @@ void launch_rowdot_add(hipStream_t s, const double* M, int ld, int rows, int col
   k_rowdot<false><<<rowdot_grid(rows), 256, 0, s>>>(M, ld, rows, cols, v, add, y, nullptr);
 }
 void launch_rowdot_abs(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y,
-                       double* yabs) {
-  k_rowdot<true><<<rowdot_grid(rows), 256, 0, s>>>(M, ld, rows, cols, v, nullptr, y, yabs);
+                       double* yabs, int max_wg) {
+  const int g = rowdot_grid(rows);
+  k_rowdot<true><<<(max_wg > 0 && max_wg < g) ? max_wg : g, 256, 0, s>>>(M, ld, rows, cols, v, nullptr, y, yabs);
+}
+
+// y = H v + add from the LOWER triangle of the symmetric H alone (the assembly leaves the strictly-upper part of its
+// off-diagonal tiles unwritten, cvxg.cpp: assemble_hessian), in two fixed-order passes like the Ruiz sweep:
+// tile (I, J), J <= I, of 64 x 64 writes
+//   S[J][i] = sum_{j in J} H_ij v_j   for its rows i in I      (row partials; a diagonal tile: its whole rows, the
+//                                                               assembly writes both triangles of diagonal tiles)
+//   S[I][j] = sum_{i in I} H_ij v_i   for its columns j in J   (I > J: the rows of the upper tile H_JI = H_IJ')
+// and k_symv_rows adds S[0..nbn)[r] in order, then add[r].  Deterministic; half the bytes of the full-row sweep.
+__global__ __launch_bounds__(256) void k_symv_tiles(const double* __restrict__ H, int ld, int nbn,
+                                                    const double* __restrict__ v, double* __restrict__ S) {
+  const int t = blockIdx.x;
+  int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  while (I * (I + 1) / 2 > t) --I;
+  const int J = t - I * (I + 1) / 2;
+  __shared__ double cred[4][NB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int c2 = tid & 31, g = tid >> 5;  // column pair 2*c2, row group g: rows g + 8q
+  const double* tile = H + (size_t)I * NB * ld + (size_t)J * NB;
+  vd2 h[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) h[q] = *reinterpret_cast<const vd2*>(tile + (size_t)(g + 8 * q) * ld + 2 * c2);
+  const vd2 vj = *reinterpret_cast<const vd2*>(v + J * NB + 2 * c2);
+  vd2 csum = {0.0, 0.0};
+  double rs[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const double vi = v[I * NB + g + 8 * q];
+    rs[q] = fma(h[q][1], vj[1], h[q][0] * vj[0]);
+    csum = __builtin_elementwise_fma(h[q], vd2{vi, vi}, csum);
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    double x = rs[q];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    rs[q] = x;
+  }
+  if (c2 == 0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) S[(size_t)J * (nbn * NB) + I * NB + g + 8 * q] = rs[q];
+  }
+  if (I == J) return;
+  csum[0] += __shfl_xor(csum[0], 32, 64);
+  csum[1] += __shfl_xor(csum[1], 32, 64);
+  if (lane < 32) {
+    cred[wid][2 * c2] = csum[0];
+    cred[wid][2 * c2 + 1] = csum[1];
+  }
+  __syncthreads();
+  if (tid < NB) S[(size_t)I * (nbn * NB) + J * NB + tid] = ((cred[0][tid] + cred[1][tid]) + cred[2][tid]) + cred[3][tid];
+}
+__global__ __launch_bounds__(256) void k_symv_rows(const double* __restrict__ S, int nbn, int n,
+                                                   const double* __restrict__ add, double* __restrict__ y) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int row = blockIdx.x * 64 + lane;
+  const int ldS = nbn * NB;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (row < n) {
+    int X = q;
+    for (; X + 12 < nbn; X += 16) {
+      s0 += S[(size_t)X * ldS + row];
+      s1 += S[(size_t)(X + 4) * ldS + row];
+      s2 += S[(size_t)(X + 8) * ldS + row];
+      s3 += S[(size_t)(X + 12) * ldS + row];
+    }
+    for (; X < nbn; X += 4) s0 += S[(size_t)X * ldS + row];
+  }
+  red[q][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (q == 0 && row < n) {
+    const double hv = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    y[row] = add ? hv + add[row] : hv;
+  }
+}
+void launch_symv_lower_add(hipStream_t s, const double* H, int ld, int n, const double* v, const double* add,
+                           double* y, double* S) {
+  const int nbn = (n + NB - 1) / NB;
+  k_symv_tiles<<<nbn * (nbn + 1) / 2, 256, 0, s>>>(H, ld, nbn, v, S);
+  k_symv_rows<<<(n + 63) / 64, 256, 0, s>>>(S, nbn, n, add, y);
+}
+
+// H_ji = H_ij for i > j (the full symmetric matrix from its lower triangle): 64 x 64 tiles (I, J), I > J, each
+// transposed through LDS.
+__global__ __launch_bounds__(256) void k_mirror_lower(double* __restrict__ H, int ld, int nbn) {
+  const int t = blockIdx.x;
+  int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  while (I * (I + 1) / 2 > t) --I;
+  const int J = t - I * (I + 1) / 2;
+  __shared__ double tl[NB][NB + 1];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < NB * NB; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    if (I != J || c < r) tl[r][c] = H[(size_t)(I * NB + r) * ld + J * NB + c];
+  }
+  __syncthreads();
+  for (int e = tid; e < NB * NB; e += 256) {
+    const int r = e >> 6, c = e & 63;  // H[J*NB + r][I*NB + c] = H[I*NB + c][J*NB + r]
+    if (I != J || r < c) H[(size_t)(J * NB + r) * ld + I * NB + c] = tl[c][r];
+  }
+}
+void launch_mirror_lower(hipStream_t s, double* H, int ld, int n) {
+  const int nbn = (n + NB - 1) / NB;
+  k_mirror_lower<<<nbn * (nbn + 1) / 2, 256, 0, s>>>(H, ld, nbn);
 }
 
 // The line search's setup sweep over A for s = dx (e = A s, eabs = |A| |s|) fused with the next step's constraint
@@ -735,43 +844,37 @@ void launch_ls_trials(hipStream_t s, const double* c, const double* e, const dou
 
 // KL dual objective along the trial steps: per trial k, sum_j R exp(-(v_j + t_k u_j)) (v = B'z, u = B's),
 // the vec_R dot exp(-B'(z + s t)) term of Dist_KL.dualObjFAt (Dist_KL.scala:146-147); t_k by repeated products.
+// One 1024-thread block per trial, summed exactly as sum_j y_j at z is (k_sum over the noutp entries of k_kl_eval's y:
+// per thread j = tid + 1024 i, then block_sum), so a trial whose exponents equal z's gives that sum bitwise (k_ls_klp).
 // With vabs / uabs (= |B'||z|, |B'||s|; certified mode) also its error scale against any evaluation order of
 // B'(z + s t): sum_j y_j (gamma (vabs_j + t_k uabs_j) + 4u) (the exponent's error propagated through exp).
-__global__ __launch_bounds__(256) void k_ls_kl(const double* __restrict__ v, const double* __restrict__ u, int nout,
-                                               double R, double tbase, double beta, double* __restrict__ part,
-                                               const double* __restrict__ vabs, const double* __restrict__ uabs,
-                                               double gamma) {
+__global__ __launch_bounds__(1024) void k_ls_kl(const double* __restrict__ v, const double* __restrict__ u, int nout,
+                                                double R, double tbase, double beta, double* __restrict__ out,
+                                                const double* __restrict__ vabs, const double* __restrict__ uabs,
+                                                double gamma) {
   constexpr double U = 1.1102230246251565e-16;  // 2^-53
-  __shared__ double sred[2][4][LS_TRIALS];
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const bool valid = j < nout;
-  const double vj = valid ? v[j] : 0.0, uj = valid ? u[j] : 0.0;
-  const double va = (valid && vabs) ? vabs[j] : 0.0, ua = (valid && uabs) ? uabs[j] : 0.0;
+  __shared__ double red[16];
+  const int k = blockIdx.x;
   double t = tbase;
-  for (int k = 0; k < LS_TRIALS; ++k) {
-    const double y = valid ? R * exp(-(vj + t * uj)) : 0.0;
-    const double ye = vabs ? y * (gamma * (va + t * ua) + 4 * U) : 0.0;
-    const double sw = wave_sum(y), se = wave_sum(ye);
-    if (lane == 0) {
-      sred[0][wid][k] = sw;
-      sred[1][wid][k] = se;
-    }
-    t *= beta;
+  for (int q = 0; q < k; ++q) t *= beta;
+  double sw = 0.0, se = 0.0;
+  for (int j = threadIdx.x; j < nout; j += blockDim.x) {  // (j >= nout: k_kl_eval's y is 0 there, exact zeros)
+    const double y = R * exp(-(v[j] + t * u[j]));
+    sw += y;
+    if (vabs) se += y * (gamma * (vabs[j] + t * uabs[j]) + 4 * U);
   }
-  __syncthreads();
-  if (threadIdx.x < 2 * LS_TRIALS) {
-    const int q = threadIdx.x / LS_TRIALS, k = threadIdx.x % LS_TRIALS;
-    part[(size_t)blockIdx.x * 2 * LS_TRIALS + q * LS_TRIALS + k] =
-        ((sred[q][0][k] + sred[q][1][k]) + sred[q][2][k]) + sred[q][3][k];
+  sw = block_sum(sw, red);
+  se = block_sum(se, red);
+  if (threadIdx.x == 0) {
+    out[k] = sw;
+    out[LS_TRIALS + k] = se;
   }
 }
 int ls_kl_blocks(int nout) { return (nout + 255) / 256; }
 void launch_ls_kl(hipStream_t s, const double* v, const double* u, int nout, double R, double tbase, double beta,
                   double* part, double* out, const double* vabs, const double* uabs, double gamma) {
-  const int nb = ls_kl_blocks(nout);
-  k_ls_kl<<<nb, 256, 0, s>>>(v, u, nout, R, tbase, beta, part, vabs, uabs, gamma);
-  k_sum_chunks<<<1, 2 * LS_TRIALS, 0, s>>>(part, nb, 2 * LS_TRIALS, out);
+  (void)part;
+  k_ls_kl<<<LS_TRIALS, 1024, 0, s>>>(v, u, nout, R, tbase, beta, out, vabs, uabs, gamma);
 }
 
 // KL primal objective Dist_KL.objectiveFunction(n) (Dist_KL.scala:223-239) at x, per coordinate j < n:

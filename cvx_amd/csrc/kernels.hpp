@@ -25,9 +25,15 @@ void launch_rowdot(hipStream_t s, const double* M, int ld, int rows, int cols, c
 // y = M v + add, the add fused into the row sweep (bitwise the rowdot followed by launch_axpy(y, add, 1.0))
 void launch_rowdot_add(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v,
                        const double* add, double* y);
-// y = M v and yabs = |M| |v| in the same sweep
+// y = M v and yabs = |M| |v| in the same sweep; max_wg > 0 bounds the grid (the waves loop over the row pairs,
+// bitwise the same sums): beside the assembly SYRK it then holds few CU slots
 void launch_rowdot_abs(hipStream_t s, const double* M, int ld, int rows, int cols, const double* v, double* y,
-                       double* yabs);
+                       double* yabs, int max_wg = 0);
+// y = H v + add from the lower triangle of a symmetric H (diagonal 64 x 64 tiles whole); S: nbn x (nbn 64) partials
+void launch_symv_lower_add(hipStream_t s, const double* H, int ld, int n, const double* v, const double* add,
+                           double* y, double* S);
+// the strictly upper triangle of H from its lower triangle
+void launch_mirror_lower(hipStream_t s, double* H, int ld, int n);
 void launch_ls_setup_eval(hipStream_t st, const double* A, int ld, int mp, int cols, const double* s, const double* x1,
                           double* e, double* eabs, const double* r, const double* ub, double* c, double* d,
                           double* invd, double* w, double* logd, double* cabs, DevCtrl* ctrl);
@@ -123,9 +129,11 @@ void launch_pd_trials(hipStream_t s, const double* c, const double* e, const dou
 // ---- MFMA SYRK (k_syrk.hip) -----------------------------------------------------------------------
 // H = t*P + A' diag(w) A over the lower tile list; split-K when nsplit > 1 (partials + ordered reduce).
 // Pd (optional, with P NULL): a diagonal objective Hessian, H_jj += t Pd_j (the KL primal objective's diag(1/x)).
+// mirror: every lower entry is also stored at its upper position; false: only those of the diagonal tiles (H stays
+// lower-only elsewhere, for consumers that read the lower triangle and whole diagonal tiles).
 void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double* w, int mp, const double* P,
                           const DevCtrl* ctrl, double* H, int ldh, TileList tiles, int nsplit, double* partials,
-                          const double* Pd = nullptr);
+                          const double* Pd = nullptr, bool mirror = true);
 
 // ---- Cholesky (k_chol.hip) ------------------------------------------------------------------------
 // k_dataflow.hip: the whole factorization (potrf + trsm + updates + fused forward solve) as one persistent

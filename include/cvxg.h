@@ -75,9 +75,9 @@ typedef struct cvxg_step_info {
   int iter;                 /* inner iteration index */
   int ls_fresh;             /* line-search feasibility trials evaluated fresh (margin inside the rounding band) */
   int ls_ties;              /* Armijo decisions inside the rounding band of the barrier value (rounding noise) */
-  int small_pivot;          /* regularized: 1-based first row of the 16-column block where the first attempt stopped
-                               on min diag(L) <= 1e-7 (MatrixUtils.scala:458-460); 0 = it ran to the end (a failed
-                               pivot, or not regularized) */
+  int small_pivot;          /* regularized: the 1-based row where the first attempt chol(Q) stopped -- its first
+                               non-positive pivot, or the first row of the 16-column block whose min diag(L) <= 1e-7
+                               (MatrixUtils.scala:456-460); 0 = not regularized */
 } cvxg_step_info;
 
 /* UnconstrainedSolver / EqualityConstrainedSolver result (Solution.scala:32-43). */

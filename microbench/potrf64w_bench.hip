@@ -2,7 +2,8 @@
 // host Cholesky / inverse / forward solve, kernel time via hipEvents over many launches on fresh copies,
 // and per-wave phase stamps (built with -DPOTRF_STAMPS).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPOTRF_STAMPS microbench/potrf64w_bench.hip -o microbench/potrf64w_bench
-// -DWITH_LFLAG: progressive L^-1 stores + flag (the chain's form); -DPOTRF_HDR='"ab_old/potrf64w.hpp"': another version
+// -DWITH_LFLAG: progressive L^-1 stores + flag (the chain's form); -Icvx_amd/csrc -DPOTRF_HDR='"potrf64w_dpp.hpp"': the
+// round-5 DPP column-sweep variant (microbench/potrf64w_dpp.hpp, measured and rejected: DESIGN.md §7)
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>

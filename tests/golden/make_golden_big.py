@@ -21,7 +21,10 @@ Late in the path (t >= 1e6) H is ill-conditioned, so the test holds those steps 
 line-search-replay criteria instead of the 1e-8 direction bar.  C2 is also solved to the standard termination: its
 final x, per-centering step counts and active sets (separated threshold and Constraint.isActive's 1e-12) are stored.
 
-Run:  python tests/golden/make_golden_big.py [C2] [C3]   (C3 takes several minutes and ~6 GB of RAM)
+C3LATE (round 5) pins the late C3 path (t = 1e10 .. 1e12) at the engine's own states: see make_late.
+
+Run:  python tests/golden/make_golden_big.py [C2] [C3] [C3LATE[=states.npz]]   (C3 takes several minutes and ~6 GB
+of RAM)
 """
 from __future__ import annotations
 
@@ -137,6 +140,74 @@ def make(name):
     print(f"{name}: wrote {path} ({os.path.getsize(path) / 1e3:.0f} KB, {time.time() - t0:.0f} s)")
 
 
+def make_late(states_path):
+    """C3LATE: the late C3 path (t = 1e10 .. 1e12, where a full solve spends 96 % of its Newton steps) at states of the
+    ENGINE's own C3 solve (scripts/c3_late_states.py on the GPU: the iterate entering inner iterations 0 and 1 of each
+    late centering and its first regularized steps, with the centering's frozen trust radius).  At each state the
+    oracle computes the gradient, the BLAS-ordered Hessian's Newton direction (Ruiz, regularizedCholesky, dtrtrs,
+    MatrixUtils.scala:240-516), its backward error, the FIRST attempt's min diag(L) of chol(Q) (MatrixUtils.scala:456-458:
+    <= 1e-7 sends the step to Q + 1e-10 I) and the reference's line search from the recorded (iteration, radius)
+    (UnconstrainedSolver.scala:83-113).  The engine's own records ride along (engine_*)."""
+    from scipy.linalg import lapack
+    n, m, inst = 4096, 8192, 0
+    t0 = time.time()
+    st = dict(np.load(states_path))
+    spec = Z.random_qp(n, m, instance=inst)
+    pb = O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"])
+    pars = O.standard_params()
+    sha, psum, a0sum = fingerprint(spec)
+    out = {k: [] for k in ("t", "it_n", "radius", "x", "grad", "f", "dx", "q", "step", "kc", "ka", "ruiz", "reg",
+                           "rel_err", "min_diag0", "info0", "rel_err_alt")}
+    for k in range(st["t"].shape[0]):
+        t, it_n, radius, x = float(st["t"][k]), int(st["it_n"][k]), float(st["radius"][k]), st["x"][k]
+        g = O.barrier_gradient(pb, t, x)
+        rec = O.NewtonStepRecord(x=x, grad=g, f=0.0, dx=None, q=0.0, newton_decrement=0.0)
+        d = O.newton_direction(pb, t, x, g, pars.tolEqSolve, rec, fast_subst=True, hess="blas")
+        assert rec.fallback == 0
+        H = O.barrier_hessian(pb, t, x, literal="blas")
+        dR, Q, _ = O.ruiz_equilibrate(H)
+        L0, info0 = lapack.dpotrf(Q, lower=1, clean=1)
+        mind0 = float(np.min(np.diag(L0))) if info0 == 0 else float("nan")
+        # the other branch of regularizedCholesky at this state (its backward error): where the branch decision is below
+        # FP64's resolution the engine may legitimately take it
+        Qa = Q + np.eye(n) * 1e-10 if rec.regularized == 0 else Q
+        La, infoa = lapack.dpotrf(Qa, lower=1, clean=1)
+        rel_alt = float("nan")
+        if infoa == 0:
+            w_ = O.triangular_solve(La, "L", (dR * -g)[:, None])[:, 0]
+            u_ = O.triangular_solve(La.T, "U", w_[:, None])[:, 0]
+            rel_alt = O.relative_size(H @ (dR * u_) + g, -g, pars.tolEqSolve)
+        del H, Q, L0, Qa, La
+        q = float(np.dot(d, g))
+        if it_n == 0:
+            radius = math.sqrt(-q)
+        f = O.barrier_value(pb, t, x)
+        _, stp, k1, it = O.unconstrained_line_search(pb, t, x, d, q, f, it_n, radius, pars)
+        for key, v in (("t", t), ("it_n", it_n), ("radius", radius), ("x", x), ("grad", g), ("f", f), ("dx", d),
+                       ("q", q), ("step", stp), ("kc", k1), ("ka", it - k1), ("ruiz", rec.ruiz_sweeps),
+                       ("reg", rec.regularized), ("rel_err", rec.rel_err), ("min_diag0", mind0), ("info0", info0),
+                       ("rel_err_alt", rel_alt)):
+            out[key].append(v)
+        print(f"C3LATE: t={t:g} it={it_n} q={q:.6e} step={stp:g} kc={k1} ka={it - k1} ruiz={rec.ruiz_sweeps} "
+              f"reg={rec.regularized} (first attempt min diag {mind0:.3e}, info {info0}; engine reg "
+              f"{int(st['regularized'][k])} min diag {float(st['min_diag'][k]):.3e}) rel_err {rec.rel_err:.2e} (other "
+              f"branch {rel_alt:.2e}) "
+              f"({time.time() - t0:.0f} s)", flush=True)
+    arrays = {k: np.array(v) for k, v in out.items()}
+    for key in ("step", "backtracks_c", "backtracks_armijo", "ruiz_sweeps", "regularized", "min_diag", "rel_err", "q",
+                "ls_ties", "small_pivot"):
+        arrays["engine_" + key] = st[key]
+    arrays.update(n=np.array(n), m=np.array(m), instance=np.array(inst), sha256=np.array(sha), P_sum=np.array(psum),
+                  a0_sum=np.array(a0sum), hess_form=np.array("blas"), source=np.array("engine states"))
+    path = os.path.join(HERE, "big", f"C3late_n{n}_m{m}.npz")
+    np.savez_compressed(path, **arrays)
+    print(f"C3LATE: wrote {path} ({os.path.getsize(path) / 1e3:.0f} KB, {time.time() - t0:.0f} s)")
+
+
 if __name__ == "__main__":
     for nm in (sys.argv[1:] or ["C2", "C3"]):
-        make(nm)
+        if nm.startswith("C3LATE"):  # C3LATE=<states.npz from scripts/c3_late_states.py>
+            make_late(nm.split("=", 1)[1] if "=" in nm else os.path.join(HERE, "..", "..", "gpurun_out",
+                                                                         "c3_late_states.npz"))
+        else:
+            make(nm)

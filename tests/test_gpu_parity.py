@@ -900,6 +900,114 @@ def test_kl_primal_direct_solves_known_answers(mods):
     kl1A.solver.engine.close()
 
 
+_KL_FIXTURE = os.path.join(HERE, "golden", "kl", "kl_direct_n2048.npz")
+
+
+def _kl_centerings(eng, pars, t_max=1e12, on_step=None):
+    """BarrierSolver.solveWithEQs's t-loop (BarrierSolver.scala:124-177) centering by centering from the engine's
+    current x; on_step(t, it, x_before, info) sees every inner iteration when given.  Returns the steps per centering;
+    an engine exception propagates (the reference's NotConvergedException)."""
+    per, t = [], 1.0
+    while t <= t_max:
+        if on_step is None:
+            per.append(eng.centering(pars, t).iter)
+        else:
+            eng.centering_begin(t)
+            k = 0
+            while True:
+                x = eng.get_x()
+                st = eng.newton_step(pars)
+                on_step(t, k, x, st)
+                k += 1
+                if st.done:
+                    break
+            per.append(k)
+        t *= 10.0
+    return per
+
+
+@pytest.mark.parametrize("fused,sparse", [("1", "1"), ("9", "1"), ("1", "0"), ("9", "0")])
+def test_kl_direct_solves_vs_oracle_fixture(mods, monkeypatch, fused, sparse):
+    """The direct KL solves at n = 2048 (kl_1, kl_2: OptimizationProblems.scala:167-210, 271-320, the first solve
+    MinimizationTests.runProblems makes, MinimizationTests.scala:23,35) from the oracle's own phase-I point, against the
+    oracle's whole solve (tests/golden/make_golden_kl.py), under four settings that give the Newton direction different
+    bits (the KKT columns fused into the factorization or solved by the many-column kernels; the positivity rows summed
+    per Hessian entry or through the SYRK).  Late in the path one ulp of f = t f0 - sum log d exceeds the Armijo
+    decrease alpha t q, so those decisions are rounding noise in every implementation -- the oracle's own kl_1 solve
+    runs its last centering to maxIter = 1000.  The reference never throws there: a trial point that rounds to x
+    evaluates to f bitwise (both sides are objF.valueAt) and passes.  Round 4's engine summed the trial objective in
+    another order than f, so such a trial could sit a few ulps above f, and 5 of 24 solves threw
+    CVXG_E_LINESEARCH (profiles/r05/kl_direct/).  Here: no exception in any setting, the oracle's step counts in every
+    centering up to t = 1e4, 13 centerings, the gaps below tolSolver and the final x within 1e-9 of the oracle's."""
+    Z, SP, Engine, O = mods
+    monkeypatch.setenv("CVXG_KKT_FUSED_RHS", fused)
+    monkeypatch.setenv("CVXG_SPARSE_ROWS", sparse)
+    fx = dict(np.load(_KL_FIXTURE))
+    n = int(fx["n"])
+    pars = SP.standardParams()
+    for kind in ("kl_1", "kl_2"):
+        spec = Z.kl_primal_spec(n, kind)
+        eng = Engine(n, spec["A"].shape[0], spec["Aeq"].shape[0])
+        eng.load_problem(spec)
+        eng.set_x(fx[f"{kind}_x0"])
+        per = _kl_centerings(eng, pars)
+        x = eng.get_x()
+        eng.close()
+        ref = fx[f"{kind}_per_centering"].tolist()
+        xr = fx[f"{kind}_x"]
+        rel = np.linalg.norm(x - xr) / np.linalg.norm(xr)
+        print(f"{kind} (fused {fused}, sparse {sparse}): engine {per}, oracle {ref}, |x - x_oracle|/|x_oracle| "
+              f"{rel:.2e}, max|x - x_opt| {np.max(np.abs(x - spec['x_opt'])):.2e}")
+        assert len(per) == len(ref) == 13
+        assert per[:5] == ref[:5], (per, ref)
+        assert all(k <= pars.maxIter for k in per)
+        assert rel < 1e-9
+        assert np.linalg.norm(spec["Aeq"] @ x - spec["beq"]) < pars.tolSolver
+
+
+def test_kl_direct_late_steps_replayed_through_oracle(mods):
+    """The late path of the direct kl_1 solve at n = 2048 (t >= 1e8) step by step: each engine step's (t, x, dx) is
+    replayed through the oracle's EqualityConstrainedSolver line search (EqualityConstrainedSolver.scala:78-97, fresh
+    isInSet / barrierFunction per trial).  Every step whose Armijo decisions the engine certified (no margin inside the
+    rounding band of f) takes exactly the reference's (step, backtracks into C, Armijo backtracks); the reference's
+    line search never throws on these inputs either; steps with rounding-noise decisions are counted and printed."""
+    Z, SP, Engine, O = mods
+    fx = dict(np.load(_KL_FIXTURE))
+    n = int(fx["n"])
+    pars = SP.standardParams()
+    spec = Z.kl_primal_spec(n, "kl_1")
+    pb = _klp_opb(O, spec)
+    eng = Engine(n, spec["A"].shape[0], spec["Aeq"].shape[0])
+    eng.load_problem(spec)
+    aux = Engine(n, spec["A"].shape[0], spec["Aeq"].shape[0])
+    aux.load_problem(spec)
+    eng.set_x(fx["kl_1_x0"])
+    rows = {"certified": 0, "noise": 0, "noise_same": 0}
+
+    def on_step(t, k, x, st):
+        if t < 1e8 or not st.took_step or k >= 12:
+            return
+        dx, _, info = aux.newton_direction(pars, t, x)
+        assert info.q == st.q, (t, k)  # the same direction the step took
+        f = O.barrier_value(pb, t, x)
+        st_o, k1, it = O.equality_line_search(pb, t, x, dx, info.q, f, pars)
+        got, want = (st.step, st.backtracks_c, st.backtracks_armijo), (st_o, k1, it - k1)
+        if st.ls_ties or st.ls_fresh:
+            rows["noise"] += 1
+            rows["noise_same"] += int(got == want)
+        else:
+            rows["certified"] += 1
+            assert got == want, (t, k, got, want)
+
+    per = _kl_centerings(eng, pars, on_step=on_step)
+    eng.close()
+    aux.close()
+    print(f"kl_1 late steps replayed: {rows['certified']} certified (all equal to the reference's line search), "
+          f"{rows['noise']} with rounding-noise Armijo decisions ({rows['noise_same']} of them equal); per centering "
+          f"{per}")
+    assert rows["certified"] + rows["noise"] > 0
+
+
 # ---- PrimalDualSolver (solverType "PD") on the device -----------------------------------------------------------
 
 def _pd_spec(Z, kind, n, m, instance):
@@ -1211,7 +1319,7 @@ def test_golden_baseline_sizes(mods, path):
     pb = _opb(O, spec)
     eng = _engine(Engine, spec)
     pars = SP.standardParams()
-    rels, late, ties = [], [], []
+    rels, late, ties, reg_ties = [], [], [], []
     for k in range(fx["t"].shape[0]):
         t, x, g = float(fx["t"][k]), fx["x"][k], fx["grad"][k]
         it_n, radius = int(fx["it_n"][k]), float(fx["radius"][k])
@@ -1219,7 +1327,16 @@ def test_golden_baseline_sizes(mods, path):
         rel = np.linalg.norm(dx - fx["dx"][k]) / np.linalg.norm(fx["dx"][k])
         qr = float(fx["q"][k])
         assert info.fallback == 0
-        assert info.regularized == int(fx["reg"][k]), (k, t)
+        # regularizedCholesky's test (MatrixUtils.scala:456-460) is decidable in FP64 only when the first attempt's
+        # smallest pivot p = min diag(L)^2 clears its own rounding, ~n u |Q| (|Q| ~ 1 after Ruiz): below sqrt(16 n u)
+        # (2.7e-6 at n = 4096) whether chol(Q) fails, or lands just above or below 1e-7, is rounding noise
+        md0 = float(fx["min_diag0"][k]) if "min_diag0" in fx else float("inf")
+        if not (md0 > np.sqrt(16 * n * np.finfo(float).eps / 2)):
+            reg_ties.append((k, t, md0, info.regularized, int(fx["reg"][k])))
+        else:
+            assert info.regularized == int(fx["reg"][k]), (k, t)
+        if "min_diag0" in fx:  # C3LATE: the engine's states; Ruiz sweeps exact on the late path too
+            assert info.ruiz_sweeps == int(fx["ruiz"][k]), (k, t, info.ruiz_sweeps, int(fx["ruiz"][k]))
         if abs(-qr / 2 - pars.tolSolver) > 0.5 * abs(qr / 2):  # the decrement far from tol: its side is no tie
             assert (-info.q / 2 > pars.tolSolver) == (-qr / 2 > pars.tolSolver), (k, t)
         eng.set_x(x)
@@ -1234,9 +1351,13 @@ def test_golden_baseline_sizes(mods, path):
             assert st.ls_ties == 0 and st.ls_fresh == 0, (k, t, st.ls_ties, st.ls_fresh)
             assert got == (float(fx["step"][k]), int(fx["kc"][k]), int(fx["ka"][k])), (k, t, got)
             continue
-        # late path: backward error against the oracle's own (each side with its own H)
+        # late path: backward error against the oracle's own (each side with its own H); where the regularization
+        # flags differ (below FP64's resolution, above) against the oracle's solve on the engine's branch
         bwd, bwd_ref = info.rel_err, float(fx["rel_err"][k])
-        assert bwd <= max(4 * bwd_ref, 1e-12), (k, t, bwd, bwd_ref)
+        if "rel_err_alt" in fx and info.regularized != int(fx["reg"][k]):
+            bwd_ref = float(fx["rel_err_alt"][k])
+        if np.isfinite(bwd_ref):  # (NaN: the oracle's chol(Q) fails on the branch the engine's succeeded on)
+            assert bwd <= max(4 * bwd_ref, 1e-12), (k, t, bwd, bwd_ref)
         # the reference's line search (fresh isInSet / barrierFunction per trial) on the engine's own direction
         f = O.barrier_value(pb, t, x)
         _, st_o, k1, it = O.unconstrained_line_search(pb, t, x, dx, info.q, f, it_n, radius, pars)
@@ -1254,6 +1375,12 @@ def test_golden_baseline_sizes(mods, path):
     for row in late:
         print("  late t=%g it=%d: rel dx %.2e, backward error engine %.2e oracle %.2e, Ruiz %d/%d, line search %s "
               "(reference on the engine's dx %s)" % row)
+    if "min_diag0" in fx:
+        regs = int(np.sum(fx["reg"]))
+        print(f"  {regs} of {fx['t'].shape[0]} states take regularizedCholesky's Q + 1e-10 I branch (oracle first "
+              f"attempt min diag(L) {np.nanmin(fx['min_diag0']):.2e} .. {np.nanmax(fx['min_diag0']):.2e}); "
+              f"flags below FP64's resolution (state, t, oracle first-attempt min diag, engine flag, oracle flag; "
+              f"reported, not asserted): {reg_ties}")
     print(f"{os.path.basename(path)} ({fx['hess_form']} H): max rel dx {max(rels):.2e} over {len(rels)} early steps, "
           f"{len(late)} late steps, {len(ties)} with a tie")
     assert late, "no late-path step in the fixture"
@@ -1450,8 +1577,9 @@ def test_regularized_first_attempt_stops_early(mods, monkeypatch):
     Q + 1e-10 I, so the engine stops its first attempt at the first 16-column block with such a pivot
     (k_chol_dataflow's early_min) instead of running it to the end.  A mid-matrix small pivot -- columns 300 and 301 of
     A nearly parallel, n = 600 (10 Cholesky blocks) -- stops it in the block of rows 289..304 (small_pivot = 289);
-    with the stop disabled (CVXG_EARLY_ABORT=0) the attempt runs to the end (small_pivot = 0).  Both give bitwise the
-    same dx, min diag(L) and regularization flag (the oracle's), and a whole Newton step from there the same x."""
+    with the stop disabled (CVXG_EARLY_ABORT=0) the attempt runs on past that block (to its first non-positive pivot,
+    which small_pivot then reports, or to the end: 0).  Both give bitwise the same dx, min diag(L) and regularization
+    flag (the oracle's), and a whole Newton step from there the same x."""
     Z, SP, Engine, O = mods
     n, m = 600, 1200
     rng = np.random.default_rng(11)
@@ -1478,7 +1606,7 @@ def test_regularized_first_attempt_stops_early(mods, monkeypatch):
         eng.close()
     a, b = out["1"], out["0"]
     print(f"early stop at row {a[3]} (full attempt: {b[3]}), min diag(L) {a[2]:.3e}, oracle {np.min(rec.diagL):.3e}")
-    assert a[3] == 289 and a[4] == 289 and b[3] == 0 and b[4] == 0
+    assert a[3] == 289 and a[4] == 289 and (b[3] == 0 or b[3] > 304) and b[4] == b[3]
     assert np.array_equal(a[0], b[0]) and a[1] == b[1] == 1 and a[2] == b[2] and a[5] == b[5]
     assert np.array_equal(a[6], b[6])
     assert abs(a[2] - np.min(rec.diagL)) <= 1e-6 * np.min(rec.diagL)
