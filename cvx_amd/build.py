@@ -8,7 +8,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcvxg.so")
-SOURCES = ["k_vec.hip", "k_syrk.hip", "k_chol.hip", "k_dataflow.hip", "k_pd.hip", "k_quad.hip", "symsolve.cpp", "affine.cpp", "k_kkt.hip", "cvxg.cpp"]
+SOURCES = ["k_vec.hip", "k_syrk.hip", "k_chol.hip", "k_dataflow.hip", "k_ruiz.hip", "k_pd.hip", "k_quad.hip", "symsolve.cpp", "affine.cpp", "k_kkt.hip", "cvxg.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 

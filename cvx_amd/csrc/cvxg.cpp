@@ -113,8 +113,15 @@ struct cvxg_ctx {
   // Cholesky and the residual (a lower-triangle symv) read nothing else; consumers of the full matrix (eigen fallback,
   // KKT paths, cvxg_barrier_eval, the primal-dual solver) mirror it first (ensure_h_full).  CVXG_H_LOWER=0: always mirror
   int h_lower = 1;
+  bool chain_b2 = true;         // the chain workgroups apply panel b-2 to block row b (CVXG_CHAIN_B2=0: the workers)
+  bool chain_defer = true;      // L_b,b-1 stored / published inside POTRF(b) (CVXG_CHAIN_DEFER=0: before it)
   bool h_full = true;           // the current H holds its upper triangle too
   double* hsv_part = nullptr;   // symv partials (nblk x np)
+  // Ruiz: every sweep in one persistent launch (k_ruiz.hip; CVXG_RUIZ_LOOP=0: two launches per sweep)
+  int ruiz_loop = 1;
+  int ruiz_wg = 0;              // its workgroups (0: one per CU; CVXG_RUIZ_WG, tests: fewer -> streamed tiles)
+  double* ruiz_S = nullptr;     // its two parity buffers of partials (2 nblk x np)
+  int* ruiz_work = nullptr;     // its counters and flags (ruiz_loop_work_ints)
   int small_piv = 0;            // the last first attempt's stop row (DevCtrl::small_piv, or chol_info)
   int have_sparse = 0;          // set_ineq found sparse rows: the SYRK runs over As / wd / mdp
   int ndense = 0, mdp = 0;      // dense rows, padded to MPAD (>= MPAD)
@@ -357,8 +364,11 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
 // back by its group.  The critical chain tasks POTRF(k), TRSM(k+1,k), UPDATE(k+1,k+1,k) are simulated but
 // not emitted (workgroup 0 runs them in sequence); every transitive dependency of a chain task still precedes
 // that task's dependents in the emitted order, which keeps the launch deadlock-free.
+// the main factorization's chain workgroups apply panel b-2 to block row b themselves (k_dataflow.hip, own_b2)
+constexpr bool CHAIN_OWN_B2_DEFAULT = true;
 static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles, int near = 0,
-                                                 double boost = 0.0, int band = 0, bool eager = true) {
+                                                 double boost = 0.0, int band = 0, bool eager = true,
+                                                 bool own_b2 = false) {
   struct Task {
     int type, i, j, k, cnt;
     double dur, bl, avail;
@@ -442,8 +452,11 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   auto code = [](const Task& x) {
     return ((unsigned)x.type << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j;
   };
-  auto is_chain = [](const Task& x) {
-    return x.type == 0 || (x.type == 1 && x.i == x.k + 1) || (x.type == 2 && x.i == x.j && x.j == x.k + 1);
+  // own_b2: the chain workgroups also apply panel b-2 to block row b (UPDATE(k+2,k+2,k), UPDATE(k+2,k+1,k); always
+  // single-panel tasks: the groups of four end two panels before the diagonal)
+  auto is_chain = [own_b2](const Task& x) {
+    return x.type == 0 || (x.type == 1 && x.i == x.k + 1) || (x.type == 2 && x.i == x.j && x.j == x.k + 1) ||
+           (own_b2 && x.type == 2 && x.i == x.k + 2 && (x.j == x.i || x.j == x.i - 1));
   };
   // the worker tasks the chain's staging of block k+2 waits on -- TRSM(k+2,k), UPDATE(k+2,k+1,k), UPDATE(k+2,k+2,k)
   // -- are emitted as soon as their last dependency is (not at their simulated start), so a worker claims them early
@@ -495,8 +508,8 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
 // The production schedule: four-panel update groups (the last two panels of a tile single) and a priority boost
 // of 100 us for the near-diagonal updates and next-row TRSMs the chain waits on (band 3).  A/B at C3 (boost 0 /
 // band 2 -> 100 / 3): Cholesky 1.553, 1.552, 1.556 -> 1.498, 1.529, 1.502 ms.
-static std::vector<unsigned> chol_schedule(int nblk, int workers) {
-  return build_chol_schedule(nblk, workers, 1, 2, 0, 100.0, 3);
+static std::vector<unsigned> chol_schedule(int nblk, int workers, bool own_b2) {
+  return build_chol_schedule(nblk, workers, 1, 2, 0, 100.0, 3, true, own_b2);
 }
 
 extern "C" int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* relaunches) {
@@ -508,7 +521,7 @@ extern "C" int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* rel
 
 extern "C" int cvxg_chol_schedule(int nblk, int workers, unsigned* order, int cap) {
   if (nblk < 1 || nblk > 1023 || workers < 1 || cap < 0 || (cap > 0 && !order)) return CVXG_E_ARG;
-  const std::vector<unsigned> o = chol_schedule(nblk, workers);
+  const std::vector<unsigned> o = chol_schedule(nblk, workers, CHAIN_OWN_B2_DEFAULT);
   for (size_t t = 0; t < o.size() && (int)t < cap; ++t) order[t] = o[t];
   return (int)o.size();
 }
@@ -730,6 +743,14 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr, const do
 // final pass records the sweep count, or -1 when sweeps were left unlaunched and rho[k1] still exceeds 1e-6.
 static void ruiz_sweeps(cvxg_ctx* ctx, int k0, int k1) {
   hipStream_t s = ctx->s;
+  if (ctx->ruiz_loop) {  // the whole loop in one launch: k0 = 0, k1 = RUIZ_MAX always
+    const int nbn = (ctx->n + NB - 1) / NB;
+    launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl, ctx->ruiz1, ctx->ruiz_work, ruiz_loop_work_ints(nbn));
+    launch_ruiz_loop(s, ctx->H, ctx->np, ctx->n, ctx->ruiz0, ctx->ruiz1, ctx->ruiz_S, ctx->ctrl, ctx->ruiz_work,
+                     ctx->ruiz_wg > 0 ? ctx->ruiz_wg : ctx->ncu);
+    launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl, RUIZ_MAX, ctx->ruiz_work + 1);
+    return;
+  }
   if (k0 == 0) launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl);
   for (int k = k0; k < k1; ++k) {
     const double* dc = (k & 1) ? ctx->ruiz1 : ctx->ruiz0;
@@ -750,6 +771,11 @@ constexpr int RUIZ_MARGIN = 1, RUIZ_CHUNK = 2;
 // The sweeps go out without a host read: the factorization attempt behind them is gated on the device (a launch that
 // finds the loop still open leaves at once), and its one host read tells whether the loop was done (factor_attempt).
 static int ruiz_lookahead(cvxg_ctx* ctx) {
+  if (ctx->ruiz_loop) {  // (the one-launch loop runs to its end on the device: nothing to look ahead of)
+    ruiz(ctx);
+    HIPC(ctx, hipGetLastError());
+    return CVXG_OK;
+  }
   ctx->ruiz_k1 = ctx->ruiz_launch;
   ruiz_sweeps(ctx, 0, ctx->ruiz_k1);
   HIPC(ctx, hipGetLastError());
@@ -787,7 +813,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   // anyway (MatrixUtils.scala:458-460 refactors Q + 1e-10 I), so only the retry's L is ever used
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
                        ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending,
-                       (reg == 0.0 && ctx->early_abort) ? 1e-7 : 0.0);
+                       (reg == 0.0 && ctx->early_abort) ? 1e-7 : 0.0, ctx->chain_b2, ctx->chain_defer);
   ctx->spec_launched = false;
   after();
   HIPC(ctx, hipGetLastError());
@@ -812,6 +838,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   ctx->spec_eval_launched = false;
   if (ctx->hctrl->df_status != 0)
     return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
+  if (ctx->hctrl->ruiz_sweeps == -2) return set_err(ctx, CVXG_E_HIP, "Ruiz loop: dependency wait timed out");
   if (ctx->df_trace) {  // instrumentation only: task order + timeline of this factorization
     std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk));
     std::vector<unsigned> ord(ctx->df_ntasks);
@@ -1079,7 +1106,7 @@ static int kkt_alloc(cvxg_ctx* ctx, bool fused) {
       CHK(dalloc(ctx, &ctx->sLinv, (size_t)ctx->s_nblk * NB * NB));
       CHK(dalloc(ctx, &ctx->kzp, (size_t)ps));
       CHK(dalloc(ctx, &ctx->sw, (size_t)ps));
-      std::vector<unsigned> order = chol_schedule(ctx->s_nblk, ctx->ncu);
+      std::vector<unsigned> order = chol_schedule(ctx->s_nblk, ctx->ncu, false);
       ctx->s_ntasks = (int)order.size();
       CHK(dalloc(ctx, &ctx->s_tasks, std::max<size_t>(order.size(), 1)));
       if (!order.empty())
@@ -1626,7 +1653,10 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   {  // dataflow Cholesky: task order for this tile count, work words
     (void)hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device);
     ctx->ncu = std::max(ctx->ncu, 1);
-    std::vector<unsigned> order = chol_schedule(ctx->nblk, ctx->ncu);
+    ctx->chain_b2 = CHAIN_OWN_B2_DEFAULT;
+    if (const char* e = getenv("CVXG_CHAIN_B2")) ctx->chain_b2 = atoi(e) != 0;
+    if (const char* e = getenv("CVXG_CHAIN_DEFER")) ctx->chain_defer = atoi(e) != 0;
+    std::vector<unsigned> order = chol_schedule(ctx->nblk, ctx->ncu, ctx->chain_b2);
     ctx->df_ntasks = (int)order.size();
     CHK(dalloc(ctx, &ctx->df_tasks, order.size()));
     CHK(copy_sync(ctx, ctx->df_tasks, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
@@ -1664,6 +1694,13 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     part = std::max(part, (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE);
   CHK(dalloc(ctx, &ctx->part, part));
   CHK(dalloc(ctx, &ctx->hsv_part, (size_t)ctx->nblk * np));
+  if (const char* e = getenv("CVXG_RUIZ_LOOP")) ctx->ruiz_loop = atoi(e) != 0;
+  if (const char* e = getenv("CVXG_RUIZ_WG")) ctx->ruiz_wg = std::max(0, atoi(e));
+  if (!ruiz_loop_fits((n + NB - 1) / NB)) ctx->ruiz_loop = 0;
+  if (ctx->ruiz_loop) {
+    CHK(dalloc(ctx, &ctx->ruiz_S, 2 * (size_t)ctx->nblk * np));
+    CHK(dalloc(ctx, &ctx->ruiz_work, ruiz_loop_work_ints(ctx->nblk)));
+  }
   CHK(dalloc(ctx, &ctx->spart,
              ctx->nsplit > 1 ? (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE : (size_t)1));
   HIPC(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
@@ -1700,7 +1737,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
   void* ptrs[] = {ctx->P, ctx->a0, ctx->A, ctx->r, ctx->ub, ctx->Aeq, ctx->beq, ctx->x, ctx->y, ctx->dx, ctx->sdir,
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
-                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
+                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->ruiz_S, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
                   ctx->ls_log, ctx->ls_pcnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,
@@ -1717,7 +1754,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->kY, (void*)ctx->kYg, (void*)ctx->kgram, (void*)ctx->kS, (void*)ctx->kzp,
                   (void*)ctx->sL, (void*)ctx->sLinv, (void*)ctx->sw, (void*)ctx->s_tasks, (void*)ctx->s_work,
-                  (void*)ctx->s_bwd})
+                  (void*)ctx->s_bwd, (void*)ctx->ruiz_work})
     if (p) (void)hipFree(p);
   if (ctx->hctrl) (void)hipHostFree(ctx->hctrl);
   if (ctx->hflag) (void)hipHostFree(ctx->hflag);

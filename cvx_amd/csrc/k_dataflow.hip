@@ -30,6 +30,7 @@ struct ChainSmem {
   double Sa[NB * (NB + 2)];       // A_b,b-1 during the TRSM slices, then L_b,b-1 (for the last rhs correction)
   double E2[2][16 * (NB + 2)];    // double-buffered row-blocks of L_b-1,b-1^-1
   double V[NB * MAX_RHS];
+  int lpub;                       // waves of POTRF(b) done storing L_b,b-1 (deferred publication)
 };
 static_assert(sizeof(ChainSmem) <= DF_SMEM * sizeof(double), "chain workspace exceeds the dataflow LDS");
 
@@ -402,7 +403,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
                                                           int* __restrict__ work, const unsigned* __restrict__ tasks,
                                                           int ntasks, int nblk, unsigned long long* __restrict__ trace,
                                                           const double* __restrict__ Hq, const double* __restrict__ dq,
-                                                          int nq, int ruiz_gate, double early_min) {
+                                                          int nq, int ruiz_gate, double early_min, int own_b2,
+                                                          int defer_pub) {
   // the Ruiz loop launched ahead of the factorization without a host read may still be open (k_ruiz_final: -1): then
   // the launch is void and the host finishes the loop and factors again
   if (ruiz_gate && ctrl->ruiz_sweeps < 0) return;
@@ -467,6 +469,72 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       } else {
         const int k = b - 1;
         mark(k, 1, 0);
+        const Sc1Mem mA(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
+        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
+        // the row-blocks of L_kk^-1 already published (cflag, read while the tile loads are in flight) are loaded
+        // at once into ps.S (free until the diagonal tile goes there at the end of the slices) and applied as one
+        // batch below
+        int pv = 0;
+        d4f dacc[NBLK16];
+        if (own_b2 && b >= 2) {
+          // Panel j = b-2 of block row b on this workgroup (the tasks UPDATE(b,b,j) and UPDATE(b,k,j), not in the
+          // worker list): A_b,k and D_b with every panel < j (state >= j), L_b,j (worker TRSM(b,j)), L_k,j (the other
+          // chain workgroup's slices), the rhs block with TRSM(b, i <= j)'s updates -- one wait, every load in
+          // flight together.  The MFMA sequences are the workers' (df_update's K = 0..63 chain), so the factor is
+          // bitwise the same; the worker -> state word -> staging hop of both tiles is gone from the chain.
+          const int j = b - 2;
+          if (tid == 0) {
+            const int v0 = df_poll(state + df_tri(b, k)), v1 = df_poll(state + df_tri(b, b)),
+                      v2 = df_poll(rhscnt + b), v3 = df_poll(state + df_tri(b, j)), v4 = df_poll(state + df_tri(k, j));
+            s_ok = (v0 >= j || df_wait(state, df_tri(b, k), j, abortw, ctrl)) &&
+                   (v1 >= j || df_wait(state, df_tri(b, b), j, abortw, ctrl)) &&
+                   (v3 >= j + 1 || df_wait(state, df_tri(b, j), j + 1, abortw, ctrl)) &&
+                   (v4 >= j + 1 || df_wait(state, df_tri(k, j), j + 1, abortw, ctrl)) &&
+                   (v2 >= k || df_wait(rhscnt, b, k, abortw, ctrl));
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          __syncthreads();
+          if (!s_ok) return;
+          const int wr = wv >> 1, wc = wv & 1;
+          d4f acc[2][2];
+          {
+            f64x2 vl[NB * NB / 512], vk[NB * NB / 512];
+            df_load(vl, Sc1Mem(L + (size_t)b * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
+            df_load(vk, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
+            df_load_c(acc, mA, ld, b, k, false, qf, wr, wc, lane);
+            const Sc1Mem mD(L + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
+#pragma unroll
+            for (int q = 0; q < NBLK16; ++q) {
+              const int ib = kChIB[wv][q], jb = kChJB[wv][q];
+              if (ib >= 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dacc[q][r] = mD.ld((16 * ib + (lane >> 4) + 4 * r) * ld + 16 * jb + (lane & 15));
+              }
+            }
+            if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+            for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
+            df_put(ps.X, vl);  // (POTRF's L^-1 workspace and tile: free until the reset / the batch below)
+            df_put(ps.S, vk);
+          }
+          __syncthreads();
+          for (int cb = 0; cb < 4; ++cb) {
+            switch (wv) {  // D_b -= L_b,j L_b,j^T on this wave's lower blocks
+              case 0: ch_update<0>(dacc, ps.X, cb, lane); break;
+              case 1: ch_update<1>(dacc, ps.X, cb, lane); break;
+              case 2: ch_update<2>(dacc, ps.X, cb, lane); break;
+              default: ch_update<3>(dacc, ps.X, cb, lane); break;
+            }
+          }
+          df_mfma(acc, ps.X, ps.S, -1.0, wr, wc, lane);  // A_b,k -= L_b,j L_k,j^T
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                cs.Sa[(wr * 32 + mi * 16 + (lane >> 4) + 4 * r) * DF_SP + wc * 32 + nj * 16 + (lane & 15)] = acc[mi][nj][r];
+        } else {
         // A_b,k and D_b with every panel < k applied (state >= k), and the rhs block b with all earlier TRSM
         // updates: one wait for both states, then every load in flight together (minus L_b,k w_k inside POTRF(b);
         // POTRF(b-2) of this workgroup is done with ps.B)
@@ -479,13 +547,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
         if (!s_ok) return;
-        const Sc1Mem mA(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
-        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
-        // the row-blocks of L_kk^-1 already published (cflag, read while the tile loads are in flight) are loaded
-        // at once into ps.S (free until the diagonal tile goes there at the end of the slices) and applied as one
-        // batch below
-        int pv = 0;
-        d4f dacc[NBLK16];
         {
           f64x2 va[NB * NB / 512];
           const bool fold = qf.H && k == 0;  // block 1: A_1,0 and D_1 are first read here
@@ -508,6 +569,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
           for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
           df_put(cs.Sa, va);
+        }
         }
         if (tid == 0) s_next = pv;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -561,7 +623,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               for (int r = 0; r < 4; ++r) {
                 const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
                 Lp[row * DF_SP + col] = acc[cb][r];
-                mA.st(row * ld + col, acc[cb][r]);
+                if (!defer_pub) mA.st(row * ld + col, acc[cb][r]);
               }
           __syncthreads();
           for (int cb = 0; cb < nbat; ++cb) {
@@ -609,7 +671,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             for (int r = 0; r < 4; ++r) {
               const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
               Lp[row * DF_SP + col] = acc[r];
-              mA.st(row * ld + col, acc[r]);
+              if (!defer_pub) mA.st(row * ld + col, acc[r]);
             }
           }
           if (tid == 0) s_next = (cb < 3) && pollv >= cb + 2;  // own word: read between this barrier and the next
@@ -628,7 +690,14 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           const int ib = kChIB[wv][q], jb = kChJB[wv][q];
           if (ib >= 0) c16_store(ps.S + 16 * ib * P64_SP + 16 * jb, P64_SP, dacc[q], lane);
         }
-        publish(df_tri(b, k), k + 1);  // L_b,k stored
+        // L_b,k goes to HBM off the chain: waves 1..3 of POTRF(b) store it from Sa and raise state(b, k) (pre hook
+        // below), while wave 0 runs the first sweep -- no drain round trip between the last slice and POTRF(b)
+        if (defer_pub) {
+          if (tid == 0) cs.lpub = 0;
+          __syncthreads();
+        } else {
+          publish(df_tri(b, k), k + 1);  // L_b,k stored
+        }
         mark(k, 1, 2);
       }
       // POTRF(b): tile and rhs block staged in LDS; L_bb^-1 row-blocks published progressively; before the
@@ -664,7 +733,19 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         potrf64w_reset(ps);
         __syncthreads();
       }  // b > 0: reset behind the staging, the tile's LDS stores behind publish()'s barrier
-      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min)) {
+      auto pre = [&](int w, int ln) {  // waves 1..3: L_b,b-1 from Sa to HBM, the last one to drain raises its state
+        if (b == 0 || !defer_pub) return;
+        const int k = b - 1;
+        const Sc1Mem mL(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
+        for (int e = 64 * (w - 1) + ln; e < NB * NB / 2; e += 192) {
+          const int r = e >> 5, c = 2 * (e & 31);
+          mL.st2(r * ld + c, *reinterpret_cast<const f64x2*>(cs.Sa + r * DF_SP + c));
+        }
+        df_drain();
+        if (ln == 0 && atomicAdd(&cs.lpub, 1) == 2)
+          __hip_atomic_store(state + df_tri(b, k), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      };
+      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
@@ -740,10 +821,11 @@ size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1)
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace, bool zero_work, const double* Hq, const double* dq, int nq,
-                          bool ruiz_gate, double early_min) {
+                          bool ruiz_gate, double early_min, bool own_b2, bool defer_pub) {
   if (zero_work) (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
   k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq,
-                                      ruiz_gate ? 1 : 0, early_min);
+                                      ruiz_gate ? 1 : 0, early_min, own_b2 ? 1 : 0,
+                                      defer_pub ? 1 : 0);
 }
 
 }  // namespace cvxg

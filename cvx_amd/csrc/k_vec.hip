@@ -552,13 +552,18 @@ void launch_scale_vec(hipStream_t s, const double* u, const double* d, int n, do
 // Ruiz equilibration, MatrixUtils.scala:240-268 (Jacobi form: a sweep reads d of the previous sweep).
 // Sweep k runs iff rho[k] > 1e-6 (rho[0] = 1); it writes d into the other buffer and max|1-u| into rho[k+1].
 // ------------------------------------------------------------------------------------------------
-__global__ void k_ruiz_init(double* d0, int np, DevCtrl* ctrl) {
+__global__ void k_ruiz_init(double* d0, double* d1, int np, DevCtrl* ctrl, int* work, int nwork) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < np) d0[i] = 1.0;
+  if (i < np) {
+    d0[i] = 1.0;
+    if (d1) d1[i] = 1.0;
+  }
+  if (i < nwork) work[i] = 0;
   if (i < RUIZ_MAX + 2) ctrl->ruiz_rho[i] = (i == 0) ? (unsigned long long)__double_as_longlong(1.0) : 0ull;
 }
-void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl) {
-  k_ruiz_init<<<(np + 255) / 256, 256, 0, s>>>(d0, np, ctrl);
+void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl, double* d1, int* work, size_t nwork) {
+  const int m = np > (int)nwork ? np : (int)nwork;
+  k_ruiz_init<<<(m + 255) / 256, 256, 0, s>>>(d0, d1, np, ctrl, work, (int)nwork);
 }
 
 // Lower-triangle form of the sweep: H is exactly symmetric (the assembly mirrors its lower triangle), so
@@ -670,7 +675,7 @@ void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np
 // k1 = the sweeps launched so far.  K = the first k < k1 whose rho[k] <= 1e-6 (sweeps K.. exited), else k1;
 // K == k1 < RUIZ_MAX with rho[k1] > 1e-6 means the loop is not done: ruiz_sweeps = -1 (cvxg.cpp: ruiz_lookahead).
 __global__ void k_ruiz_final(const double* __restrict__ d0, const double* __restrict__ d1, int np,
-                             double* __restrict__ dfin, DevCtrl* ctrl, int k1) {
+                             double* __restrict__ dfin, DevCtrl* ctrl, int k1, const int* abortw) {
   int K = k1;
   for (int k = 0; k < k1; ++k) {
     if (!(__longlong_as_double((long long)ctrl->ruiz_rho[k]) > 1e-6)) {
@@ -682,10 +687,11 @@ __global__ void k_ruiz_final(const double* __restrict__ d0, const double* __rest
   const double* src = (K & 1) ? d1 : d0;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < np) dfin[i] = src[i];
-  if (i == 0) ctrl->ruiz_sweeps = open ? -1 : K;
+  if (i == 0) ctrl->ruiz_sweeps = (abortw && *abortw) ? -2 : (open ? -1 : K);
 }
-void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl, int k1) {
-  k_ruiz_final<<<(np + 255) / 256, 256, 0, s>>>(d0, d1, np, dfin, ctrl, k1);
+void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl, int k1,
+                       const int* abortw) {
+  k_ruiz_final<<<(np + 255) / 256, 256, 0, s>>>(d0, d1, np, dfin, ctrl, k1, abortw);
 }
 
 // Q = (dd') o H (+ reg I), lower triangle into L; padded part: identity.   MatrixUtils.scala:267, :454

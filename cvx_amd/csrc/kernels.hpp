@@ -75,11 +75,21 @@ void launch_axpy(hipStream_t s, const double* u, const double* v, double alpha, 
 void launch_scale_vec(hipStream_t s, const double* u, const double* d, int n, double* out);  // out = d*u
 
 // ---- Ruiz equilibration + Q formation ------------------------------------------------------------
-void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl);
+// d0 (and d1 when given) = 1, rho[0] = 1, rho[1..] = 0, work[0..nwork) = 0 (k_ruiz_loop's counters and flags)
+void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl, double* d1 = nullptr, int* work = nullptr,
+                      size_t nwork = 0);
 // The same sweep from the lower triangle only (64 x 64 tiles -> partials S[nbn][nbn*64] -> fixed-order row sums).
 void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np, const double* dcur, double* dnext,
                            double* S, DevCtrl* ctrl, int k);
-void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl, int k1);
+void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl, int k1,
+                       const int* abortw = nullptr /* k_ruiz_loop's abort word: set -> ruiz_sweeps = -2 */);
+// Every sweep in one persistent launch of nwg workgroups (k_ruiz.hip): the same d, rho and sweep count as
+// launch_ruiz_sweep_tri for k = 0 .. RUIZ_MAX-1; S = 2 nbn x (nbn 64) partials, work = ruiz_loop_work_ints(nbn) ints
+// zeroed by launch_ruiz_init.  Only while ruiz_loop_fits(nbn).
+size_t ruiz_loop_work_ints(int nbn);
+bool ruiz_loop_fits(int nbn);
+void launch_ruiz_loop(hipStream_t s, const double* H, int ld, int n, double* d0, double* d1, double* S, DevCtrl* ctrl,
+                      int* work, int nwg);
 // L[i][j] = d_i d_j H_ij (+reg on the diagonal), lower triangle; padded diagonal = 1.
 void launch_form_q(hipStream_t s, const double* H, double* L, int ld, int n, int np, const double* d,
                    const DevCtrl* ctrl);
@@ -149,7 +159,12 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                           bool ruiz_gate = false /* true: every workgroup leaves at once when ctrl->ruiz_sweeps < 0
                                                     (a short Ruiz lookahead, cvxg.cpp: factor_attempt) */,
                           double early_min = 0.0 /* > 0: stop (abort word, min_diag and small_piv set) at the first
-                                                    16-column block whose min diag(L) <= early_min */);
+                                                    16-column block whose min diag(L) <= early_min */,
+                          bool own_b2 = false /* the chain workgroups apply panel b-2 to block row b themselves
+                                                 (UPDATE(b,b,b-2), UPDATE(b,b-1,b-2) not in `tasks`: chol_schedule
+                                                 with the same flag) */,
+                          bool defer_pub = false /* the chain's TRSM tile L_b,b-1 is stored and published by waves 1..3
+                                                    of POTRF(b) instead of before it */);
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
 size_t bwd_work_ints(int nblk);  // flag words + the data-tagged u granules of k_bwd_dataflow
 // Optional epilogue (nrhs = 1): dx = d :* u; with s, also s = dx and x1 = x + s (the speculative line search's

@@ -135,5 +135,9 @@ constexpr int P64_EP = 16 + 2;  // row stride of the 16 x 16 L16^-T blocks
 struct NoFix {
   __device__ bool operator()() const { return true; }
 };
+// pre(w, lane) hook (potrf64w.hpp): waves 1..3 run it first, while wave 0 starts the first sweep
+struct NoPre {
+  __device__ void operator()(int, int) const {}
+};
 
 }  // namespace cvxg

@@ -238,10 +238,10 @@ __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int
 // stored to rhs block k); Linv[k] = L^-1 is stored row-block by row-block as it becomes final (wave 3), and *lflag
 // (when given) counts the stored row-blocks (sc1 hand-off: the stores drained first).  fix() runs on all threads
 // between the factorization and the forward solve (barrier behind it).  L_kk is not stored (potrf64w_store_L).
-template <class M, class Fix = NoFix>
+template <class M, class Fix = NoFix, class Pre = NoPre>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
-                                                Fix fix = Fix(), double early_min = 0.0) {
+                                                Fix fix = Fix(), double early_min = 0.0, Pre pre = Pre()) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -275,6 +275,7 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       }
     }
   } else {
+    pre(w, lane);
 #pragma unroll 1
     for (int kb = 0; kb < 4 && ok; ++kb) {
       ok = p64w_wait(sm, &sm.fP, kb + 1) && (kb == 0 || p64w_wait(sm, &sm.cntU[kb - 1], 3));

@@ -4,7 +4,8 @@ claim in order, cvx_amd/csrc/cvxg.cpp build_chol_schedule) -- host-only, no GPU.
 Deadlock freedom of the persistent launch rests on two properties checked here for several block counts:
   * coverage: every TRSM / UPDATE of the right-looking tile factorization (MatrixUtils.scala:452-461 as 64 x 64
     tiles) is either listed exactly once (UPDATE4 covering four consecutive panels of one tile) or is a chain task
-    (POTRF(k), TRSM(k+1,k), UPDATE(k+1,k+1,k): run by the chain workgroups, never listed);
+    (POTRF(k), TRSM(k+1,k), UPDATE(k+1,k+1,k), UPDATE(k+2,k+2,k), UPDATE(k+2,k+1,k): run by the chain workgroups,
+    never listed);
   * order: a listed task appears after every listed task it depends on (a claimed task only ever waits on tasks
     claimed before it, or on chain tasks, whose own inputs come earlier in the list).
 """
@@ -28,7 +29,9 @@ def _order(nblk, workers=256):
 
 
 def _is_chain(typ, k, i, j):
-    return (typ == 1 and i == k + 1) or (typ == 2 and i == j == k + 1)
+    # POTRF(k), TRSM(k+1,k), UPDATE(k+1,k+1,k), and panel k of block row k+2 (UPDATE(k+2,k+2,k), UPDATE(k+2,k+1,k)),
+    # which the chain workgroup of block k+2 applies itself (k_dataflow.hip, own_b2)
+    return (typ == 1 and i == k + 1) or (typ == 2 and i == j == k + 1) or (typ == 2 and i == k + 2 and j in (i, i - 1))
 
 
 @pytest.mark.parametrize("nblk", [2, 4, 10, 16, 64])
@@ -53,7 +56,7 @@ def test_schedule_covers_every_task_once_in_dependency_order(nblk):
         for i in range(k + 1, nblk):
             assert (i, k) in pos_trsm or i == k + 1
             for j in range(k + 1, i + 1):
-                assert (i, j, k) in pos_upd or (i == j == k + 1), (i, j, k)
+                assert (i, j, k) in pos_upd or _is_chain(2, k, i, j), (i, j, k)
     # order: TRSM(i,k) after the update of tile (i,k) with panel k-1; UPDATE(i,j,k) after TRSM(i,k), TRSM(j,k)
     # and after the update of tile (i,j) with panel k-1
     for (i, k), p in pos_trsm.items():

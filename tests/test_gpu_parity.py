@@ -1381,7 +1381,8 @@ def test_golden_baseline_sizes(mods, path):
               f"attempt min diag(L) {np.nanmin(fx['min_diag0']):.2e} .. {np.nanmax(fx['min_diag0']):.2e}); "
               f"flags below FP64's resolution (state, t, oracle first-attempt min diag, engine flag, oracle flag; "
               f"reported, not asserted): {reg_ties}")
-    print(f"{os.path.basename(path)} ({fx['hess_form']} H): max rel dx {max(rels):.2e} over {len(rels)} early steps, "
+    print(f"{os.path.basename(path)} ({fx['hess_form']} H): max rel dx {max(rels, default=float('nan')):.2e} over "
+          f"{len(rels)} early steps, "
           f"{len(late)} late steps, {len(ties)} with a tie")
     assert late, "no late-path step in the fixture"
     if "x_final" in fx:  # C2: the whole solve and its active set (Constraint.isActive, Constraint.scala:26)
@@ -1610,6 +1611,75 @@ def test_regularized_first_attempt_stops_early(mods, monkeypatch):
     assert np.array_equal(a[0], b[0]) and a[1] == b[1] == 1 and a[2] == b[2] and a[5] == b[5]
     assert np.array_equal(a[6], b[6])
     assert abs(a[2] - np.min(rec.diagL)) <= 1e-6 * np.min(rec.diagL)
+
+
+@pytest.mark.parametrize("n,m", [(200, 400), (1024, 2048), (4096, 8192)])
+def test_chain_owned_panel_updates_bitwise(mods, monkeypatch, n, m):
+    """The chain workgroups of k_chol_dataflow apply panel b-2 to block row b themselves (UPDATE(b,b,b-2) and
+    UPDATE(b,b-1,b-2) taken out of the worker list, CVXG_CHAIN_B2=1, the default): the MFMA sequences are the
+    workers' (K = 0..63 in order on the same accumulator), so the factorization is bitwise the one with the workers
+    applying them (CVXG_CHAIN_B2=0).  Likewise the chain's TRSM tile L_b,b-1 stored and published by waves 1..3 of
+    POTRF(b) (CVXG_CHAIN_DEFER=1, the default) or before it (=0).  Checked on dx, min diag(L) and a whole Newton step,
+    at t = 1 and at later t."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp(n, m, instance=3)
+    pars = SP.standardParams()
+    states = [(1.0, spec["x0"], None, 0, float("nan")), (1e8, spec["x0"], None, 0, float("nan"))]
+    if n == 4096:  # plus a late C3 state whose first attempt is discarded (both factorizations through the chain)
+        fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "big", "C3late_n4096_m8192.npz")))
+        spec = Z.random_qp(n, m, instance=int(fx["instance"]))
+        states = [(1.0, spec["x0"], None, 0, float("nan"))] + [
+            (float(fx["t"][k]), fx["x"][k], fx["grad"][k], int(fx["it_n"][k]), float(fx["radius"][k])) for k in (2, 6)]
+    out = {}
+    for flag in ("11", "01", "10"):  # (CVXG_CHAIN_B2, CVXG_CHAIN_DEFER)
+        monkeypatch.setenv("CVXG_CHAIN_B2", flag[0])
+        monkeypatch.setenv("CVXG_CHAIN_DEFER", flag[1])
+        eng = _engine(Engine, spec)
+        res = []
+        for t, x, g, it_n, radius in states:
+            dx, _, info = eng.newton_direction(pars, t, x, grad=g)
+            eng.set_x(x)
+            eng.centering_resume(t, it_n, radius, grad=g)
+            st = eng.newton_step(pars)
+            res.append((dx, info.min_diag, info.regularized, st.step, eng.get_x()))
+        out[flag] = res
+        eng.close()
+    for other in ("01", "10"):
+        for a, b in zip(out["11"], out[other]):
+            assert np.array_equal(a[0], b[0]) and a[1] == b[1] and a[2] == b[2] and a[3] == b[3], other
+            assert np.array_equal(a[4], b[4]), other
+
+
+@pytest.mark.parametrize("n,m,wg", [(200, 400, 0), (1000, 2000, 0), (1000, 2000, 3), (4096, 8192, 0)])
+def test_ruiz_loop_bitwise(mods, monkeypatch, n, m, wg):
+    """Every Ruiz sweep in one persistent launch (k_ruiz.hip, CVXG_RUIZ_LOOP=1, the default) against the two launches
+    per sweep of k_ruiz_tiles / k_ruiz_rows (CVXG_RUIZ_LOOP=0): the same partial sums in the same order, so the sweep
+    count, min diag(L) and dx are bitwise equal.  n = 1000 has a partial last block; wg = 3 (CVXG_RUIZ_WG) leaves most
+    tiles to the claims beyond the register batch, streamed from H every sweep.  At n = 4096 also two late C3 states
+    (13 sweeps, t = 1e11 and 1e12, the second regularized)."""
+    Z, SP, Engine, O = mods
+    spec = Z.random_qp(n, m, instance=5)
+    pars = SP.standardParams()
+    states = [(1.0, spec["x0"], None), (1e6, spec["x0"], None)]
+    if n == 4096:
+        fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "big", "C3late_n4096_m8192.npz")))
+        spec = Z.random_qp(n, m, instance=int(fx["instance"]))
+        states = [(1.0, spec["x0"], None)] + [(float(fx["t"][k]), fx["x"][k], fx["grad"][k]) for k in (2, 6)]
+    if wg:
+        monkeypatch.setenv("CVXG_RUIZ_WG", str(wg))
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CVXG_RUIZ_LOOP", flag)
+        eng = _engine(Engine, spec)
+        out[flag] = []
+        for t, x, g in states:
+            dx, _, info = eng.newton_direction(pars, t, x, grad=g)
+            out[flag].append((dx, info.ruiz_sweeps, info.min_diag, info.regularized))
+        eng.close()
+    for a, b in zip(out["1"], out["0"]):
+        assert a[1] == b[1] and a[1] > 0 and a[2] == b[2] and a[3] == b[3]
+        assert np.array_equal(a[0], b[0])
+    print(f"n={n}: Ruiz sweeps {[r[1] for r in out['1']]}")
 
 
 def test_batch_barrier_solve_matches_single_contexts(mods):
