@@ -501,14 +501,19 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             f64x2 vl[NB * NB / 512], vk[NB * NB / 512];
             df_load(vl, Sc1Mem(L + (size_t)b * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
             df_load(vk, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
-            df_load_c(acc, mA, ld, b, k, false, qf, wr, wc, lane);
-            const Sc1Mem mD(L + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
+            const bool fold = qf.H && j == 0;  // block 2: A_2,1 and D_2 are first read here (Q formed from H)
+            df_load_c(acc, mA, ld, b, k, fold, qf, wr, wc, lane);
+            const Sc1Mem mD(const_cast<double*>(fold ? qf.H : L) + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
 #pragma unroll
             for (int q = 0; q < NBLK16; ++q) {
               const int ib = kChIB[wv][q], jb = kChJB[wv][q];
               if (ib >= 0) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) dacc[q][r] = mD.ld((16 * ib + (lane >> 4) + 4 * r) * ld + 16 * jb + (lane & 15));
+                for (int r = 0; r < 4; ++r) {
+                  const int rr = 16 * ib + (lane >> 4) + 4 * r, cc = 16 * jb + (lane & 15);
+                  const double h = mD.ld(rr * ld + cc);
+                  dacc[q][r] = fold ? qf_entry(qf, b * NB + rr, b * NB + cc, h) : h;
+                }
               }
             }
             if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
