@@ -115,6 +115,8 @@ struct cvxg_ctx {
   int h_lower = 1;
   bool chain_b2 = true;         // the chain workgroups apply panel b-2 to block row b (CVXG_CHAIN_B2=0: the workers)
   bool chain_defer = true;      // L_b,b-1 stored / published inside POTRF(b) (CVXG_CHAIN_DEFER=0: before it)
+  double* ltag = nullptr;       // CVXG_CHAIN_TAG=1: L_kk^-1 row-blocks also as data-tagged granules for the chain
+  unsigned long long tag_gen = 0;
   bool h_full = true;           // the current H holds its upper triangle too
   double* hsv_part = nullptr;   // symv partials (nblk x np)
   // Ruiz: every sweep in one persistent launch (k_ruiz.hip; CVXG_RUIZ_LOOP=0: two launches per sweep)
@@ -813,7 +815,8 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   // anyway (MatrixUtils.scala:458-460 refactors Q + 1e-10 I), so only the retry's L is ever used
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
                        ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending,
-                       (reg == 0.0 && ctx->early_abort) ? 1e-7 : 0.0, ctx->chain_b2, ctx->chain_defer);
+                       (reg == 0.0 && ctx->early_abort) ? 1e-7 : 0.0, ctx->chain_b2, ctx->chain_defer, ctx->ltag,
+                       ctx->ltag ? ++ctx->tag_gen : 0);
   ctx->spec_launched = false;
   after();
   HIPC(ctx, hipGetLastError());
@@ -1656,6 +1659,11 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     ctx->chain_b2 = CHAIN_OWN_B2_DEFAULT;
     if (const char* e = getenv("CVXG_CHAIN_B2")) ctx->chain_b2 = atoi(e) != 0;
     if (const char* e = getenv("CVXG_CHAIN_DEFER")) ctx->chain_defer = atoi(e) != 0;
+    if (const char* e = getenv("CVXG_CHAIN_TAG"))
+      if (atoi(e) != 0) {
+        CHK(dalloc(ctx, &ctx->ltag, (size_t)ctx->nblk * NB * NB * 2));
+        HIPC(ctx, hipMemset(ctx->ltag, 0, (size_t)ctx->nblk * NB * NB * 16));
+      }
     std::vector<unsigned> order = chol_schedule(ctx->nblk, ctx->ncu, ctx->chain_b2);
     ctx->df_ntasks = (int)order.size();
     CHK(dalloc(ctx, &ctx->df_tasks, order.size()));
@@ -1737,7 +1745,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
   void* ptrs[] = {ctx->P, ctx->a0, ctx->A, ctx->r, ctx->ub, ctx->Aeq, ctx->beq, ctx->x, ctx->y, ctx->dx, ctx->sdir,
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
-                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->ruiz_S, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
+                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->ruiz_S, ctx->ltag, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
                   ctx->ls_log, ctx->ls_pcnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,

@@ -404,7 +404,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
                                                           int ntasks, int nblk, unsigned long long* __restrict__ trace,
                                                           const double* __restrict__ Hq, const double* __restrict__ dq,
                                                           int nq, int ruiz_gate, double early_min, int own_b2,
-                                                          int defer_pub) {
+                                                          int defer_pub, double* __restrict__ ltag,
+                                                          unsigned long long tag_gen) {
   // the Ruiz loop launched ahead of the factorization without a host read may still be open (k_ruiz_final: -1): then
   // the launch is void and the host finishes the loop and factors again
   if (ruiz_gate && ctrl->ruiz_sweeps < 0) return;
@@ -609,6 +610,47 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             er[q] = mI.ld2((16 * cb + (e >> 5)) * NB + 2 * (e & 31));
           }
         };
+        // ltag: row-block cb polled straight from POTRF(k)'s data-tagged granules (no flag, no drain round trip on
+        // the producer); each thread spins on its own granules until every tag is this launch's.  False: abort.
+        const Sc1Mem mT(ltag ? ltag + (size_t)k * NB * NB * 2 : Linv, (unsigned)(NB * NB * 16));
+        const double tagd = __longlong_as_double((long long)tag_gen);
+        f64x2 tg[2][2];
+        auto tissue = [&](int cb) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int e = tid + 256 * q, r = 16 * cb + (e >> 5), c = 2 * (e & 31);
+            if (c < 16 * (cb + 1)) {
+              tg[q][0] = mT.ld2(2 * (r * NB + c));
+              tg[q][1] = mT.ld2(2 * (r * NB + c + 1));
+            } else {
+              tg[q][0] = tg[q][1] = f64x2{0.0, tagd};
+            }
+          }
+        };
+        auto tready = [&]() {
+          bool ok = true;
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            ok = ok && __double_as_longlong(tg[q][0][1]) == __double_as_longlong(tagd) &&
+                 __double_as_longlong(tg[q][1][1]) == __double_as_longlong(tagd);
+          return ok;
+        };
+        auto tfinish = [&](int cb) -> bool {  // spin until this thread's granules carry the tag, then er
+          const unsigned long long t0 = spin_clock();
+          for (unsigned spins = 0; !tready(); ++spins) {
+            if ((spins & 15) == 15 && df_poll(abortw)) return false;
+            if (spin_expired(spins, t0)) {
+              __hip_atomic_store(abortw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              atomicExch(&ctrl->df_status, 2);
+              return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            tissue(cb);
+          }
+#pragma unroll
+          for (int q = 0; q < 2; ++q) er[q] = f64x2{tg[q][0][0], tg[q][1][0]};
+          return true;
+        };
         __syncthreads();  // Sa and the batch's row-blocks in ps.S complete
         double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments
 #pragma unroll
@@ -640,16 +682,24 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             }
           }
         }
+        bool tfail = false;
         if (nbat < 4) {
-          if (!wait(cflag, k, nbat + 1)) return;
-          eload(nbat);
+          if (ltag) {
+            tissue(nbat);
+            tfail = !tfinish(nbat);
+          } else {
+            if (!wait(cflag, k, nbat + 1)) return;
+            eload(nbat);
+          }
         }
         bool have_next = nbat < 4;
 #pragma unroll 1
         for (int cb = nbat; cb < 4; ++cb) {
           double* E = cs.E2[cb & 1];
           if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
-          if (!have_next) {
+          if (ltag) {
+            if (cb > nbat) tfail = tfail || !tfinish(cb);  // (issued behind the previous slice)
+          } else if (!have_next) {
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
           }
@@ -657,13 +707,22 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           // non-blocking look at the next row-block: the sc1 poll is issued here and its value consumed only after
           // this slice's MFMAs, so its round trip stays off the chain
           int pollv = 0;
-          if (cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!ltag && cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q;
             *reinterpret_cast<f64x2*>(E + (e >> 5) * DF_SP + 2 * (e & 31)) = er[q];
           }
-          __syncthreads();
+          if (ltag) {
+            if (tid == 0) s_ok = 1;
+            __syncthreads();
+            if (tfail) s_ok = 0;
+            __syncthreads();
+            if (!s_ok) return;
+            if (cb < 3) tissue(cb + 1);  // the next row-block's granules in flight behind this slice
+          } else {
+            __syncthreads();
+          }
           {  // L'[16 wv.., 16 cb..] = A[16 wv.., :] L^-1[16 cb.., :]^T, K = 16 (cb + 1), two MFMA chains
             d4f acc;
             switch (cb) {
@@ -682,7 +741,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           if (tid == 0) s_next = (cb < 3) && pollv >= cb + 2;  // own word: read between this barrier and the next
           __syncthreads();
           have_next = s_next;
-          if (have_next) eload(cb + 1);  // lands behind the diagonal update below
+          if (!ltag && have_next) eload(cb + 1);  // lands behind the diagonal update below
           switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
             case 0: ch_update<0>(dacc, Lp, cb, lane); break;
             case 1: ch_update<1>(dacc, Lp, cb, lane); break;
@@ -750,7 +809,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         if (ln == 0 && atomicAdd(&cs.lpub, 1) == 2)
           __hip_atomic_store(state + df_tri(b, k), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       };
-      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre)) {
+      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre, ltag, tag_gen)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
@@ -826,11 +885,12 @@ size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1)
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace, bool zero_work, const double* Hq, const double* dq, int nq,
-                          bool ruiz_gate, double early_min, bool own_b2, bool defer_pub) {
+                          bool ruiz_gate, double early_min, bool own_b2, bool defer_pub, double* ltag,
+                          unsigned long long tag_gen) {
   if (zero_work) (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
   k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq,
                                       ruiz_gate ? 1 : 0, early_min, own_b2 ? 1 : 0,
-                                      defer_pub ? 1 : 0);
+                                      defer_pub ? 1 : 0, ltag, tag_gen);
 }
 
 }  // namespace cvxg

@@ -164,7 +164,10 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                                                  (UPDATE(b,b,b-2), UPDATE(b,b-1,b-2) not in `tasks`: chol_schedule
                                                  with the same flag) */,
                           bool defer_pub = false /* the chain's TRSM tile L_b,b-1 is stored and published by waves 1..3
-                                                    of POTRF(b) instead of before it */);
+                                                    of POTRF(b) instead of before it */,
+                          double* ltag = nullptr /* nblk x 64 x 64 granules {value, tag} (16 B): the chain polls the
+                                                    L_kk^-1 row-blocks from them instead of the chain flag */,
+                          unsigned long long tag_gen = 0 /* this launch's tag: nonzero, never repeated on the buffer */);
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
 size_t bwd_work_ints(int nblk);  // flag words + the data-tagged u granules of k_bwd_dataflow
 // Optional epilogue (nrhs = 1): dx = d :* u; with s, also s = dx and x1 = x + s (the speculative line search's

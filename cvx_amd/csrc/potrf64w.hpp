@@ -241,7 +241,8 @@ __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int
 template <class M, class Fix = NoFix, class Pre = NoPre>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
-                                                Fix fix = Fix(), double early_min = 0.0, Pre pre = Pre()) {
+                                                Fix fix = Fix(), double early_min = 0.0, Pre pre = Pre(),
+                                                double* ltag = nullptr, unsigned long long tag_gen = 0) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -292,10 +293,19 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
           break;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        // (ltag: also as data-tagged 16-B granules {value, tag_gen}, the columns < 16 (kb + 1) a consumer's product
+        // reads, which it polls directly instead of the flag)
+        const Sc1Mem mT(ltag ? ltag + (size_t)k * NB * NB * 2 : Linv, (unsigned)(NB * NB * 16));
+        const double tagd = __longlong_as_double((long long)tag_gen);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int e = lane + 64 * q, rr = 16 * kb + (e >> 5), cc = 2 * (e & 31);
-          mI.st2(rr * NB + cc, *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc));
+          const f64x2 v = *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc);
+          mI.st2(rr * NB + cc, v);
+          if (ltag && cc < 16 * (kb + 1)) {
+            mT.st2(2 * (rr * NB + cc), f64x2{v[0], tagd});
+            mT.st2(2 * (rr * NB + cc + 1), f64x2{v[1], tagd});
+          }
         }
         if (lflag != PUBLISH_ONLY) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

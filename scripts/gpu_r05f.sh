@@ -14,10 +14,11 @@ for i in 1 2 3; do
   timeout -k 10 300 $B > $O/ab_def$i.json 2>&1; chk $? def$i
   CVXG_CHAIN_B2=0 timeout -k 10 300 $B > $O/ab_b2off$i.json 2>&1; chk $? b2off$i
   CVXG_CHAIN_DEFER=0 timeout -k 10 300 $B > $O/ab_dfoff$i.json 2>&1; chk $? dfoff$i
+  CVXG_CHAIN_TAG=1 timeout -k 10 300 $B > $O/ab_tag$i.json 2>&1; chk $? tag$i
   CVXG_RUIZ_LOOP=0 timeout -k 10 300 $B > $O/ab_rloff$i.json 2>&1; chk $? rloff$i
 done
-for v in 11 00; do
-  CVXG_CHAIN_B2=${v:0:1} CVXG_CHAIN_DEFER=${v:1:1} CVXG_DF_TRACE=$R/$O/df_$v.bin timeout -k 10 200 python bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/trace_$v.log 2>&1; chk $? trace$v
+for v in 110 000 111; do
+  CVXG_CHAIN_B2=${v:0:1} CVXG_CHAIN_DEFER=${v:1:1} CVXG_CHAIN_TAG=${v:2:1} CVXG_DF_TRACE=$R/$O/df_$v.bin timeout -k 10 200 python bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/trace_$v.log 2>&1; chk $? trace$v
 done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$R/$O/prof.log" 2>&1; chk $? prof
