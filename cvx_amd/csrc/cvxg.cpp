@@ -117,6 +117,7 @@ struct cvxg_ctx {
   bool chain_defer = true;      // L_b,b-1 stored / published inside POTRF(b) (CVXG_CHAIN_DEFER=0: before it)
   double* ltag = nullptr;       // CVXG_CHAIN_TAG=1: L_kk^-1 row-blocks also as data-tagged granules for the chain
   unsigned long long tag_gen = 0;
+  bool chain_dpp = false;       // CVXG_CHAIN_DPP=1: POTRF's column sweep with DPP broadcasts
   bool h_full = true;           // the current H holds its upper triangle too
   double* hsv_part = nullptr;   // symv partials (nblk x np)
   // Ruiz: every sweep in one persistent launch (k_ruiz.hip; CVXG_RUIZ_LOOP=0: two launches per sweep)
@@ -816,7 +817,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
                        ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending,
                        (reg == 0.0 && ctx->early_abort) ? 1e-7 : 0.0, ctx->chain_b2, ctx->chain_defer, ctx->ltag,
-                       ctx->ltag ? ++ctx->tag_gen : 0);
+                       ctx->ltag ? ++ctx->tag_gen : 0, ctx->chain_dpp);
   ctx->spec_launched = false;
   after();
   HIPC(ctx, hipGetLastError());
@@ -1659,6 +1660,13 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     ctx->chain_b2 = CHAIN_OWN_B2_DEFAULT;
     if (const char* e = getenv("CVXG_CHAIN_B2")) ctx->chain_b2 = atoi(e) != 0;
     if (const char* e = getenv("CVXG_CHAIN_DEFER")) ctx->chain_defer = atoi(e) != 0;
+    if (const char* e = getenv("CVXG_CHAIN_DPP")) ctx->chain_dpp = atoi(e) != 0;
+    {
+      const bool tag = getenv("CVXG_CHAIN_TAG") && atoi(getenv("CVXG_CHAIN_TAG")) != 0;
+      const int v = (ctx->chain_b2 ? 1 : 0) | (ctx->chain_defer ? 2 : 0) | (tag ? 4 : 0) | (ctx->chain_dpp ? 8 : 0);
+      if (!chol_dataflow_variant_ok(v))
+        return set_err(ctx, CVXG_E_UNSUPPORTED, "CVXG_CHAIN_* variant %d of the dataflow Cholesky is not built", v);
+    }
     if (const char* e = getenv("CVXG_CHAIN_TAG"))
       if (atoi(e) != 0) {
         CHK(dalloc(ctx, &ctx->ltag, (size_t)ctx->nblk * NB * NB * 2));

@@ -398,14 +398,18 @@ __device__ __forceinline__ void ch_update(d4f (&dacc)[3], const double* Lp, int 
                                                        lf[kChJB[W][q] < 0 ? 0 : kChJB[W][q]][st], dacc[q], 0, 0, 0);
 }
 
+// V: compile-time variant bits (each a separate instantiation, so an unused variant costs no registers):
+//   1 the chain applies panel b-2 to block row b, 2 L_b,b-1 stored / published inside POTRF(b), 4 L_kk^-1 row-blocks
+//   handed to the chain as data-tagged granules (ltag), 8 POTRF's column sweep with DPP broadcasts
+template <int V>
 __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L, int ld, double* __restrict__ rhs,
                                                           int nrhs, double* __restrict__ Linv, DevCtrl* ctrl,
                                                           int* __restrict__ work, const unsigned* __restrict__ tasks,
                                                           int ntasks, int nblk, unsigned long long* __restrict__ trace,
                                                           const double* __restrict__ Hq, const double* __restrict__ dq,
-                                                          int nq, int ruiz_gate, double early_min, int own_b2,
-                                                          int defer_pub, double* __restrict__ ltag,
-                                                          unsigned long long tag_gen) {
+                                                          int nq, int ruiz_gate, double early_min,
+                                                          double* __restrict__ ltag, unsigned long long tag_gen) {
+  constexpr bool kB2 = (V & 1) != 0, kDefer = (V & 2) != 0, kTag = (V & 4) != 0, kDpp = (V & 8) != 0;
   // the Ruiz loop launched ahead of the factorization without a host read may still be open (k_ruiz_final: -1): then
   // the launch is void and the host finishes the loop and factors again
   if (ruiz_gate && ctrl->ruiz_sweeps < 0) return;
@@ -477,7 +481,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         // batch below
         int pv = 0;
         d4f dacc[NBLK16];
-        if (own_b2 && b >= 2) {
+        if (kB2 && b >= 2) {
           // Panel j = b-2 of block row b on this workgroup (the tasks UPDATE(b,b,j) and UPDATE(b,k,j), not in the
           // worker list): A_b,k and D_b with every panel < j (state >= j), L_b,j (worker TRSM(b,j)), L_k,j (the other
           // chain workgroup's slices), the rhs block with TRSM(b, i <= j)'s updates -- one wait, every load in
@@ -670,7 +674,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               for (int r = 0; r < 4; ++r) {
                 const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
                 Lp[row * DF_SP + col] = acc[cb][r];
-                if (!defer_pub) mA.st(row * ld + col, acc[cb][r]);
+                if (!kDefer) mA.st(row * ld + col, acc[cb][r]);
               }
           __syncthreads();
           for (int cb = 0; cb < nbat; ++cb) {
@@ -684,7 +688,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         }
         bool tfail = false;
         if (nbat < 4) {
-          if (ltag) {
+          if constexpr (kTag) {
             tissue(nbat);
             tfail = !tfinish(nbat);
           } else {
@@ -697,8 +701,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         for (int cb = nbat; cb < 4; ++cb) {
           double* E = cs.E2[cb & 1];
           if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
-          if (ltag) {
-            if (cb > nbat) tfail = tfail || !tfinish(cb);  // (issued behind the previous slice)
+          if constexpr (kTag) {
+            if (cb > nbat) {
+              tissue(cb);
+              tfail = tfail || !tfinish(cb);
+            }
           } else if (!have_next) {
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
@@ -707,19 +714,18 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           // non-blocking look at the next row-block: the sc1 poll is issued here and its value consumed only after
           // this slice's MFMAs, so its round trip stays off the chain
           int pollv = 0;
-          if (!ltag && cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!kTag && cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q;
             *reinterpret_cast<f64x2*>(E + (e >> 5) * DF_SP + 2 * (e & 31)) = er[q];
           }
-          if (ltag) {
+          if constexpr (kTag) {
             if (tid == 0) s_ok = 1;
             __syncthreads();
             if (tfail) s_ok = 0;
             __syncthreads();
             if (!s_ok) return;
-            if (cb < 3) tissue(cb + 1);  // the next row-block's granules in flight behind this slice
           } else {
             __syncthreads();
           }
@@ -735,13 +741,13 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             for (int r = 0; r < 4; ++r) {
               const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
               Lp[row * DF_SP + col] = acc[r];
-              if (!defer_pub) mA.st(row * ld + col, acc[r]);
+              if (!kDefer) mA.st(row * ld + col, acc[r]);
             }
           }
           if (tid == 0) s_next = (cb < 3) && pollv >= cb + 2;  // own word: read between this barrier and the next
           __syncthreads();
           have_next = s_next;
-          if (!ltag && have_next) eload(cb + 1);  // lands behind the diagonal update below
+          if (!kTag && have_next) eload(cb + 1);  // lands behind the diagonal update below
           switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
             case 0: ch_update<0>(dacc, Lp, cb, lane); break;
             case 1: ch_update<1>(dacc, Lp, cb, lane); break;
@@ -756,7 +762,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         }
         // L_b,k goes to HBM off the chain: waves 1..3 of POTRF(b) store it from Sa and raise state(b, k) (pre hook
         // below), while wave 0 runs the first sweep -- no drain round trip between the last slice and POTRF(b)
-        if (defer_pub) {
+        if (kDefer) {
           if (tid == 0) cs.lpub = 0;
           __syncthreads();
         } else {
@@ -798,7 +804,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         __syncthreads();
       }  // b > 0: reset behind the staging, the tile's LDS stores behind publish()'s barrier
       auto pre = [&](int w, int ln) {  // waves 1..3: L_b,b-1 from Sa to HBM, the last one to drain raises its state
-        if (b == 0 || !defer_pub) return;
+        if (b == 0 || !kDefer) return;
         const int k = b - 1;
         const Sc1Mem mL(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
         for (int e = 64 * (w - 1) + ln; e < NB * NB / 2; e += 192) {
@@ -809,7 +815,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         if (ln == 0 && atomicAdd(&cs.lpub, 1) == 2)
           __hip_atomic_store(state + df_tri(b, k), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       };
-      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre, ltag, tag_gen)) {
+      if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre,
+                                   kTag ? ltag : nullptr, tag_gen, kDpp)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
@@ -880,17 +887,30 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
 
 // work: [0] counter, [1] abort word, [2] role ticket, [64 ..) one state word per lower tile, then one chain flag and
 // one rhs counter per diagonal block; zeroed before every launch.
+bool chol_dataflow_variant_ok(int v) { return v == 0 || v == 1 || v == 2 || v == 3 || v == 7 || v == 11 || v == 15; }
 size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + 2 * (size_t)nblk; }
 
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace, bool zero_work, const double* Hq, const double* dq, int nq,
                           bool ruiz_gate, double early_min, bool own_b2, bool defer_pub, double* ltag,
-                          unsigned long long tag_gen) {
+                          unsigned long long tag_gen, bool dpp_sweep) {
+  const int v = (own_b2 ? 1 : 0) | (defer_pub ? 2 : 0) | (ltag ? 4 : 0) | (dpp_sweep ? 8 : 0);
   if (zero_work) (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
-  k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq,
-                                      ruiz_gate ? 1 : 0, early_min, own_b2 ? 1 : 0,
-                                      defer_pub ? 1 : 0, ltag, tag_gen);
+#define CVXG_DF_LAUNCH(VV)                                                                                       \
+  k_chol_dataflow<VV><<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq,  \
+                                          ruiz_gate ? 1 : 0, early_min, ltag, tag_gen)
+  switch (v) {  // the instantiated variants (chol_dataflow_variant_ok)
+    case 0: CVXG_DF_LAUNCH(0); break;
+    case 1: CVXG_DF_LAUNCH(1); break;
+    case 2: CVXG_DF_LAUNCH(2); break;
+    case 3: CVXG_DF_LAUNCH(3); break;
+    case 7: CVXG_DF_LAUNCH(7); break;
+    case 11: CVXG_DF_LAUNCH(11); break;
+    case 15: CVXG_DF_LAUNCH(15); break;
+    default: CVXG_DF_LAUNCH(3); break;
+  }
+#undef CVXG_DF_LAUNCH
 }
 
 }  // namespace cvxg

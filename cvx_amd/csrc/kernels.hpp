@@ -149,6 +149,8 @@ void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double*
 // k_dataflow.hip: the whole factorization (potrf + trsm + updates + fused forward solve) as one persistent
 // launch over the 64x64 tile DAG in the host-built task order (build_chol_schedule in cvxg.cpp)
 size_t chol_dataflow_work_ints(int nblk);
+// the k_chol_dataflow variants built (bits: 1 own_b2, 2 defer_pub, 4 ltag, 8 dpp_sweep)
+bool chol_dataflow_variant_ok(int v);
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */,
@@ -167,7 +169,8 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                                                     of POTRF(b) instead of before it */,
                           double* ltag = nullptr /* nblk x 64 x 64 granules {value, tag} (16 B): the chain polls the
                                                     L_kk^-1 row-blocks from them instead of the chain flag */,
-                          unsigned long long tag_gen = 0 /* this launch's tag: nonzero, never repeated on the buffer */);
+                          unsigned long long tag_gen = 0 /* this launch's tag: nonzero, never repeated on the buffer */,
+                          bool dpp_sweep = false /* POTRF's column sweep with DPP broadcasts (bitwise the same) */);
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
 size_t bwd_work_ints(int nblk);  // flag words + the data-tagged u granules of k_bwd_dataflow
 // Optional epilogue (nrhs = 1): dx = d :* u; with s, also s = dx and x1 = x + s (the speculative line search's

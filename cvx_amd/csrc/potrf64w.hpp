@@ -19,6 +19,8 @@
 // shared by all waves between the barriers) the chain of wave 0 per step is the sweep, 8 MFMAs and two LDS round
 // trips.
 #pragma once
+#include <utility>
+
 #include "potrf64.hpp"
 
 namespace cvxg {
@@ -193,6 +195,92 @@ __device__ __forceinline__ bool p64w_eliminate(Potrf64wSmem& sm, int kb, int bas
   return true;
 }
 
+// The same sweep with the column broadcasts folded into the update instructions (dpp_sweep): every lane-row of 16
+// lanes holds a copy of D_kb (row r in lane r), so D_cj is one DPP row_newbcast:c away and rides in v_fmac_f64_dpp
+// (64-bit DPP, gfx90a+) instead of two v_readlane per broadcast value; the identity border beside it (-> L~16^-T) is
+// a second register row of lane-row 0.  Per entry the same fma as p64w_eliminate -- fma(D_cj, -(a_j r_j), a_c) is
+// fma(-(a_j r_j), D_cj, a_c) -- and the next pivot the same value, so L16, L16^-T and the pivots are bitwise equal.
+// (microbench/sweep_dpp.hip: 3 600 cycles per 16 columns with 48 panel rows riding along.)
+template <int C>
+__device__ __forceinline__ void p64w_fmac_bc(double& dst, double src, double m) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(dst) : "v"(src), "v"(m), "i"(C));
+}
+template <int C>
+__device__ __forceinline__ double p64w_bc(double src) {
+  double d;
+  asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(d) : "v"(src), "i"(C));
+  return d;
+}
+template <int J, int... Cs>
+__device__ __forceinline__ void p64w_rest(double (&a)[16], double (&b)[16], double nta, double ntb,
+                                          std::integer_sequence<int, Cs...>) {
+  ((p64w_fmac_bc<J + 2 + Cs>(a[J + 2 + Cs], a[J], nta), p64w_fmac_bc<J + 2 + Cs>(b[J + 2 + Cs], a[J], ntb)), ...);
+}
+template <int J>
+__device__ __forceinline__ void p64w_dstep(double (&a)[16], double (&b)[16], double& piv, double& rinv, double& mypiv,
+                                           int r, double& pmin, int& firstbad) {
+  if constexpr (J < 16) {
+    if (!(piv > 0.0) && firstbad < 0) firstbad = J;
+    pmin = fmin(pmin, piv);
+    if (r == J) mypiv = piv;
+    const double nta = -(a[J] * rinv), ntb = -(b[J] * rinv);
+    if constexpr (J + 1 < 16) {
+      p64w_fmac_bc<J + 1>(a[J + 1], a[J], nta);
+      p64w_fmac_bc<J + 1>(b[J + 1], a[J], ntb);
+      piv = p64w_bc<J + 1>(a[J + 1]);
+      rinv = rcp_nr(piv);
+    }
+    p64w_rest<J>(a, b, nta, ntb, std::make_integer_sequence<int, (J + 2 < 16 ? 14 - J : 0)>{});
+    p64w_dstep<J + 1>(a, b, piv, rinv, mypiv, r, pmin, firstbad);
+  }
+}
+__device__ __forceinline__ bool p64w_eliminate_dpp(Potrf64wSmem& sm, int kb, int base, DevCtrl* ctrl, double& mind,
+                                                   int lane, double early_min) {
+  const int o = 16 * kb, r = lane & 15, g = lane >> 4;
+  double a[16], b[16];
+  {
+    const double* src = sm.S + (o + r) * P64_SP + o;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) {
+      const f64x2 v = *reinterpret_cast<const f64x2*>(src + c);
+      a[c] = (c <= r) ? v[0] : 0.0;
+      a[c + 1] = (c + 1 <= r) ? v[1] : 0.0;
+      b[c] = (g == 0 && c == r) ? 1.0 : 0.0;
+      b[c + 1] = (g == 0 && c + 1 == r) ? 1.0 : 0.0;
+    }
+  }
+  int firstbad = -1;
+  double piv = p64w_bc<0>(a[0]);
+  double rinv = rcp_nr(piv);
+  double pmin = piv;
+  double mypiv = 1.0;
+  p64w_dstep<0>(a, b, piv, rinv, mypiv, r, pmin, firstbad);
+  const double bmin = pmin * rsqrt_nr(pmin);
+  mind = fmin(mind, bmin);
+  if (lane < 16) {
+    sm.SV[kb][r] = rsqrt_nr(mypiv);
+    double* dS = sm.S + (o + r) * P64_SP + o;
+    double* dE = sm.ET[kb] + r * P64_EP;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) {
+      *reinterpret_cast<f64x2*>(dS + c) = f64x2{(c <= r) ? a[c] : 0.0, (c + 1 <= r) ? a[c + 1] : 0.0};
+      *reinterpret_cast<f64x2*>(dE + c) = f64x2{b[c], b[c + 1]};
+    }
+  }
+  if (firstbad >= 0) {
+    if (lane == 0) atomicCAS(&ctrl->chol_info, 0, base + o + firstbad + 1);
+    return false;
+  }
+  if (early_min > 0.0 && !(bmin > early_min)) {
+    if (lane == 0) {
+      atomic_min_pos(&ctrl->min_diag, bmin);
+      atomicCAS(&ctrl->small_piv, 0, base + o + 1);
+    }
+    return false;
+  }
+  return true;
+}
+
 // Phase A / B work of waves 1..3 at step kb (static assignment, see the header).
 __device__ __forceinline__ void p64w_phaseA(Potrf64wSmem& sm, int kb, int w, int lane) {
   if (kb == 0) {
@@ -242,7 +330,8 @@ template <class M, class Fix = NoFix, class Pre = NoPre>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
                                                 Fix fix = Fix(), double early_min = 0.0, Pre pre = Pre(),
-                                                double* ltag = nullptr, unsigned long long tag_gen = 0) {
+                                                double* ltag = nullptr, unsigned long long tag_gen = 0,
+                                                bool dpp_sweep = false) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -252,7 +341,8 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
 #pragma unroll 1
     for (int kb = 0; kb < 4 && ok; ++kb) {
       P64_STAMP(1 + 4 * kb);
-      ok = p64w_eliminate(sm, kb, base, ctrl, mind, lane, early_min);
+      ok = dpp_sweep ? p64w_eliminate_dpp(sm, kb, base, ctrl, mind, lane, early_min)
+                     : p64w_eliminate(sm, kb, base, ctrl, mind, lane, early_min);
       P64_STAMP(2 + 4 * kb);
       if (!ok) {
         if (lane == 0) __hip_atomic_store(&sm.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -3,13 +3,17 @@
 // and per-wave phase stamps (built with -DPOTRF_STAMPS).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPOTRF_STAMPS microbench/potrf64w_bench.hip -o microbench/potrf64w_bench
 // -DWITH_LFLAG: progressive L^-1 stores + flag (the chain's form); -Icvx_amd/csrc -DPOTRF_HDR='"potrf64w_dpp.hpp"': the
-// round-5 DPP column-sweep variant (microbench/potrf64w_dpp.hpp, measured and rejected: DESIGN.md §7)
+// round-5 DPP column-sweep variant (microbench/potrf64w_dpp.hpp, measured and rejected: DESIGN.md §7);
+// -DP64_DPP_ON=true: potrf64w's own DPP sweep (same structure as the v_readlane sweep, bitwise the same factor)
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 
 #include <vector>
 
+#ifndef P64_DPP_ON
+#define P64_DPP_ON false  // -DP64_DPP_ON=true: the DPP column sweep (potrf64w.hpp p64w_eliminate_dpp)
+#endif
 #ifndef POTRF_HDR
 #define POTRF_HDR "../cvx_amd/csrc/potrf64w.hpp"
 #endif
@@ -34,9 +38,11 @@ __global__ __launch_bounds__(256) void k_p64(double* L, int ld, int k, double* r
     potrf64w_reset(sm);
     __syncthreads();
 #ifdef WITH_LFLAG
-    if (potrf64w_factor<Sc1Mem>(k, rhs, nrhs, Linv, ctrl, sm, &g_lflag)) potrf64w_store_L<Sc1Mem>(L, ld, k, sm);
+    if (potrf64w_factor<Sc1Mem>(k, rhs, nrhs, Linv, ctrl, sm, &g_lflag, NoFix(), 0.0, NoPre(), nullptr, 0, P64_DPP_ON))
+      potrf64w_store_L<Sc1Mem>(L, ld, k, sm);
 #else
-    if (potrf64w_factor<PlainMem>(k, rhs, nrhs, Linv, ctrl, sm)) potrf64w_store_L<PlainMem>(L, ld, k, sm);
+    if (potrf64w_factor<PlainMem>(k, rhs, nrhs, Linv, ctrl, sm, nullptr, NoFix(), 0.0, NoPre(), nullptr, 0, P64_DPP_ON))
+      potrf64w_store_L<PlainMem>(L, ld, k, sm);
 #endif
     __syncthreads();
   }
