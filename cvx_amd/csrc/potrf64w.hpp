@@ -83,6 +83,17 @@ __device__ __forceinline__ void potrf64w_stage(const double* L, int ld, size_t o
   for (int t = tid; t < NB * nrhs; t += 256) sm.B[t] = mR.ld(t);
 }
 
+// Optional data-tagged copy of L^-1 (the chain's consumer polls it, k_dataflow.hip): granule (r, c) of block k's
+// L^-1 = {value, tag} at base[2 (64 r + c)], stored by whichever wave computes the entry, as soon as it is final.
+struct TagOut {
+  double* base;  // nullptr: none
+  double tag;
+  __device__ __forceinline__ void put(int r, int c, double v) const {
+    const Sc1Mem m(base, (unsigned)(NB * NB * 16));
+    m.st2(2 * (r * NB + c), f64x2{v, tag});
+  }
+};
+
 // 16 x 16 block ops on LDS operands (one wave)
 __device__ __forceinline__ void p64w_T(Potrf64wSmem& sm, int ib, int kb, int lane) {  // L_ib,kb = A_ib,kb L16^-T
   double* C = sm.S + 16 * ib * P64_SP + 16 * kb;
@@ -98,7 +109,7 @@ __device__ __forceinline__ void p64w_U(Potrf64wSmem& sm, int ib, int jb, int kb,
                    lane);
   c16_store(C, P64_SP, acc, lane);
 }
-__device__ __forceinline__ void p64w_X(Potrf64wSmem& sm, int kb, int j, int lane) {  // X_kb,j, j < kb
+__device__ __forceinline__ void p64w_X(Potrf64wSmem& sm, int kb, int j, int lane, const TagOut& to) {  // X_kb,j, j < kb
   d4f T = {0.0, 0.0, 0.0, 0.0};
   for (int m = j; m < kb; ++m)
     T = mfma16_ab(T, sm.S + 16 * kb * P64_SP + 16 * m, P64_SP, sm.X + 16 * m * P64_SP + 16 * j, P64_SP, 1.0, lane);
@@ -110,16 +121,22 @@ __device__ __forceinline__ void p64w_X(Potrf64wSmem& sm, int kb, int j, int lane
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] *= sm.SV[kb][(lane >> 4) + 4 * i];  // row scales (C layout: row (lane>>4) + 4i)
   c16_store(sm.X + 16 * kb * P64_SP + 16 * j, P64_SP, acc, lane);
+  if (to.base) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) to.put(16 * kb + (lane >> 4) + 4 * i, 16 * j + (lane & 15), acc[i]);
+  }
 }
 // X_kb,kb = (L16^-T)' with the column scales, and the scales of the L16 block of S (L16 = L~16 diag(s))
-__device__ __forceinline__ void p64w_Xdiag(Potrf64wSmem& sm, int kb, int lane) {
+__device__ __forceinline__ void p64w_Xdiag(Potrf64wSmem& sm, int kb, int lane, const TagOut& to) {
   const double* ET = sm.ET[kb];
   const double* sv = sm.SV[kb];
   const int o = 16 * kb;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int e = lane + 64 * i, rr = e >> 4, cc = e & 15;
-    sm.X[(o + cc) * P64_SP + o + rr] = ET[rr * P64_EP + cc] * sv[cc];
+    const double x = ET[rr * P64_EP + cc] * sv[cc];
+    sm.X[(o + cc) * P64_SP + o + rr] = x;
+    if (to.base) to.put(o + cc, o + rr, x);
     double* sd = sm.S + (o + rr) * P64_SP + o + cc;
     *sd = (cc <= rr) ? *sd * sv[cc] : 0.0;
   }
@@ -282,25 +299,25 @@ __device__ __forceinline__ bool p64w_eliminate_dpp(Potrf64wSmem& sm, int kb, int
 }
 
 // Phase A / B work of waves 1..3 at step kb (static assignment, see the header).
-__device__ __forceinline__ void p64w_phaseA(Potrf64wSmem& sm, int kb, int w, int lane) {
+__device__ __forceinline__ void p64w_phaseA(Potrf64wSmem& sm, int kb, int w, int lane, const TagOut& to) {
   if (kb == 0) {
     if (w == 1) p64w_T(sm, 2, 0, lane);
     if (w == 2) p64w_T(sm, 3, 0, lane);
-    if (w == 3) p64w_Xdiag(sm, 0, lane);
+    if (w == 3) p64w_Xdiag(sm, 0, lane, to);
   } else if (kb == 1) {
     if (w == 1) p64w_T(sm, 3, 1, lane);
-    if (w == 2) p64w_X(sm, 1, 0, lane);
-    if (w == 3) p64w_Xdiag(sm, 1, lane);
+    if (w == 2) p64w_X(sm, 1, 0, lane, to);
+    if (w == 3) p64w_Xdiag(sm, 1, lane, to);
   } else if (kb == 2) {
-    if (w == 1) p64w_X(sm, 2, 0, lane);
-    if (w == 2) p64w_X(sm, 2, 1, lane);
-    if (w == 3) p64w_Xdiag(sm, 2, lane);
+    if (w == 1) p64w_X(sm, 2, 0, lane, to);
+    if (w == 2) p64w_X(sm, 2, 1, lane, to);
+    if (w == 3) p64w_Xdiag(sm, 2, lane, to);
   } else {
-    if (w == 1) p64w_X(sm, 3, 0, lane);
-    if (w == 2) p64w_X(sm, 3, 1, lane);
+    if (w == 1) p64w_X(sm, 3, 0, lane, to);
+    if (w == 2) p64w_X(sm, 3, 1, lane, to);
     if (w == 3) {
-      p64w_X(sm, 3, 2, lane);
-      p64w_Xdiag(sm, 3, lane);
+      p64w_X(sm, 3, 2, lane, to);
+      p64w_Xdiag(sm, 3, lane, to);
     }
   }
 }
@@ -335,6 +352,7 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
+  const TagOut to{ltag ? ltag + (size_t)k * NB * NB * 2 : nullptr, __longlong_as_double((long long)tag_gen)};
   double mind = __builtin_inf();
   bool ok = true;
   if (w == 0) {
@@ -373,7 +391,7 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       if (!ok) break;
       P64_STAMP(1 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      p64w_phaseA(sm, kb, w, lane);
+      p64w_phaseA(sm, kb, w, lane, to);
       P64_STAMP(2 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_add(&sm.cntT[kb]);
@@ -383,19 +401,10 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
           break;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        // (ltag: also as data-tagged 16-B granules {value, tag_gen}, the columns < 16 (kb + 1) a consumer's product
-        // reads, which it polls directly instead of the flag)
-        const Sc1Mem mT(ltag ? ltag + (size_t)k * NB * NB * 2 : Linv, (unsigned)(NB * NB * 16));
-        const double tagd = __longlong_as_double((long long)tag_gen);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int e = lane + 64 * q, rr = 16 * kb + (e >> 5), cc = 2 * (e & 31);
-          const f64x2 v = *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc);
-          mI.st2(rr * NB + cc, v);
-          if (ltag && cc < 16 * (kb + 1)) {
-            mT.st2(2 * (rr * NB + cc), f64x2{v[0], tagd});
-            mT.st2(2 * (rr * NB + cc + 1), f64x2{v[1], tagd});
-          }
+          mI.st2(rr * NB + cc, *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc));
         }
         if (lflag != PUBLISH_ONLY) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
