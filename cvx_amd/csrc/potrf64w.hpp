@@ -85,12 +85,14 @@ __device__ __forceinline__ void potrf64w_stage(const double* L, int ld, size_t o
 
 // Optional data-tagged copy of L^-1 (the chain's consumer polls it, k_dataflow.hip): granule (r, c) of block k's
 // L^-1 = {value, tag} at base[2 (64 r + c)], stored by whichever wave computes the entry, as soon as it is final.
+// The byte offset is split into a per-lane part (one VGPR for all of a wave's stores) and a wave-uniform part (an
+// SGPR), so the many store sites do not each keep a precomputed per-lane address alive.
 struct TagOut {
   double* base;  // nullptr: none
   double tag;
-  __device__ __forceinline__ void put(int r, int c, double v) const {
-    const Sc1Mem m(base, (unsigned)(NB * NB * 16));
-    m.st2(2 * (r * NB + c), f64x2{v, tag});
+  __device__ __forceinline__ void put(int lane_bytes, int uni_bytes, double v) const {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f64x2{v, tag}),
+                                           uniform_rsrc(base, (unsigned)(NB * NB * 16)), lane_bytes, uni_bytes, AUX_SC1);
   }
 };
 
@@ -121,9 +123,10 @@ __device__ __forceinline__ void p64w_X(Potrf64wSmem& sm, int kb, int j, int lane
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] *= sm.SV[kb][(lane >> 4) + 4 * i];  // row scales (C layout: row (lane>>4) + 4i)
   c16_store(sm.X + 16 * kb * P64_SP + 16 * j, P64_SP, acc, lane);
-  if (to.base) {
+  if (to.base) {  // granule (16 kb + (lane >> 4) + 4 i, 16 j + (lane & 15))
+    const int vo = ((lane >> 4) * NB + (lane & 15)) * 16;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) to.put(16 * kb + (lane >> 4) + 4 * i, 16 * j + (lane & 15), acc[i]);
+    for (int i = 0; i < 4; ++i) to.put(vo, ((16 * kb + 4 * i) * NB + 16 * j) * 16, acc[i]);
   }
 }
 // X_kb,kb = (L16^-T)' with the column scales, and the scales of the L16 block of S (L16 = L~16 diag(s))
@@ -136,7 +139,7 @@ __device__ __forceinline__ void p64w_Xdiag(Potrf64wSmem& sm, int kb, int lane, c
     const int e = lane + 64 * i, rr = e >> 4, cc = e & 15;
     const double x = ET[rr * P64_EP + cc] * sv[cc];
     sm.X[(o + cc) * P64_SP + o + rr] = x;
-    if (to.base) to.put(o + cc, o + rr, x);
+    if (to.base) to.put(((lane & 15) * NB + (lane >> 4)) * 16, (o * NB + o + 4 * i) * 16, x);  // granule (o + cc, o + rr)
     double* sd = sm.S + (o + rr) * P64_SP + o + cc;
     *sd = (cc <= rr) ? *sd * sv[cc] : 0.0;
   }
