@@ -45,20 +45,6 @@ namespace {
 __device__ __forceinline__ int rz_poll(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void rz_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// thread 0: wait until flag[idx] >= want (false: the launch aborted, or this wait timed out and aborted it)
-__device__ __noinline__ bool rz_wait(const int* flag, int idx, int want, int* abortw) {
-  const unsigned long long t0 = spin_clock();
-  for (unsigned spins = 0;; ++spins) {
-    if (rz_poll(flag + idx) >= want) return true;
-    if ((spins & 15) == 15 && rz_poll(abortw)) return false;
-    if (spin_expired(spins, t0)) {
-      __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
 struct RzShared {
   int tile[RZ_LIST];             // claimed tiles, (I << 16) | J
   int nt, ok, stop, nred;
@@ -90,19 +76,36 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
   const unsigned dbytes = (unsigned)(ldS * 8);
   const Sc1Mem dc((k & 1) ? a.d1 : a.d0, dbytes), dn((k & 1) ? a.d0 : a.d1, dbytes);
   const Sc1Mem Sk(a.S + (size_t)(k & 1) * nbn * ldS, (unsigned)((size_t)nbn * ldS * 8));
-  if (tid == 0) {
+  // wave 0: lane q < 2 nb polls the flag of block q & 1 ? J : I of tile q >> 1, all of them in flight together
+  // (2 nb <= 2 RZ_MT < 64), until every one has reached sweep k
+  if (wid == 0) {
+    const bool act = lane < 2 * nb;
+    const int X = act ? ((lane & 1) ? (tiles[lane >> 1] & 0xffff) : (tiles[lane >> 1] >> 16)) : 0;
     bool ok = true;
     if (k > 0) {
-      for (int t = 0; t < nb && ok; ++t) {
-        const int I = tiles[t] >> 16, J = tiles[t] & 0xffff;
-        ok = rz_wait(a.dver, I, k, a.abortw) && rz_wait(a.dver, J, k, a.abortw);
+      const unsigned long long t0 = spin_clock();
+      for (unsigned spins = 0;; ++spins) {
+        const bool mine = !act || rz_poll(a.dver + X) >= k;
+        if (__ballot(!mine) == 0) break;
+        if ((spins & 15) == 15 && rz_poll(a.abortw)) {
+          ok = false;
+          break;
+        }
+        if (spin_expired(spins, t0)) {
+          if (lane == 0) __hip_atomic_store(a.abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
     }
-    sh.ok = ok;
-    // rho[k-1] is complete here (header): sweep k runs while it exceeds 1e-6
-    sh.stop = ok && k > 0 &&
-              !(__longlong_as_double((long long)__hip_atomic_load(&a.ctrl->ruiz_rho[k - 1], __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT)) > 1e-6);
+    if (lane == 0) {
+      sh.ok = ok;
+      // rho[k-1] is complete here (header): sweep k runs while it exceeds 1e-6
+      sh.stop = ok && k > 0 &&
+                !(__longlong_as_double((long long)__hip_atomic_load(&a.ctrl->ruiz_rho[k - 1], __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT)) > 1e-6);
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   __syncthreads();
@@ -161,28 +164,17 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
   }
   rz_drain();
   __syncthreads();
-  // contributions (all atomics in flight, then the tests): the one completing a block reduces it
-  if (tid == 0) {
+  // contributions, one lane of wave 0 per (tile, block), all in flight together: the one completing a block reduces it
+  if (wid == 0) {
     const int full = (k + 1) * nbn - 1;
-    int oi[MT], oj[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      oi[t] = oj[t] = -1;
-      if (t < nb) {
-        const int I = tiles[t] >> 16, J = tiles[t] & 0xffff;
-        oi[t] = __hip_atomic_fetch_add(a.cnt + I, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (I != J) oj[t] = __hip_atomic_fetch_add(a.cnt + J, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    int nr = 0;
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      if (t < nb) {
-        if (oi[t] == full) sh.redX[nr++] = tiles[t] >> 16;
-        if (oj[t] == full) sh.redX[nr++] = tiles[t] & 0xffff;
-      }
-    }
-    sh.nred = nr;
+    const int I = lane < 2 * nb ? tiles[lane >> 1] >> 16 : 0, J = lane < 2 * nb ? tiles[lane >> 1] & 0xffff : 0;
+    const bool act = lane < 2 * nb && !((lane & 1) && I == J);  // (a diagonal tile contributes to its block once)
+    const int X = (lane & 1) ? J : I;
+    bool red = false;
+    if (act) red = __hip_atomic_fetch_add(a.cnt + X, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == full;
+    const unsigned long long mask = __ballot(red);
+    if (red) sh.redX[__popcll(mask & ((1ull << lane) - 1))] = X;
+    if (lane == 0) sh.nred = __popcll(mask);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   __syncthreads();
