@@ -521,7 +521,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
                 }
               }
             }
-            if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
             for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
             df_put(ps.X, vl);  // (POTRF's L^-1 workspace and tile: free until the reset / the batch below)
@@ -544,6 +543,9 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 cs.Sa[(wr * 32 + mi * 16 + (lane >> 4) + 4 * r) * DF_SP + wc * 32 + nj * 16 + (lane & 15)] = acc[mi][nj][r];
+          // the row-blocks of L_kk^-1 published by now (after this panel's MFMAs, so the batch below takes as many as
+          // it can)
+          if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
         // A_b,k and D_b with every panel < k applied (state >= k), and the rhs block b with all earlier TRSM
         // updates: one wait for both states, then every load in flight together (minus L_b,k w_k inside POTRF(b);
