@@ -123,7 +123,8 @@ struct cvxg_ctx {
   // Ruiz: every sweep in one persistent launch (k_ruiz.hip; CVXG_RUIZ_LOOP=0: two launches per sweep)
   int ruiz_loop = 1;
   int ruiz_wg = 0;              // its workgroups (0: one per CU; CVXG_RUIZ_WG, tests: fewer -> streamed tiles)
-  double* ruiz_S = nullptr;     // its two parity buffers of partials (2 nblk x np)
+  double* ruiz_S = nullptr;     // its data-tagged granules (ruiz_loop_doubles)
+  unsigned long long ruiz_gen = 0;  // its launch generation (the granules' tags)
   int* ruiz_work = nullptr;     // its counters and flags (ruiz_loop_work_ints)
   int small_piv = 0;            // the last first attempt's stop row (DevCtrl::small_piv, or chol_info)
   int have_sparse = 0;          // set_ineq found sparse rows: the SYRK runs over As / wd / mdp
@@ -747,11 +748,8 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr, const do
 static void ruiz_sweeps(cvxg_ctx* ctx, int k0, int k1) {
   hipStream_t s = ctx->s;
   if (ctx->ruiz_loop) {  // the whole loop in one launch: k0 = 0, k1 = RUIZ_MAX always
-    const int nbn = (ctx->n + NB - 1) / NB;
-    launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl, ctx->ruiz1, ctx->ruiz_work, ruiz_loop_work_ints(nbn));
-    launch_ruiz_loop(s, ctx->H, ctx->np, ctx->n, ctx->ruiz0, ctx->ruiz1, ctx->ruiz_S, ctx->ctrl, ctx->ruiz_work,
-                     ctx->ruiz_wg > 0 ? ctx->ruiz_wg : ctx->ncu);
-    launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl, RUIZ_MAX, ctx->ruiz_work + 1);
+    launch_ruiz_loop(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->ruiz_S, ctx->ruiz_work, ctx->dfin, ctx->ctrl,
+                     ctx->ruiz_wg > 0 ? ctx->ruiz_wg : ctx->ncu, ++ctx->ruiz_gen);
     return;
   }
   if (k0 == 0) launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl);
@@ -1714,7 +1712,8 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   if (const char* e = getenv("CVXG_RUIZ_WG")) ctx->ruiz_wg = std::max(0, atoi(e));
   if (!ruiz_loop_fits((n + NB - 1) / NB)) ctx->ruiz_loop = 0;
   if (ctx->ruiz_loop) {
-    CHK(dalloc(ctx, &ctx->ruiz_S, 2 * (size_t)ctx->nblk * np));
+    CHK(dalloc(ctx, &ctx->ruiz_S, ruiz_loop_doubles(ctx->nblk)));
+    HIPC(ctx, hipMemset(ctx->ruiz_S, 0, ruiz_loop_doubles(ctx->nblk) * sizeof(double)));
     CHK(dalloc(ctx, &ctx->ruiz_work, ruiz_loop_work_ints(ctx->nblk)));
   }
   CHK(dalloc(ctx, &ctx->spart,

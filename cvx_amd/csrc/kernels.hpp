@@ -83,13 +83,15 @@ void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np
                            double* S, DevCtrl* ctrl, int k);
 void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl, int k1,
                        const int* abortw = nullptr /* k_ruiz_loop's abort word: set -> ruiz_sweeps = -2 */);
-// Every sweep in one persistent launch of nwg workgroups (k_ruiz.hip): the same d, rho and sweep count as
-// launch_ruiz_sweep_tri for k = 0 .. RUIZ_MAX-1; S = 2 nbn x (nbn 64) partials, work = ruiz_loop_work_ints(nbn) ints
-// zeroed by launch_ruiz_init.  Only while ruiz_loop_fits(nbn).
+// Every sweep in one persistent launch of nwg workgroups (k_ruiz.hip), then dfin and ruiz_sweeps: the same d, rho
+// and sweep count as launch_ruiz_sweep_tri for k = 0 .. RUIZ_MAX-1 + launch_ruiz_final.  gbuf =
+// ruiz_loop_doubles(nbn) doubles of data-tagged granules, work = ruiz_loop_work_ints(nbn) ints; gen: nonzero, new
+// per launch on the same buffers.  Only while ruiz_loop_fits(nbn).
 size_t ruiz_loop_work_ints(int nbn);
+size_t ruiz_loop_doubles(int nbn);
 bool ruiz_loop_fits(int nbn);
-void launch_ruiz_loop(hipStream_t s, const double* H, int ld, int n, double* d0, double* d1, double* S, DevCtrl* ctrl,
-                      int* work, int nwg);
+void launch_ruiz_loop(hipStream_t s, const double* H, int ld, int n, int np, double* gbuf, int* work, double* dfin,
+                      DevCtrl* ctrl, int nwg, unsigned long long gen);
 // L[i][j] = d_i d_j H_ij (+reg on the diagonal), lower triangle; padded diagonal = 1.
 void launch_form_q(hipStream_t s, const double* H, double* L, int ld, int n, int np, const double* d,
                    const DevCtrl* ctrl);
