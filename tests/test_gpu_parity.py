@@ -1873,12 +1873,13 @@ def test_speculative_next_evaluation_bitwise(mods):
 
 
 @pytest.mark.parametrize("n,m", [(384, 700), (1024, 2048)])
-def test_ruiz_lookahead_equals_full_loop(mods, n, m):
-    """The Newton step first launches only the Ruiz sweeps the previous step needed + 1 (cvxg.cpp: ruiz_lookahead)
-    and launches more while the loop is not done.  Every lookahead -- all 20 sweeps, one sweep, exactly the count,
-    one short -- gives bitwise the same dx and sweep count (MatrixUtils.scala:240-268), and only the short ones
-    launch more."""
+def test_ruiz_lookahead_equals_full_loop(mods, monkeypatch, n, m):
+    """The multi-launch Ruiz form (CVXG_RUIZ_LOOP=0; the one-launch loop has nothing to look ahead of): the Newton
+    step first launches only the sweeps the previous step needed + 1 (cvxg.cpp: ruiz_lookahead) and launches more
+    while the loop is not done.  Every lookahead -- all 20 sweeps, one sweep, exactly the count, one short -- gives
+    bitwise the same dx and sweep count (MatrixUtils.scala:240-268), and only the short ones launch more."""
     Z, SP, Engine, O = mods
+    monkeypatch.setenv("CVXG_RUIZ_LOOP", "0")
     spec = Z.random_qp(n, m, instance=23)
     eng = _engine(Engine, spec)
     pars = SP.standardParams()
