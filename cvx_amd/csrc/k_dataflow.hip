@@ -500,6 +500,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           __syncthreads();
           if (!s_ok) return;
+          mark(k, 2, 3);  // trace: the b-2 panel's inputs are in (field 3 of the fix record)
           const int wr = wv >> 1, wc = wv & 1;
           d4f acc[2][2];
           {
@@ -546,6 +547,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           // the row-blocks of L_kk^-1 published by now (after this panel's MFMAs, so the batch below takes as many as
           // it can)
           if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          mark(k, 0, 3);  // trace: the b-2 panel applied (field 3 of POTRF(k)'s record)
         } else {
         // A_b,k and D_b with every panel < k applied (state >= k), and the rhs block b with all earlier TRSM
         // updates: one wait for both states, then every load in flight together (minus L_b,k w_k inside POTRF(b);

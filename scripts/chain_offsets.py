@@ -15,9 +15,11 @@ for k in range(2,nb-2):
     F=ch[k+1,0,0]
     fix0=ch[k,2,0]; fix1=ch[k,2,1]; fix2=ch[k,2,2]  # fix of block k+1 (waits POTRF(k) done)
     s2=ch[k+1,0,1]
-    rows.append([us(B-A),us(stg0-A),us(C-A),us(s2-A) if s2>A else np.nan,us(D-A) if D>A else np.nan,us(E-A),us(F-A),us(fix0-F) if fix0>0 else 0, us(fix1-F) if fix1>0 else 0,us(fix2-F) if fix2>0 else 0])
+    b2in=ch[k,2,3]; b2done=ch[k,0,3]  # chain-owned b-2 staging (k_dataflow.hip own_b2): inputs in / panel applied
+    rows.append([us(B-A),us(stg0-A),us(C-A),us(s2-A) if s2>A else np.nan,us(D-A) if D>A else np.nan,us(E-A),us(F-A),us(fix0-F) if fix0>0 else 0, us(fix1-F) if fix1>0 else 0,us(fix2-F) if fix2>0 else 0,
+                 us(b2in-A) if b2in>0 else np.nan, us(b2done-A) if b2done>0 else np.nan])
 r=np.array(rows)
-names=['potrf_done','stage_begin(k+1)','staged(k+1)','slice2done(k+1)','lastrow(k+1)','slices_done(k+1)','potrf_start(k+1)','fix0(k+1)-F','fix1-F','fix2-F']
+names=['potrf_done','stage_begin(k+1)','staged(k+1)','slice2done(k+1)','lastrow(k+1)','slices_done(k+1)','potrf_start(k+1)','fix0(k+1)-F','fix1-F','fix2-F','b2_inputs(k+1)','b2_applied(k+1)']
 for i,nm in enumerate(names):
     print(f"{nm:22s} mean {np.nanmean(r[:,i]):7.2f} med {np.nanmedian(r[:,i]):7.2f} min {np.nanmin(r[:,i]):7.2f} max {np.nanmax(r[:,i]):7.2f}")
 order=np.frombuffer(raw[8:8+4*nq],dtype=np.uint32)
