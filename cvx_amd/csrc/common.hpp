@@ -33,6 +33,7 @@ struct DevCtrl {
   int small_piv;                  // k_chol_dataflow with early_min > 0 (regularizedCholesky's first attempt): 1-based
                                   // first row of the 16-column block where it stopped on min diag(L) <= early_min
                                   // (min_diag holds that block's value); 0 = it did not stop
+  int ruiz_abort;                 // k_ruiz_loop's abort word of its last launch (0 = none; else which wait gave up)
 };
 
 enum {

@@ -840,7 +840,8 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   ctx->spec_eval_launched = false;
   if (ctx->hctrl->df_status != 0)
     return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
-  if (ctx->hctrl->ruiz_sweeps == -2) return set_err(ctx, CVXG_E_HIP, "Ruiz loop: dependency wait timed out");
+  if (ctx->hctrl->ruiz_sweeps == -2)
+    return set_err(ctx, CVXG_E_HIP, "Ruiz loop: dependency wait timed out (abort word 0x%x)", ctx->hctrl->ruiz_abort);
   if (ctx->df_trace) {  // instrumentation only: task order + timeline of this factorization
     std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 3 * ctx->nblk));
     std::vector<unsigned> ord(ctx->df_ntasks);

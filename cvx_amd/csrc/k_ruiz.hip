@@ -88,7 +88,7 @@ struct RzArgs {
 // false on abort / timeout (abort word raised).
 template <int G, class Idx>
 __device__ __forceinline__ bool rz_wait_all(f64x2 (&g)[G], unsigned need, double tag, const Gran& src, Idx idx,
-                                            int* abortw) {
+                                            int* abortw, int code) {
 #pragma unroll
   for (int i = 0; i < G; ++i)
     if (need >> i & 1) g[i] = src.ld(idx(i));
@@ -101,7 +101,7 @@ __device__ __forceinline__ bool rz_wait_all(f64x2 (&g)[G], unsigned need, double
     if (!miss) return true;
     if ((spins & 15) == 15 && rz_poll(abortw)) return false;
     if (spin_expired(spins, t0)) {
-      __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(abortw, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -109,6 +109,22 @@ __device__ __forceinline__ bool rz_wait_all(f64x2 (&g)[G], unsigned need, double
     for (int i = 0; i < G; ++i)
       if (miss >> i & 1) g[i] = src.ld(idx(i));
   }
+}
+
+// Wave 0 probes one sentinel granule per producer (lane l < np: index idx(l)) until each carries `tag`, so the block
+// polls a few granules instead of every thread polling all of its own (which floods the memory system while it
+// waits); the full loads behind it then find their tags in place, normally at the first try.  False: abort/timeout.
+template <class Idx>
+__device__ __forceinline__ bool rz_probe(int np, double tag, const Gran& src, Idx idx, int* abortw, int code) {
+  const int lane = threadIdx.x & 63;
+  bool ok = true;
+  for (int l0 = 0; l0 < np && ok; l0 += 64) {
+    f64x2 gq[1];
+    const unsigned nq = (l0 + lane < np) ? 1u : 0u;
+    ok = rz_wait_all<1>(gq, nq, tag, src, [&](int) { return idx(l0 + lane); }, abortw, code);
+    ok = __ballot(!ok) == 0;
+  }
+  return ok;
 }
 
 // Block-uniform verdict of per-thread waits (false anywhere -> false everywhere); a barrier on both sides.
@@ -149,7 +165,7 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
     const double tr = rz_tag(a.gen, k - 1);
     f64x2 gr[2];
     const unsigned nr = (lane < nbn ? 1u : 0u) | (lane + 64 < nbn ? 2u : 0u);
-    ok = rz_wait_all<2>(gr, nr, tr, rp, [&](int i) { return lane + 64 * i; }, a.abortw);
+    ok = rz_wait_all<2>(gr, nr, tr, rp, [&](int i) { return lane + 64 * i; }, a.abortw, 0x10000 | k << 8);
     double m = 0.0;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -159,7 +175,12 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
   } else if (tid == 0) {
     sh.stop = 0;
   }
-  ok = ok && rz_wait_all<G>(gd, need, tk, dk, didx, a.abortw);
+  if (k > 0 && wid == 0)  // sentinel: the last row of each needed block (2 nb of them)
+    ok = ok && rz_probe(2 * nb, tk, dk,
+                        [&](int l) { return ((l & 1) ? (tiles[l >> 1] & 0xffff) : (tiles[l >> 1] >> 16)) * NB + NB - 1; },
+                        a.abortw, 0x50000 | k << 8);
+  if (k > 0 && !rz_agree(ok, sh)) return false;
+  ok = ok && rz_wait_all<G>(gd, need, tk, dk, didx, a.abortw, 0x20000 | k << 8);
   if (!rz_agree(ok, sh)) return false;
   if (sh.stop) return false;
 #pragma unroll
@@ -229,6 +250,9 @@ __device__ __forceinline__ bool rz_reduce(int X, int k, const RzArgs& a, RzShare
   // k_ruiz_rows' order: s0..s3 over P, P + 4, P + 8, P + 12 while P + 12 < nbn (P += 16), then the tail into s0
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   bool ok = true, main = true;
+  if (wid == 0)  // sentinel: row X*64 of every producer's slot S[P][rows of X]
+    ok = rz_probe(nbn, tk, S, [&](int P) { return P * ldS + X * NB; }, a.abortw, 0x60000 | k << 8 | X);
+  if (!rz_agree(ok, sh)) return false;
   for (int half = 0; half < 2 && ok; ++half) {
     const int P0 = wid + 64 * half;
     if (!live || P0 >= nbn) break;
@@ -237,7 +261,8 @@ __device__ __forceinline__ bool rz_reduce(int X, int k, const RzArgs& a, RzShare
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (P0 + 4 * i < nbn) nd |= 1u << i;
-    ok = rz_wait_all<16>(gp, nd, tk, S, [&](int i) { return (P0 + 4 * i) * ldS + row; }, a.abortw);
+    ok = rz_wait_all<16>(gp, nd, tk, S, [&](int i) { return (P0 + 4 * i) * ldS + row; }, a.abortw,
+                         0x30000 | k << 8 | X);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int P = P0 + 16 * c;
@@ -257,7 +282,7 @@ __device__ __forceinline__ bool rz_reduce(int X, int k, const RzArgs& a, RzShare
   // d^(k) of the block's rows (wave 0; the workgroup's own diagonal tile polled it this sweep)
   f64x2 gdi[1];
   const unsigned ndi = (wid == 0 && live && k > 0) ? 1u : 0u;
-  ok = ok && rz_wait_all<1>(gdi, ndi, tk, dk, [&](int) { return row; }, a.abortw);
+  ok = ok && rz_wait_all<1>(gdi, ndi, tk, dk, [&](int) { return row; }, a.abortw, 0x40000 | k << 8 | X);
   sh.red[wid][lane] = (s0 + s1) + (s2 + s3);
   if (!rz_agree(ok, sh)) return false;
   if (wid == 0) {
@@ -386,7 +411,10 @@ __global__ __launch_bounds__(256) void k_ruiz_loop_final(const double* __restric
   const int K = sK;
   const f64x2* dK = reinterpret_cast<const f64x2*>(gbuf) + (size_t)K * ldS;
   for (int i = tid; i < np; i += 256) dfin[i] = (i < (int)ldS) ? dK[i][0] : 1.0;
-  if (tid == 0) ctrl->ruiz_sweeps = work[1] ? -2 : K;
+  if (tid == 0) {
+    ctrl->ruiz_sweeps = work[1] ? -2 : K;
+    ctrl->ruiz_abort = work[1];
+  }
 }
 
 void launch_ruiz_loop(hipStream_t s, const double* H, int ld, int n, int np, double* gbuf, int* work, double* dfin,
