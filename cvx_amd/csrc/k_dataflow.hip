@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     Potrf64wSmem& ps = cs.p;
     const int lane = tid & 63, wv = tid >> 6;
     auto mark = [&](int k, int step, int field) {
-      if (trace && tid == 0) trace[4 * (size_t)(ntasks + 3 * k + step) + field] = __builtin_amdgcn_s_memrealtime();
+      if (trace && tid == 0) trace[4 * (size_t)(ntasks + 4 * k + step) + field] = __builtin_amdgcn_s_memrealtime();
     };
     auto publish = [&](int idx, int v) {
       df_drain();  // every storing wave: its sc1 stores have left
@@ -820,7 +820,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           __hip_atomic_store(state + df_tri(b, k), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       };
       if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre,
-                                   kTag ? ltag : nullptr, tag_gen, kDpp)) {
+                                   kTag ? ltag : nullptr, tag_gen, kDpp,
+                                   trace ? trace + 4 * (size_t)(ntasks + 4 * b + 3) : nullptr)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }

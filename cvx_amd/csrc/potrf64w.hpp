@@ -351,7 +351,7 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
                                                 Fix fix = Fix(), double early_min = 0.0, Pre pre = Pre(),
                                                 double* ltag = nullptr, unsigned long long tag_gen = 0,
-                                                bool dpp_sweep = false) {
+                                                bool dpp_sweep = false, unsigned long long* rb_stamp = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -412,6 +412,7 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
         if (lflag != PUBLISH_ONLY) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (lane == 0) __hip_atomic_store(lflag, kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (rb_stamp && lane == 0) rb_stamp[kb] = __builtin_amdgcn_s_memrealtime();  // (instrumentation)
         }
       }
       if (kb < 3) {
