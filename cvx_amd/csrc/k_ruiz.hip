@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256, 1) void k_ruiz_loop(const double* __restrict__
   RzArgs a{n, nbn, gbuf, gbuf + (RUIZ_MAX + 1) * ldS * 2, gbuf + (RUIZ_MAX + 1 + (size_t)nbn) * ldS * 2, work + 1, gen};
   for (int k = 0; k < RUIZ_MAX; ++k) {
     if (!rz_batch<RZ_MT>(h, nreg, sh.tile, k, a, sh, true)) return;
-    for (int b = RZ_MT; b < nt; ++b) {
+    for (int b = nreg; b < nt; ++b) {  // (the claims beyond the first batch: its register tiles are 0 .. nreg-1)
       f64x2 hs[1][8];
       rz_load_tile(hs[0], H, ld, sh.tile[b]);
       if (!rz_batch<1>(hs, 1, sh.tile + b, k, a, sh, false)) return;
