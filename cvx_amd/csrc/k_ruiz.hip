@@ -88,10 +88,12 @@ struct RzArgs {
 // false on abort / timeout (abort word raised).
 template <int G, class Idx>
 __device__ __forceinline__ bool rz_wait_all(f64x2 (&g)[G], unsigned need, double tag, const Gran& src, Idx idx,
-                                            int* abortw, int code) {
+                                            int* abortw, int code, bool loaded = false) {
+  if (!loaded) {
 #pragma unroll
-  for (int i = 0; i < G; ++i)
-    if (need >> i & 1) g[i] = src.ld(idx(i));
+    for (int i = 0; i < G; ++i)
+      if (need >> i & 1) g[i] = src.ld(idx(i));
+  }
   const unsigned long long t0 = spin_clock();
   for (unsigned spins = 0;; ++spins) {
     unsigned miss = 0;
@@ -104,27 +106,11 @@ __device__ __forceinline__ bool rz_wait_all(f64x2 (&g)[G], unsigned need, double
       __hip_atomic_store(abortw, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(2);
 #pragma unroll
     for (int i = 0; i < G; ++i)
       if (miss >> i & 1) g[i] = src.ld(idx(i));
   }
-}
-
-// Wave 0 probes one sentinel granule per producer (lane l < np: index idx(l)) until each carries `tag`, so the block
-// polls a few granules instead of every thread polling all of its own (which floods the memory system while it
-// waits); the full loads behind it then find their tags in place, normally at the first try.  False: abort/timeout.
-template <class Idx>
-__device__ __forceinline__ bool rz_probe(int np, double tag, const Gran& src, Idx idx, int* abortw, int code) {
-  const int lane = threadIdx.x & 63;
-  bool ok = true;
-  for (int l0 = 0; l0 < np && ok; l0 += 64) {
-    f64x2 gq[1];
-    const unsigned nq = (l0 + lane < np) ? 1u : 0u;
-    ok = rz_wait_all<1>(gq, nq, tag, src, [&](int) { return idx(l0 + lane); }, abortw, code);
-    ok = __ballot(!ok) == 0;
-  }
-  return ok;
 }
 
 // Block-uniform verdict of per-thread waits (false anywhere -> false everywhere); a barrier on both sides.
@@ -158,6 +144,10 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
     const int e = tid + 256 * i, t = e / (2 * NB), w = (e / NB) & 1;
     return (w ? (tiles[t] & 0xffff) : (tiles[t] >> 16)) * NB + (e & (NB - 1));
   };
+  // d loads first (in flight while wave 0 polls the stop test)
+#pragma unroll
+  for (int i = 0; i < G; ++i)
+    if (need >> i & 1) gd[i] = dk.ld(didx(i));
   // the stop test: rho[k-1] = max_X rhop[k-1][X], polled by wave 0 (k >= 2; rho[0] = 1)
   bool ok = true;
   if (check_stop && k >= 2 && wid == 0) {
@@ -175,12 +165,7 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
   } else if (tid == 0) {
     sh.stop = 0;
   }
-  if (k > 0 && wid == 0)  // sentinel: the last row of each needed block (2 nb of them)
-    ok = ok && rz_probe(2 * nb, tk, dk,
-                        [&](int l) { return ((l & 1) ? (tiles[l >> 1] & 0xffff) : (tiles[l >> 1] >> 16)) * NB + NB - 1; },
-                        a.abortw, 0x50000 | k << 8);
-  if (k > 0 && !rz_agree(ok, sh)) return false;
-  ok = ok && rz_wait_all<G>(gd, need, tk, dk, didx, a.abortw, 0x20000 | k << 8);
+  ok = ok && rz_wait_all<G>(gd, need, tk, dk, didx, a.abortw, 0x20000 | k << 8, true);
   if (!rz_agree(ok, sh)) return false;
   if (sh.stop) return false;
 #pragma unroll
@@ -250,9 +235,6 @@ __device__ __forceinline__ bool rz_reduce(int X, int k, const RzArgs& a, RzShare
   // k_ruiz_rows' order: s0..s3 over P, P + 4, P + 8, P + 12 while P + 12 < nbn (P += 16), then the tail into s0
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   bool ok = true, main = true;
-  if (wid == 0)  // sentinel: row X*64 of every producer's slot S[P][rows of X]
-    ok = rz_probe(nbn, tk, S, [&](int P) { return P * ldS + X * NB; }, a.abortw, 0x60000 | k << 8 | X);
-  if (!rz_agree(ok, sh)) return false;
   for (int half = 0; half < 2 && ok; ++half) {
     const int P0 = wid + 64 * half;
     if (!live || P0 >= nbn) break;
