@@ -483,32 +483,24 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         d4f dacc[NBLK16];
         if (kB2 && b >= 2) {
           // Panel j = b-2 of block row b on this workgroup (the tasks UPDATE(b,b,j) and UPDATE(b,k,j), not in the
-          // worker list): A_b,k and D_b with every panel < j (state >= j), L_b,j (worker TRSM(b,j)), L_k,j (the other
-          // chain workgroup's slices), the rhs block with TRSM(b, i <= j)'s updates -- one wait, every load in
-          // flight together.  The MFMA sequences are the workers' (df_update's K = 0..63 chain), so the factor is
+          // worker list), in two waits (below).  The MFMA sequences are the workers' (df_update's K = 0..63 chain), so the factor is
           // bitwise the same; the worker -> state word -> staging hop of both tiles is gone from the chain.
           const int j = b - 2;
+          // (1) A_b,k and D_b with every panel < j: final long before (the workers' updates of panel j-1), so their
+          // loads go out first and land while (2) waits for the two fresh L tiles
           if (tid == 0) {
-            const int v0 = df_poll(state + df_tri(b, k)), v1 = df_poll(state + df_tri(b, b)),
-                      v2 = df_poll(rhscnt + b), v3 = df_poll(state + df_tri(b, j)), v4 = df_poll(state + df_tri(k, j));
+            const int v0 = df_poll(state + df_tri(b, k)), v1 = df_poll(state + df_tri(b, b));
             s_ok = (v0 >= j || df_wait(state, df_tri(b, k), j, abortw, ctrl)) &&
-                   (v1 >= j || df_wait(state, df_tri(b, b), j, abortw, ctrl)) &&
-                   (v3 >= j + 1 || df_wait(state, df_tri(b, j), j + 1, abortw, ctrl)) &&
-                   (v4 >= j + 1 || df_wait(state, df_tri(k, j), j + 1, abortw, ctrl)) &&
-                   (v2 >= k || df_wait(rhscnt, b, k, abortw, ctrl));
+                   (v1 >= j || df_wait(state, df_tri(b, b), j, abortw, ctrl));
           }
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           __syncthreads();
           if (!s_ok) return;
-          mark(k, 2, 3);  // trace: the b-2 panel's inputs are in (field 3 of the fix record)
           const int wr = wv >> 1, wc = wv & 1;
           d4f acc[2][2];
+          const bool fold = qf.H && j == 0;  // block 2: A_2,1 and D_2 are first read here (Q formed from H)
+          df_load_c(acc, mA, ld, b, k, fold, qf, wr, wc, lane);
           {
-            f64x2 vl[NB * NB / 512], vk[NB * NB / 512];
-            df_load(vl, Sc1Mem(L + (size_t)b * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
-            df_load(vk, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
-            const bool fold = qf.H && j == 0;  // block 2: A_2,1 and D_2 are first read here (Q formed from H)
-            df_load_c(acc, mA, ld, b, k, fold, qf, wr, wc, lane);
             const Sc1Mem mD(const_cast<double*>(fold ? qf.H : L) + (size_t)b * NB * ld + (size_t)b * NB, tile_bytes(ld));
 #pragma unroll
             for (int q = 0; q < NBLK16; ++q) {
@@ -522,6 +514,23 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
                 }
               }
             }
+          }
+          // (2) L_b,j (worker TRSM(b,j)), L_k,j (the other chain workgroup's TRSM, published inside its POTRF(k)) and
+          // the rhs block with TRSM(b, i <= j)'s updates
+          if (tid == 0) {
+            const int v2 = df_poll(rhscnt + b), v3 = df_poll(state + df_tri(b, j)), v4 = df_poll(state + df_tri(k, j));
+            s_ok = (v3 >= j + 1 || df_wait(state, df_tri(b, j), j + 1, abortw, ctrl)) &&
+                   (v4 >= j + 1 || df_wait(state, df_tri(k, j), j + 1, abortw, ctrl)) &&
+                   (v2 >= k || df_wait(rhscnt, b, k, abortw, ctrl));
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          __syncthreads();
+          if (!s_ok) return;
+          mark(k, 2, 3);  // trace: the b-2 panel's inputs are in (field 3 of the fix record)
+          {
+            f64x2 vl[NB * NB / 512], vk[NB * NB / 512];
+            df_load(vl, Sc1Mem(L + (size_t)b * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
+            df_load(vk, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
             const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
             for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
             df_put(ps.X, vl);  // (POTRF's L^-1 workspace and tile: free until the reset / the batch below)
