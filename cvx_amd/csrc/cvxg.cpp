@@ -121,7 +121,9 @@ struct cvxg_ctx {
   bool h_full = true;           // the current H holds its upper triangle too
   double* hsv_part = nullptr;   // symv partials (nblk x np)
   // Ruiz: every sweep in one persistent launch (k_ruiz.hip; CVXG_RUIZ_LOOP=0: two launches per sweep)
-  int ruiz_loop = 1;
+  int ruiz_loop = 0;            // (opt-in until it beats the multi-launch form: DESIGN.md §7)
+  unsigned long long* ruiz_trace = nullptr;  // CVXG_RUIZ_TRACE=<file>: per-workgroup sweep stamps of the last loop
+  std::string ruiz_trace_path;
   int ruiz_wg = 0;              // its workgroups (0: one per CU; CVXG_RUIZ_WG, tests: fewer -> streamed tiles)
   double* ruiz_S = nullptr;     // its data-tagged granules (ruiz_loop_doubles)
   unsigned long long ruiz_gen = 0;  // its launch generation (the granules' tags)
@@ -748,8 +750,18 @@ static int assemble_hessian(cvxg_ctx* ctx, const double* wts = nullptr, const do
 static void ruiz_sweeps(cvxg_ctx* ctx, int k0, int k1) {
   hipStream_t s = ctx->s;
   if (ctx->ruiz_loop) {  // the whole loop in one launch: k0 = 0, k1 = RUIZ_MAX always
-    launch_ruiz_loop(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->ruiz_S, ctx->ruiz_work, ctx->dfin, ctx->ctrl,
-                     ctx->ruiz_wg > 0 ? ctx->ruiz_wg : ctx->ncu, ++ctx->ruiz_gen);
+    const int nwg = ctx->ruiz_wg > 0 ? ctx->ruiz_wg : ctx->ncu;
+    launch_ruiz_loop(s, ctx->H, ctx->np, ctx->n, ctx->np, ctx->ruiz_S, ctx->ruiz_work, ctx->dfin, ctx->ctrl, nwg,
+                     ++ctx->ruiz_gen, ctx->ruiz_trace);
+    if (ctx->ruiz_trace) {  // instrumentation only
+      std::vector<unsigned long long> tr((size_t)nwg * RUIZ_MAX * 4);
+      if (copy_sync(ctx, tr.data(), ctx->ruiz_trace, tr.size() * 8, hipMemcpyDeviceToHost) == CVXG_OK)
+        if (FILE* f = fopen(ctx->ruiz_trace_path.c_str(), "wb")) {
+          fwrite(&nwg, 4, 1, f);
+          fwrite(tr.data(), 8, tr.size(), f);
+          fclose(f);
+        }
+    }
     return;
   }
   if (k0 == 0) launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl);
@@ -1711,6 +1723,12 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   CHK(dalloc(ctx, &ctx->hsv_part, (size_t)ctx->nblk * np));
   if (const char* e = getenv("CVXG_RUIZ_LOOP")) ctx->ruiz_loop = atoi(e) != 0;
   if (const char* e = getenv("CVXG_RUIZ_WG")) ctx->ruiz_wg = std::max(0, atoi(e));
+  if (const char* e = getenv("CVXG_RUIZ_TRACE")) {
+    ctx->ruiz_trace_path = e;
+    const int nwg = ctx->ruiz_wg > 0 ? ctx->ruiz_wg : std::max(ctx->ncu, 1);
+    CHK(dalloc(ctx, &ctx->ruiz_trace, (size_t)nwg * RUIZ_MAX * 4));
+    HIPC(ctx, hipMemset(ctx->ruiz_trace, 0, (size_t)nwg * RUIZ_MAX * 4 * 8));
+  }
   if (!ruiz_loop_fits((n + NB - 1) / NB)) ctx->ruiz_loop = 0;
   if (ctx->ruiz_loop) {
     CHK(dalloc(ctx, &ctx->ruiz_S, ruiz_loop_doubles(ctx->nblk)));

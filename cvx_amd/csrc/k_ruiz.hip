@@ -127,7 +127,7 @@ __device__ __forceinline__ bool rz_agree(bool mine, RzShared& sh) {
 // columns 2 c2, 2 c2 + 1).  False: stop (the loop is done) or abort.
 template <int MT>
 __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const int* tiles, int k, const RzArgs& a,
-                                         RzShared& sh, bool check_stop) {
+                                         RzShared& sh, bool check_stop, unsigned long long* dstamp = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int c2 = tid & 31, g = tid >> 5;
   const int nbn = a.nbn, ldS = nbn * NB;
@@ -168,6 +168,7 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
   ok = ok && rz_wait_all<G>(gd, need, tk, dk, didx, a.abortw, 0x20000 | k << 8, true);
   if (!rz_agree(ok, sh)) return false;
   if (sh.stop) return false;
+  if (dstamp && tid == 0) *dstamp = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
   for (int i = 0; i < G; ++i) {
     const int e = tid + 256 * i;
@@ -296,9 +297,11 @@ __device__ __forceinline__ void rz_load_tile(f64x2 (&h)[8], const double* H, int
 }  // namespace
 
 // work: [0] claim counter, [1] abort word -- zeroed by k_ruiz_loop_init
+// trace (instrumentation, CVXG_RUIZ_TRACE): per workgroup and sweep, 4 timestamps: batch start, its d in hand,
+// its tiles done, its reductions done (s_memrealtime, 100 MHz); [nwg][RUIZ_MAX][4]
 __global__ __launch_bounds__(256, 1) void k_ruiz_loop(const double* __restrict__ H, int ld, int n, int nbn,
                                                       double* __restrict__ gbuf, int* __restrict__ work, int batch,
-                                                      unsigned long long gen) {
+                                                      unsigned long long gen, unsigned long long* __restrict__ trace) {
   __shared__ RzShared sh;
   const int tid = threadIdx.x;
   const int ntiles = nbn * (nbn + 1) / 2;
@@ -342,8 +345,14 @@ __global__ __launch_bounds__(256, 1) void k_ruiz_loop(const double* __restrict__
   __syncthreads();
   const int nt = sh.nt, nown = sh.nown;
   RzArgs a{n, nbn, gbuf, gbuf + (RUIZ_MAX + 1) * ldS * 2, gbuf + (RUIZ_MAX + 1 + (size_t)nbn) * ldS * 2, work + 1, gen};
+  auto stamp = [&](int k, int f) {
+    if (trace && tid == 0) trace[((size_t)blockIdx.x * RUIZ_MAX + k) * 4 + f] = __builtin_amdgcn_s_memrealtime();
+  };
   for (int k = 0; k < RUIZ_MAX; ++k) {
-    if (!rz_batch<RZ_MT>(h, nreg, sh.tile, k, a, sh, true)) return;
+    stamp(k, 0);
+    if (!rz_batch<RZ_MT>(h, nreg, sh.tile, k, a, sh, true, trace ? trace + ((size_t)blockIdx.x * RUIZ_MAX + k) * 4 + 1 : nullptr))
+      return;
+    stamp(k, 2);
     for (int b = nreg; b < nt; ++b) {  // (the claims beyond the first batch: its register tiles are 0 .. nreg-1)
       f64x2 hs[1][8];
       rz_load_tile(hs[0], H, ld, sh.tile[b]);
@@ -351,6 +360,7 @@ __global__ __launch_bounds__(256, 1) void k_ruiz_loop(const double* __restrict__
     }
     for (int o = 0; o < nown; ++o)
       if (!rz_reduce(sh.own[o], k, a, sh)) return;
+    stamp(k, 3);
   }
 }
 
@@ -400,13 +410,13 @@ __global__ __launch_bounds__(256) void k_ruiz_loop_final(const double* __restric
 }
 
 void launch_ruiz_loop(hipStream_t s, const double* H, int ld, int n, int np, double* gbuf, int* work, double* dfin,
-                      DevCtrl* ctrl, int nwg, unsigned long long gen) {
+                      DevCtrl* ctrl, int nwg, unsigned long long gen, unsigned long long* trace) {
   const int nbn = (n + NB - 1) / NB;
   const int ntiles = nbn * (nbn + 1) / 2;
   const int batch = std::max(1, std::min(RZ_MT, (ntiles + nwg - 1) / nwg));
   const int rows = nbn * NB;
   k_ruiz_loop_init<<<(rows + 255) / 256, 256, 0, s>>>(gbuf, rows, work, gen);
-  k_ruiz_loop<<<nwg, 256, 0, s>>>(H, ld, n, nbn, gbuf, work, batch, gen);
+  k_ruiz_loop<<<nwg, 256, 0, s>>>(H, ld, n, nbn, gbuf, work, batch, gen, trace);
   k_ruiz_loop_final<<<1, 256, 0, s>>>(gbuf, nbn, np, dfin, ctrl, work, gen);
 }
 

@@ -91,7 +91,7 @@ size_t ruiz_loop_work_ints(int nbn);
 size_t ruiz_loop_doubles(int nbn);
 bool ruiz_loop_fits(int nbn);
 void launch_ruiz_loop(hipStream_t s, const double* H, int ld, int n, int np, double* gbuf, int* work, double* dfin,
-                      DevCtrl* ctrl, int nwg, unsigned long long gen);
+                      DevCtrl* ctrl, int nwg, unsigned long long gen, unsigned long long* trace = nullptr);
 // L[i][j] = d_i d_j H_ij (+reg on the diagonal), lower triangle; padded diagonal = 1.
 void launch_form_q(hipStream_t s, const double* H, double* L, int ld, int n, int np, const double* d,
                    const DevCtrl* ctrl);
