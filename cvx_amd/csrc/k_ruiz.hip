@@ -29,6 +29,7 @@
 #include <algorithm>
 
 #include "potrf64.hpp"
+#include "ruiz_tile.hpp"
 
 namespace cvxg {
 
@@ -71,7 +72,7 @@ struct RzShared {
   int own[RZ_OWN];               // blocks whose reduction this workgroup runs (its diagonal tiles)
   int nt, nown, ok, stop;
   double d[2 * RZ_MT][NB];       // d^(k) of the batch's blocks: tile t's I at 2t, J at 2t + 1
-  double cred[RZ_MT][4][NB];     // column partials per wave
+  double cred[RZ_MT][8][NB];     // column partials per row group
   double red[4][NB];
 };
 
@@ -181,33 +182,18 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
       const int I = tiles[t] >> 16, J = tiles[t] & 0xffff;
       const f64x2 dj = {sh.d[2 * t + 1][2 * c2], sh.d[2 * t + 1][2 * c2 + 1]};
       f64x2 csum = {0.0, 0.0};
-      double rs[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < 8; ++q) {  // ruiz_tile.hpp's arithmetic, as k_ruiz_tiles
         const double di = sh.d[2 * t][g + 8 * q];
         const f64x2 av = dj * h[t][q];
-        rs[q] = av[0] * av[0] + av[1] * av[1];
+        const double rs = rz_rowgroup_sum(av[0] * av[0] + av[1] * av[1]);
+        if (c2 == RZ_ROW_LANE) S.st(J * ldS + I * NB + g + 8 * q, rs, tk);
         const f64x2 bv = h[t][q] * di;
         csum = __builtin_elementwise_fma(bv, bv, csum);
       }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        double v = rs[q];
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        rs[q] = v;
-      }
-      if (c2 == 0) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) S.st(J * ldS + I * NB + g + 8 * q, rs[q], tk);
-      }
       if (I != J) {
-        csum[0] += __shfl_xor(csum[0], 32, 64);
-        csum[1] += __shfl_xor(csum[1], 32, 64);
-        if (lane < 32) {
-          sh.cred[t][wid][2 * c2] = csum[0];
-          sh.cred[t][wid][2 * c2 + 1] = csum[1];
-        }
+        sh.cred[t][g][2 * c2] = csum[0];
+        sh.cred[t][g][2 * c2 + 1] = csum[1];
       }
     }
   }
@@ -215,9 +201,12 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
   if (tid < NB) {
     for (int t = 0; t < nb; ++t) {
       const int I = tiles[t] >> 16, J = tiles[t] & 0xffff;
-      if (I != J)
-        S.st(I * ldS + J * NB + tid,
-             ((sh.cred[t][0][tid] + sh.cred[t][1][tid]) + sh.cred[t][2][tid]) + sh.cred[t][3][tid], tk);
+      if (I != J) {
+        double v = sh.cred[t][0][tid];
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v += sh.cred[t][r][tid];
+        S.st(I * ldS + J * NB + tid, v, tk);
+      }
     }
   }
   return true;

@@ -6,6 +6,7 @@
 #include <math.h>
 
 #include "kernels.hpp"
+#include "ruiz_tile.hpp"
 
 namespace cvxg {
 
@@ -571,7 +572,8 @@ void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl, double* 
 // triangle alone -- half the bytes per sweep.  Tile (I, J) writes
 //   S[J][i] = sum_{j in J} (d_j H_ij)^2   for its rows i in I      (row partials)
 //   S[I][j] = sum_{i in I} (d_i H_ij)^2   for its columns j in J   (column partials = rows of H_JI, I > J)
-// so every S[X][r] is written by exactly one tile, and k_ruiz_rows adds S[0..nbn)[r] in a fixed order.
+// so every S[X][r] is written by exactly one tile, and k_ruiz_rows adds S[0..nbn)[r] in a fixed order.  The per-tile
+// arithmetic is ruiz_tile.hpp's (shared with the one-launch loop, k_ruiz.hip).
 __global__ __launch_bounds__(256) void k_ruiz_tiles(const double* __restrict__ H, int ld, int nbn,
                                                     const double* __restrict__ dcur, double* __restrict__ S,
                                                     const DevCtrl* ctrl, int k) {
@@ -583,8 +585,8 @@ __global__ __launch_bounds__(256) void k_ruiz_tiles(const double* __restrict__ H
   while ((I + 1) * (I + 2) / 2 <= t) ++I;
   while (I * (I + 1) / 2 > t) --I;
   const int J = t - I * (I + 1) / 2;
-  __shared__ double cred[4][NB];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ double cred[8][NB];
+  const int tid = threadIdx.x;
   const int c2 = tid & 31, g = tid >> 5;  // column pair 2*c2, row group g: rows g + 8q
   const double* tile = H + (size_t)I * NB * ld + (size_t)J * NB;
   vd2 h[8];
@@ -592,37 +594,25 @@ __global__ __launch_bounds__(256) void k_ruiz_tiles(const double* __restrict__ H
   for (int q = 0; q < 8; ++q) h[q] = *reinterpret_cast<const vd2*>(tile + (size_t)(g + 8 * q) * ld + 2 * c2);
   const vd2 dj = *reinterpret_cast<const vd2*>(dcur + J * NB + 2 * c2);
   vd2 csum = {0.0, 0.0};
-  double rs[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const double di = dcur[I * NB + g + 8 * q];
     const vd2 a = dj * h[q];
-    rs[q] = a[0] * a[0] + a[1] * a[1];
+    const double rs = rz_rowgroup_sum(a[0] * a[0] + a[1] * a[1]);
+    if (c2 == RZ_ROW_LANE) S[(size_t)J * (nbn * NB) + I * NB + g + 8 * q] = rs;
     const vd2 b = h[q] * di;
     csum = __builtin_elementwise_fma(b, b, csum);
   }
-  // row partials: reduce over the 32 lanes of one row group
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    double v = rs[q];
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    rs[q] = v;
-  }
-  if (c2 == 0) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) S[(size_t)J * (nbn * NB) + I * NB + g + 8 * q] = rs[q];
-  }
   if (I == J) return;  // a diagonal tile's rows already cover its columns
-  // column partials: the two row groups of this wave, then the four waves in order
-  csum[0] += __shfl_xor(csum[0], 32, 64);
-  csum[1] += __shfl_xor(csum[1], 32, 64);
-  if (lane < 32) {
-    cred[wid][2 * c2] = csum[0];
-    cred[wid][2 * c2 + 1] = csum[1];
-  }
+  cred[g][2 * c2] = csum[0];
+  cred[g][2 * c2 + 1] = csum[1];
   __syncthreads();
-  if (tid < NB) S[(size_t)I * (nbn * NB) + J * NB + tid] = ((cred[0][tid] + cred[1][tid]) + cred[2][tid]) + cred[3][tid];
+  if (tid < NB) {
+    double v = cred[0][tid];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) v += cred[r][tid];
+    S[(size_t)I * (nbn * NB) + J * NB + tid] = v;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_ruiz_rows(const double* __restrict__ S, int nbn, int n, int np,
