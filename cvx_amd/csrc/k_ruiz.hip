@@ -126,10 +126,18 @@ __device__ __forceinline__ bool rz_agree(bool mine, RzShared& sh) {
 
 // One sweep over a batch of nb <= MT tiles whose entries are in h (k_ruiz_tiles' per-thread layout: row g + 8 q,
 // columns 2 c2, 2 c2 + 1).  False: stop (the loop is done) or abort.
+// the thread index through an empty asm: the compiler cannot prove it loop-invariant, so the many addresses derived
+// from it are recomputed per sweep instead of being held (and spilled) across the sweep loop
+__device__ __forceinline__ int rz_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 template <int MT>
 __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const int* tiles, int k, const RzArgs& a,
                                          RzShared& sh, bool check_stop, unsigned long long* dstamp = nullptr) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = rz_tid(), lane = tid & 63, wid = tid >> 6;
   const int c2 = tid & 31, g = tid >> 5;
   const int nbn = a.nbn, ldS = nbn * NB;
   const Gran dk(a.dbuf + (size_t)k * ldS * 2, ldS), S(a.part, (size_t)nbn * ldS);
@@ -182,14 +190,19 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
       const int I = tiles[t] >> 16, J = tiles[t] & 0xffff;
       const f64x2 dj = {sh.d[2 * t + 1][2 * c2], sh.d[2 * t + 1][2 * c2 + 1]};
       f64x2 csum = {0.0, 0.0};
+      double rs[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {  // ruiz_tile.hpp's arithmetic, as k_ruiz_tiles
+      for (int q = 0; q < 8; ++q) {  // ruiz_tile.hpp's arithmetic, as k_ruiz_tiles (the 8 sums side by side)
         const double di = sh.d[2 * t][g + 8 * q];
         const f64x2 av = dj * h[t][q];
-        const double rs = rz_rowgroup_sum(av[0] * av[0] + av[1] * av[1]);
-        if (c2 == RZ_ROW_LANE) S.st(J * ldS + I * NB + g + 8 * q, rs, tk);
+        rs[q] = av[0] * av[0] + av[1] * av[1];
         const f64x2 bv = h[t][q] * di;
         csum = __builtin_elementwise_fma(bv, bv, csum);
+      }
+      rz_rowgroup_sum8(rs);
+      if (c2 == RZ_ROW_LANE) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) S.st(J * ldS + I * NB + g + 8 * q, rs[q], tk);
       }
       if (I != J) {
         sh.cred[t][g][2 * c2] = csum[0];
@@ -214,7 +227,7 @@ __device__ __forceinline__ bool rz_batch(const f64x2 (&h)[MT][8], int nb, const 
 
 // The reduction of block X in sweep k (k_ruiz_rows' sums in its order): d^(k+1) of the block, its max |1 - u|.
 __device__ __forceinline__ bool rz_reduce(int X, int k, const RzArgs& a, RzShared& sh) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = rz_tid(), lane = tid & 63, wid = tid >> 6;
   const int nbn = a.nbn, ldS = nbn * NB;
   const Gran S(a.part, (size_t)nbn * ldS), dk(a.dbuf + (size_t)k * ldS * 2, ldS),
       dn(a.dbuf + (size_t)(k + 1) * ldS * 2, ldS), rp(a.rhop + (size_t)(k + 1) * nbn * 2, (size_t)nbn);

@@ -594,14 +594,19 @@ __global__ __launch_bounds__(256) void k_ruiz_tiles(const double* __restrict__ H
   for (int q = 0; q < 8; ++q) h[q] = *reinterpret_cast<const vd2*>(tile + (size_t)(g + 8 * q) * ld + 2 * c2);
   const vd2 dj = *reinterpret_cast<const vd2*>(dcur + J * NB + 2 * c2);
   vd2 csum = {0.0, 0.0};
+  double rs[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const double di = dcur[I * NB + g + 8 * q];
     const vd2 a = dj * h[q];
-    const double rs = rz_rowgroup_sum(a[0] * a[0] + a[1] * a[1]);
-    if (c2 == RZ_ROW_LANE) S[(size_t)J * (nbn * NB) + I * NB + g + 8 * q] = rs;
+    rs[q] = a[0] * a[0] + a[1] * a[1];
     const vd2 b = h[q] * di;
     csum = __builtin_elementwise_fma(b, b, csum);
+  }
+  rz_rowgroup_sum8(rs);
+  if (c2 == RZ_ROW_LANE) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) S[(size_t)J * (nbn * NB) + I * NB + g + 8 * q] = rs[q];
   }
   if (I == J) return;  // a diagonal tile's rows already cover its columns
   cred[g][2 * c2] = csum[0];

@@ -29,4 +29,18 @@ __device__ __forceinline__ double rz_rowgroup_sum(double v) {
   return v + rz_dppd<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3: + the other row's sum
 }
 
+// eight independent row-group sums, level by level so their DPP chains interleave
+__device__ __forceinline__ void rz_rowgroup_sum8(double (&v)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = v[q] + rz_dppd<0xB1>(v[q]);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = v[q] + rz_dppd<0x4E>(v[q]);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = v[q] + rz_dppd<0x141>(v[q]);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = v[q] + rz_dppd<0x140>(v[q]);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = v[q] + rz_dppd<0x142, 0xA>(v[q]);
+}
+
 }  // namespace cvxg
