@@ -117,7 +117,7 @@ struct cvxg_ctx {
   bool chain_defer = true;      // L_b,b-1 stored / published inside POTRF(b) (CVXG_CHAIN_DEFER=0: before it)
   double* ltag = nullptr;       // CVXG_CHAIN_TAG=1: L_kk^-1 row-blocks also as data-tagged granules for the chain
   unsigned long long tag_gen = 0;
-  bool chain_dpp = false;       // CVXG_CHAIN_DPP=1: POTRF's column sweep with DPP broadcasts
+  bool chain_dpp = true;        // POTRF's column sweep with DPP broadcasts (CVXG_CHAIN_DPP=0: v_readlane)
   bool h_full = true;           // the current H holds its upper triangle too
   double* hsv_part = nullptr;   // symv partials (nblk x np)
   // Ruiz: every sweep in one persistent launch (k_ruiz.hip; CVXG_RUIZ_LOOP=0: two launches per sweep)

@@ -1621,7 +1621,7 @@ def test_chain_owned_panel_updates_bitwise(mods, monkeypatch, n, m):
     applying them (CVXG_CHAIN_B2=0).  Likewise the chain's TRSM tile L_b,b-1 stored and published by waves 1..3 of
     POTRF(b) (CVXG_CHAIN_DEFER=1, the default) or before it (=0), and the L_kk^-1 row-blocks handed to the chain as
     data-tagged granules (CVXG_CHAIN_TAG=1) or behind the chain flag, and POTRF's column sweep with DPP broadcasts
-    (CVXG_CHAIN_DPP=1: the same fma per entry) or v_readlane.  Checked on dx, min diag(L) and a whole Newton step, at
+    (CVXG_CHAIN_DPP=1, the default: the same fma per entry) or v_readlane.  Checked on dx, min diag(L) and a whole Newton step, at
     t = 1 and at later t, for every built variant (k_dataflow.hip: chol_dataflow_variant_ok)."""
     Z, SP, Engine, O = mods
     spec = Z.random_qp(n, m, instance=3)
@@ -1633,7 +1633,7 @@ def test_chain_owned_panel_updates_bitwise(mods, monkeypatch, n, m):
         states = [(1.0, spec["x0"], None, 0, float("nan"))] + [
             (float(fx["t"][k]), fx["x"][k], fx["grad"][k], int(fx["it_n"][k]), float(fx["radius"][k])) for k in (2, 6)]
     out = {}
-    variants = ("1100", "0000", "0100", "1000", "1110", "1101", "1111")  # (B2, DEFER, TAG, DPP): the built variants
+    variants = ("1101", "0000", "0100", "1000", "1100", "1110", "1111")  # (B2, DEFER, TAG, DPP): the built variants
     for flag in variants:
         for name, v in zip(("CVXG_CHAIN_B2", "CVXG_CHAIN_DEFER", "CVXG_CHAIN_TAG", "CVXG_CHAIN_DPP"), flag):
             monkeypatch.setenv(name, v)
@@ -1648,7 +1648,7 @@ def test_chain_owned_panel_updates_bitwise(mods, monkeypatch, n, m):
         out[flag] = res
         eng.close()
     for other in variants[1:]:
-        for a, b in zip(out["1100"], out[other]):
+        for a, b in zip(out["1101"], out[other]):
             assert np.array_equal(a[0], b[0]) and a[1] == b[1] and a[2] == b[2] and a[3] == b[3], other
             assert np.array_equal(a[4], b[4]), other
 
