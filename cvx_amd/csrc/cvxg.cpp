@@ -855,7 +855,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   if (ctx->hctrl->ruiz_sweeps == -2)
     return set_err(ctx, CVXG_E_HIP, "Ruiz loop: dependency wait timed out (abort word 0x%x)", ctx->hctrl->ruiz_abort);
   if (ctx->df_trace) {  // instrumentation only: task order + timeline of this factorization
-    std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 4 * ctx->nblk));
+    std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 5 * ctx->nblk));
     std::vector<unsigned> ord(ctx->df_ntasks);
     CHK(copy_sync(ctx, tr.data(), ctx->df_trace, tr.size() * 8, hipMemcpyDeviceToHost));
     CHK(copy_sync(ctx, ord.data(), ctx->df_tasks, ord.size() * 4, hipMemcpyDeviceToHost));
@@ -1690,7 +1690,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     CHK(dalloc(ctx, &ctx->df_work, chol_dataflow_work_ints(ctx->nblk)));
     if (const char* e = getenv("CVXG_DF_TRACE")) {  // instrumentation only: the task timeline of the last factorization
       ctx->df_trace_path = e;
-      CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 4 * ctx->nblk)));
+      CHK(dalloc(ctx, &ctx->df_trace, (size_t)4 * (ctx->df_ntasks + 5 * ctx->nblk)));
     }
   }
   CHK(dalloc(ctx, &ctx->bwd_flags, bwd_work_ints(ctx->nblk)));

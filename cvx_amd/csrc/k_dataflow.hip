@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     Potrf64wSmem& ps = cs.p;
     const int lane = tid & 63, wv = tid >> 6;
     auto mark = [&](int k, int step, int field) {
-      if (trace && tid == 0) trace[4 * (size_t)(ntasks + 4 * k + step) + field] = __builtin_amdgcn_s_memrealtime();
+      if (trace && tid == 0) trace[4 * (size_t)(ntasks + 5 * k + step) + field] = __builtin_amdgcn_s_memrealtime();
     };
     auto publish = [&](int idx, int v) {
       df_drain();  // every storing wave: its sc1 stores have left
@@ -669,6 +669,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           return true;
         };
         __syncthreads();  // Sa and the batch's row-blocks in ps.S complete
+        mark(k, 4, 0);    // trace: every wave's staging loads landed (record 4: the batch's phases)
         double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments
 #pragma unroll
         for (int q = 0; q < 16; ++q) af[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
@@ -680,6 +681,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           if (nbat > 2) acc[2] = ch_trsm<2>(af, ps.S + 32 * P64_SP, lane);
           if (nbat > 3) acc[3] = ch_trsm<3>(af, ps.S + 48 * P64_SP, lane);
           __syncthreads();  // every wave holds its fragments of A (Sa takes L')
+          mark(k, 4, 1);
 #pragma unroll
           for (int cb = 0; cb < 4; ++cb)
             if (cb < nbat)
@@ -698,6 +700,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               default: ch_update<3>(dacc, Lp, cb, lane); break;
             }
           }
+          mark(k, 4, 2);
         }
         bool tfail = false;
         if (nbat < 4) {
@@ -830,7 +833,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       };
       if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre,
                                    kTag ? ltag : nullptr, tag_gen, kDpp,
-                                   trace ? trace + 4 * (size_t)(ntasks + 4 * b + 3) : nullptr)) {
+                                   trace ? trace + 4 * (size_t)(ntasks + 5 * b + 3) : nullptr)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }

@@ -4,7 +4,7 @@ POTRF(k+1) start, the fix hook of POTRF(k+1); then the worker tasks feeding bloc
 import sys, numpy as np
 raw=open(sys.argv[1],'rb').read()
 nq,nb=(int(v) for v in np.frombuffer(raw[:8],dtype=np.int32))
-R=((len(raw)-8-4*nq)//32-nq)//nb  # chain records per block (k_dataflow.hip: 4 since round 5, 3 before)
+R=((len(raw)-8-4*nq)//32-nq)//nb  # chain records per block (k_dataflow.hip: 5 since round 5, 3 before)
 tr=np.frombuffer(raw[8+4*nq:8+4*nq+32*(nq+R*nb)],dtype=np.uint64).reshape(nq+R*nb,4).astype(np.int64)
 ch=tr[nq:].reshape(nb,R,4)
 us=lambda v:v/100.0
@@ -17,10 +17,11 @@ for k in range(2,nb-2):
     s2=ch[k+1,0,1]
     b2in=ch[k,2,3]; b2done=ch[k,0,3]  # chain-owned b-2 staging (k_dataflow.hip own_b2): inputs in / panel applied
     rbp=[ch[k,3,i] if R>3 else 0 for i in range(4)]  # POTRF(k)'s L^-1 row-block flags raised (wave 3)
+    bat=[ch[k,4,i] if R>4 else 0 for i in range(3)]  # the batch of block k+1: loads landed, TRSM products, updates
     rows.append([us(B-A),us(stg0-A),us(C-A),us(s2-A) if s2>A else np.nan,us(D-A) if D>A else np.nan,us(E-A),us(F-A),us(fix0-F) if fix0>0 else 0, us(fix1-F) if fix1>0 else 0,us(fix2-F) if fix2>0 else 0,
-                 us(b2in-A) if b2in>0 else np.nan, us(b2done-A) if b2done>0 else np.nan]+[us(v-A) if v>0 else np.nan for v in rbp])
+                 us(b2in-A) if b2in>0 else np.nan, us(b2done-A) if b2done>0 else np.nan]+[us(v-A) if v>0 else np.nan for v in rbp]+[us(v-A) if v>0 else np.nan for v in bat])
 r=np.array(rows)
-names=['potrf_done','stage_begin(k+1)','staged(k+1)','slice2done(k+1)','lastrow(k+1)','slices_done(k+1)','potrf_start(k+1)','fix0(k+1)-F','fix1-F','fix2-F','b2_inputs(k+1)','b2_applied(k+1)','rb0_flag(k)','rb1_flag(k)','rb2_flag(k)','rb3_flag(k)']
+names=['potrf_done','stage_begin(k+1)','staged(k+1)','slice2done(k+1)','lastrow(k+1)','slices_done(k+1)','potrf_start(k+1)','fix0(k+1)-F','fix1-F','fix2-F','b2_inputs(k+1)','b2_applied(k+1)','rb0_flag(k)','rb1_flag(k)','rb2_flag(k)','rb3_flag(k)','batch_loaded(k+1)','batch_trsm(k+1)','batch_upd(k+1)']
 for i,nm in enumerate(names):
     print(f"{nm:22s} mean {np.nanmean(r[:,i]):7.2f} med {np.nanmedian(r[:,i]):7.2f} min {np.nanmin(r[:,i]):7.2f} max {np.nanmax(r[:,i]):7.2f}")
 order=np.frombuffer(raw[8:8+4*nq],dtype=np.uint32)
