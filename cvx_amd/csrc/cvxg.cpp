@@ -824,6 +824,8 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   // (+ reg I) is formed as each tile is first read (no separate k_form_q pass)
   // the first attempt (reg = 0) stops at the first block with min diag(L) <= 1e-7: its factor would be discarded
   // anyway (MatrixUtils.scala:458-460 refactors Q + 1e-10 I), so only the retry's L is ever used
+  if (ctx->df_trace)  // (instrumentation: marks a launch does not reach read 0, not a previous launch's value)
+    (void)hipMemsetAsync(ctx->df_trace, 0, (size_t)4 * (ctx->df_ntasks + 5 * ctx->nblk) * 8, s);
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
                        ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending,
                        (reg == 0.0 && ctx->early_abort) ? 1e-7 : 0.0, ctx->chain_b2, ctx->chain_defer, ctx->ltag,
