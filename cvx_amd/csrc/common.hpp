@@ -34,6 +34,12 @@ struct DevCtrl {
                                   // first row of the 16-column block where it stopped on min diag(L) <= early_min
                                   // (min_diag holds that block's value); 0 = it did not stop
   int ruiz_abort;                 // k_ruiz_loop's abort word of its last launch (0 = none; else which wait gave up)
+  // speculative regularized attempt (cvxg.cpp: regularized_cholesky_spec): chol(Q) and chol(Q + 1e-10 I) side by side;
+  // spec_sel = 1 when the first is discarded (its pivot failed or min diag(L) <= 1e-7), the second's results beside
+  int spec_sel;
+  int chol_info2;
+  int small_piv2;
+  unsigned long long min_diag2;
 };
 
 enum {

@@ -194,6 +194,17 @@ struct cvxg_ctx {
   // assembly at the current x and t (x_eval_valid too).
   hipStream_t s2 = nullptr;
   hipEvent_t ev_w = nullptr, ev_h = nullptr;
+  // speculative regularized pair (regularized_cholesky_spec): after a regularized Newton direction the next one runs
+  // chol(Q) and chol(Q + 1e-10 I) side by side, each on half of the CUs (CVXG_SPEC_REG=0: one after the other)
+  int spec_reg = 1;
+  int prev_reg = 0;
+  bool pair_active = false;
+  double *L2 = nullptr, *Linv2 = nullptr, *rhs2 = nullptr;
+  int* df_work2 = nullptr;
+  DevCtrl* ctrl2 = nullptr;
+  hipStream_t s3 = nullptr;
+  hipEvent_t ev_p0 = nullptr, ev_p1 = nullptr;
+  long long spec_pairs = 0, spec_pairs_used = 0;  // pairs launched / pairs whose second attempt was the one used
   bool h_valid = false;
   // The line search's setup (A s, P s, their dots) and first trial batch, enqueued behind each factorization attempt
   // of a Newton step with s = dx (the trust radius does not clamp in the common case), so the attempt's host read
@@ -899,8 +910,97 @@ static int regularized_cholesky(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regula
 }
 
 static void backward_solve(cvxg_ctx* ctx, int nrhs, BwdEpilogue epi = {}) {
+  BwdAlt alt;
+  if (ctx->pair_active) alt = BwdAlt{ctx->L2, ctx->Linv2, ctx->rhs2};  // (the device picks by ctrl->spec_sel)
   launch_bwd_dataflow(ctx->s, ctx->L, ctx->np, ctx->Linv, ctx->rhs, ctx->sol, nrhs, ctx->nblk, ctx->bwd_flags,
-                      ++ctx->bwd_gen, ctx->ctrl, epi);
+                      ++ctx->bwd_gen, ctx->ctrl, epi, alt);
+}
+
+// The buffers of the speculative pair's second attempt (allocated on first use: 134 MB of L at C3).
+static int spec_alloc(cvxg_ctx* ctx) {
+  if (ctx->L2) return CVXG_OK;
+  const size_t np = ctx->np;
+  CHK(dalloc(ctx, &ctx->L2, np * np));
+  CHK(dalloc(ctx, &ctx->Linv2, (size_t)ctx->nblk * NB * NB));
+  CHK(dalloc(ctx, &ctx->rhs2, np * MAX_RHS));
+  CHK(dalloc(ctx, &ctx->df_work2, chol_dataflow_work_ints(ctx->nblk)));
+  HIPC(ctx, hipMalloc((void**)&ctx->ctrl2, sizeof(DevCtrl)));
+  HIPC(ctx, hipMemset(ctx->ctrl2, 0, sizeof(DevCtrl)));
+  HIPC(ctx, hipStreamCreateWithFlags(&ctx->s3, hipStreamNonBlocking));
+  HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_p0, hipEventDisableTiming));
+  HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_p1, hipEventDisableTiming));
+  return CVXG_OK;
+}
+
+// regularizedCholesky (MatrixUtils.scala:452-461) with both attempts in flight together: chol(Q) (stopping at its
+// first block with min diag(L) <= 1e-7, as factor_attempt) and chol(Q + 1e-10 I), each a dataflow launch on half of
+// the CUs, on two streams.  The device picks the attempt the reference keeps (k_spec_select), the backward solve and
+// everything behind it run on that one, and the one host read returns both verdicts.  The factors are bitwise those
+// of the sequential form (the same launches, only concurrent).  Used after a regularized direction: late in the path
+// the Q + 1e-10 I branch repeats step after step, and its first attempt fails in the last block (C3FULL stop rows
+// 4081..4096), so the sequential form pays two whole factorizations.
+template <class F, class G>
+static int regularized_cholesky_spec(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* regularized, double* mind, G after) {
+  hipStream_t s = ctx->s;
+  CHK(spec_alloc(ctx));
+  ++ctx->spec_pairs;
+  launch_factor_prep(s, ctx->ctrl, 0.0, ctx->df_work, chol_dataflow_work_ints(ctx->nblk));
+  launch_spec_prep2(s, ctx->ctrl2, ctx->ctrl, 1e-10);
+  HIPC(ctx, hipMemsetAsync(ctx->df_work2, 0, chol_dataflow_work_ints(ctx->nblk) * sizeof(int), s));
+  fill_rhs();
+  HIPC(ctx, hipMemcpyAsync(ctx->rhs2, ctx->rhs, (size_t)ctx->np * nrhs * sizeof(double), hipMemcpyDeviceToDevice, s));
+  HIPC(ctx, hipEventRecord(ctx->ev_p0, s));
+  HIPC(ctx, hipStreamWaitEvent(ctx->s3, ctx->ev_p0, 0));
+  const int half = std::max(3, ctx->ncu / 2);
+  launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
+                       ctx->df_ntasks, half, nullptr, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending,
+                       ctx->early_abort ? 1e-7 : 0.0, ctx->chain_b2, ctx->chain_defer, nullptr, 0, ctx->chain_dpp);
+  launch_chol_dataflow(ctx->s3, ctx->L2, ctx->np, ctx->rhs2, nrhs, ctx->Linv2, ctx->ctrl2, ctx->df_work2, ctx->nblk,
+                       ctx->df_tasks, ctx->df_ntasks, half, nullptr, false, ctx->H, ctx->dfin, ctx->n,
+                       ctx->ruiz_pending, 0.0, ctx->chain_b2, ctx->chain_defer, nullptr, 0, ctx->chain_dpp);
+  HIPC(ctx, hipEventRecord(ctx->ev_p1, ctx->s3));
+  HIPC(ctx, hipStreamWaitEvent(s, ctx->ev_p1, 0));
+  launch_spec_select(s, ctx->ctrl, ctx->ctrl2);
+  ctx->spec_launched = false;
+  ctx->pair_active = true;
+  after();
+  ctx->pair_active = false;
+  HIPC(ctx, hipGetLastError());
+  if (ctx->spec_launched) {
+    CHK(host_read(ctx, ctx->ctrl, ctx->hctrl_dev, sizeof(DevCtrl), ctx->ls_log, ctx->hls_dev,
+                  5 * LS_TRIALS * sizeof(double)));
+  } else {
+    CHK(sync_ctrl(ctx));
+  }
+  if (ctx->ruiz_pending) {
+    ctx->ruiz_pending = false;
+    if (ctx->hctrl->ruiz_sweeps < 0) {  // the Ruiz loop was still open: both attempts were void
+      ctx->spec_launched = ctx->spec_eval_launched = false;
+      CHK(ruiz_finish(ctx));
+      return regularized_cholesky(ctx, nrhs, fill_rhs, regularized, mind, after);
+    }
+  }
+  ctx->spec_have = ctx->spec_launched;
+  ctx->spec_eval_have = ctx->spec_launched && ctx->spec_eval_launched;
+  ctx->spec_launched = false;
+  ctx->spec_eval_launched = false;
+  if (ctx->hctrl->df_status != 0)
+    return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
+  if (!ctx->hctrl->spec_sel) {
+    *regularized = 0;
+    ctx->small_piv = 0;
+    *mind = min_diag_of(*ctx->hctrl);
+    return CVXG_OK;
+  }
+  ++ctx->spec_pairs_used;
+  *regularized = 1;
+  ctx->small_piv = ctx->hctrl->small_piv ? ctx->hctrl->small_piv : ctx->hctrl->chol_info;
+  double md2;
+  memcpy(&md2, &ctx->hctrl->min_diag2, sizeof(md2));
+  *mind = md2;
+  if (ctx->hctrl->chol_info2 != 0)
+    return set_err(ctx, CVXG_E_NOT_PD, "cholesky: matrix not positive definite (pivot %d)", ctx->hctrl->chol_info2);
+  return CVXG_OK;
 }
 
 static void ls_setup_launch(cvxg_ctx* ctx, bool spec_eval = false, DotBatch db = {});
@@ -949,9 +1049,11 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
       ctx->spec_eval_launched = se;
     }
   };
-  int rc = regularized_cholesky(
-      ctx, 1, [&]() { launch_scaled_col(s, ctx->dfin, ctx->y, -1.0, ctx->n, ctx->np, 1, 0, ctx->rhs); }, &reg, &mind,
-      solve_and_residual);
+  auto fill = [&]() { launch_scaled_col(s, ctx->dfin, ctx->y, -1.0, ctx->n, ctx->np, 1, 0, ctx->rhs); };
+  int rc = (ctx->spec_reg && ctx->prev_reg && !ctx->df_trace)
+               ? regularized_cholesky_spec(ctx, 1, fill, &reg, &mind, solve_and_residual)
+               : regularized_cholesky(ctx, 1, fill, &reg, &mind, solve_and_residual);
+  ctx->prev_reg = reg;
   info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
   if (info->ruiz_sweeps >= 0) ruiz_learn(ctx, info->ruiz_sweeps);
   info->regularized = reg;
@@ -1740,6 +1842,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   CHK(dalloc(ctx, &ctx->spart,
              ctx->nsplit > 1 ? (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE : (size_t)1));
   HIPC(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
+  if (const char* e = getenv("CVXG_SPEC_REG")) ctx->spec_reg = atoi(e) != 0;
   HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_w, hipEventDisableTiming));
   HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_h, hipEventDisableTiming));
   const int lsb = ls_blocks(std::max(m, 1));
@@ -1801,6 +1904,12 @@ void cvxg_destroy(cvxg_ctx* ctx) {
       for (hipEvent_t e : pr)
         if (e) (void)hipEventDestroy(e);
   if (ctx->s2) (void)hipStreamSynchronize(ctx->s2);
+  if (ctx->s3) (void)hipStreamSynchronize(ctx->s3);
+  for (void* p : {(void*)ctx->L2, (void*)ctx->Linv2, (void*)ctx->rhs2, (void*)ctx->df_work2, (void*)ctx->ctrl2})
+    if (p) (void)hipFree(p);
+  for (hipEvent_t e : {ctx->ev_p0, ctx->ev_p1})
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->s3) (void)hipStreamDestroy(ctx->s3);
   if (ctx->spart) (void)hipFree(ctx->spart);
   for (hipEvent_t e : {ctx->ev_w, ctx->ev_h})
     if (e) (void)hipEventDestroy(e);

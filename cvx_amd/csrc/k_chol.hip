@@ -20,8 +20,16 @@ namespace cvxg {
 __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__ L, int ld,
                                                       const double* __restrict__ Linv, const double* __restrict__ rhs,
                                                       double* __restrict__ out, int nrhs, int nblk, int* flags, int gen,
-                                                      const DevCtrl* ctrl, BwdEpilogue epi) {
-  if (ctrl->chol_info != 0 || ctrl->ruiz_sweeps < 0) return;  // a failed or void factorization attempt
+                                                      const DevCtrl* ctrl, BwdEpilogue epi, BwdAlt alt) {
+  if (ctrl->ruiz_sweeps < 0) return;  // a void factorization attempt
+  if (alt.L && ctrl->spec_sel) {      // the speculative pair's second attempt is the one to use
+    if (ctrl->chol_info2 != 0) return;
+    L = alt.L;
+    Linv = alt.Linv;
+    rhs = alt.rhs;
+  } else if (ctrl->chol_info != 0) {
+    return;  // a failed attempt
+  }
   __shared__ double u[MAX_RHS][NB];
   __shared__ double part[4][MAX_RHS][NB];
   __shared__ int s_bad;
@@ -126,9 +134,32 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
 size_t bwd_work_ints(int nblk) { return (size_t)((nblk + 63) & ~63) + (size_t)nblk * NB * MAX_RHS * 4; }
 
 void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,
-                         int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl, BwdEpilogue epi) {
+                         int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl, BwdEpilogue epi, BwdAlt alt) {
   // (flags: nblk words + the granules, bwd_work_ints)
-  k_bwd_dataflow<<<nblk, 256, 0, s>>>(L, ld, Linv, rhs, out, nrhs, nblk, flags, gen, ctrl, epi);
+  k_bwd_dataflow<<<nblk, 256, 0, s>>>(L, ld, Linv, rhs, out, nrhs, nblk, flags, gen, ctrl, epi, alt);
 }
+
+__global__ void k_spec_prep2(DevCtrl* ctrl2, const DevCtrl* ctrl, double reg) {
+  ctrl2->reg = reg;
+  ctrl2->small_piv = 0;
+  ctrl2->chol_info = 0;
+  ctrl2->df_status = 0;
+  ctrl2->min_diag = (unsigned long long)__double_as_longlong(__builtin_inf());
+  ctrl2->ruiz_sweeps = ctrl->ruiz_sweeps;
+}
+void launch_spec_prep2(hipStream_t s, DevCtrl* ctrl2, const DevCtrl* ctrl, double reg) {
+  k_spec_prep2<<<1, 1, 0, s>>>(ctrl2, ctrl, reg);
+}
+// regularizedCholesky's test on the first attempt (MatrixUtils.scala:456-460): discarded when its pivot failed or
+// min diag(L) <= 1e-7
+__global__ void k_spec_select(DevCtrl* ctrl, const DevCtrl* ctrl2) {
+  const double md = __longlong_as_double((long long)ctrl->min_diag);
+  ctrl->spec_sel = (ctrl->chol_info == 0 && md > 1e-7) ? 0 : 1;
+  ctrl->chol_info2 = ctrl2->chol_info;
+  ctrl->small_piv2 = ctrl2->small_piv;
+  ctrl->min_diag2 = ctrl2->min_diag;
+  if (ctrl2->df_status) ctrl->df_status = ctrl2->df_status;
+}
+void launch_spec_select(hipStream_t s, DevCtrl* ctrl, const DevCtrl* ctrl2) { k_spec_select<<<1, 1, 0, s>>>(ctrl, ctrl2); }
 
 }  // namespace cvxg

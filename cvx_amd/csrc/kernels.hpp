@@ -185,8 +185,21 @@ struct BwdEpilogue {
   double* x1 = nullptr;
   DevCtrl* sctrl = nullptr;
 };
+// The second factorization of a speculative pair (regularized_cholesky_spec): used instead of L / Linv / rhs when
+// ctrl->spec_sel is set (its failure word is ctrl->chol_info2).
+struct BwdAlt {
+  const double* L = nullptr;
+  const double* Linv = nullptr;
+  const double* rhs = nullptr;
+};
 void launch_bwd_dataflow(hipStream_t s, const double* L, int ld, const double* Linv, const double* rhs, double* out,
-                         int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl, BwdEpilogue epi = {});
+                         int nrhs, int nblk, int* flags, int gen, const DevCtrl* ctrl, BwdEpilogue epi = {},
+                         BwdAlt alt = {});
+// ctrl2 of the speculative second attempt: its factor prep (reg, chol fields) and the main control block's Ruiz
+// verdict (the dataflow launch's gate)
+void launch_spec_prep2(hipStream_t s, DevCtrl* ctrl2, const DevCtrl* ctrl, double reg);
+// after both attempts: ctrl->spec_sel (first attempt discarded) and the second attempt's chol fields into ctrl
+void launch_spec_select(hipStream_t s, DevCtrl* ctrl, const DevCtrl* ctrl2);
 
 // ---- line search ----------------------------------------------------------------------------------
 // For trials k in [0, LS_TRIALS): t_k = tbase*beta^k; g_i = c_i + t_k e_i; per-block partials of

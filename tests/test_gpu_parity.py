@@ -1685,6 +1685,41 @@ def test_ruiz_loop_bitwise(mods, monkeypatch, n, m, wg):
     print(f"n={n}: Ruiz sweeps {[r[1] for r in out['1']]}")
 
 
+def test_speculative_regularized_pair_bitwise(mods, monkeypatch):
+    """After a regularized Newton direction the next one runs chol(Q) and chol(Q + 1e-10 I) side by side
+    (cvxg.cpp: regularized_cholesky_spec, CVXG_SPEC_REG=1, the default) and the device keeps the one
+    regularizedCholesky keeps (MatrixUtils.scala:452-461).  Over late C3 states -- regularized, regularized,
+    regularized, then one that is not (the pair's first attempt kept) and a Newton step from there -- Δx,
+    min diag(L), the regularization flag and the step's x are bitwise those of the one-after-the-other form."""
+    Z, SP, Engine, O = mods
+    fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "big", "C3late_n4096_m8192.npz")))
+    spec = Z.random_qp(4096, 8192, instance=int(fx["instance"]))
+    pars = SP.standardParams()
+    seq = (5, 6, 7, 2, 6)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CVXG_SPEC_REG", flag)
+        eng = _engine(Engine, spec)
+        res = []
+        for k in seq:
+            t, x, g = float(fx["t"][k]), fx["x"][k], fx["grad"][k]
+            dx, _, info = eng.newton_direction(pars, t, x, grad=g)
+            res.append((dx, info.min_diag, info.regularized, info.small_pivot, info.ruiz_sweeps))
+        k = 2  # a whole Newton step behind a regularized direction (the pair, its first attempt kept)
+        eng.newton_direction(pars, float(fx["t"][5]), fx["x"][5], grad=fx["grad"][5])
+        eng.set_x(fx["x"][k])
+        eng.centering_resume(float(fx["t"][k]), int(fx["it_n"][k]), float(fx["radius"][k]), grad=fx["grad"][k])
+        st = eng.newton_step(pars)
+        res.append((eng.get_x(), st.step, st.regularized, st.small_pivot, st.ruiz_sweeps))
+        out[flag] = res
+        eng.close()
+    regs = [r[2] for r in out["1"][:len(seq)]]
+    print(f"regularized per direction {regs}")
+    assert regs[:3] == [1, 1, 1] or regs[:3] == [int(fx['reg'][k]) for k in seq[:3]]
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a[0], b[0]) and a[1] == b[1] and a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
+
+
 def test_batch_barrier_solve_matches_single_contexts(mods):
     """cvxg_batch_barrier_solve / cvxg_batch_newton_step (config C5 from one host process, one thread per context):
     three independent instances solved concurrently give bitwise the x, step counts and gaps of three one-at-a-time
