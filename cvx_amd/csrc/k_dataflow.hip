@@ -325,7 +325,7 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
       }
   // L_ik is published before the rhs update: its consumers (the updates of row i and column i) start a rhs update
   // earlier.  The rhs updates of block row i stay in panel order through rhscnt[i] (applied TRSM(i, .) updates):
-  // this one waits for w_k and for rhscnt[i] == k, and the chain's staging of block i waits for rhscnt[i] == i - 1.
+  // this one waits for w_k and for rhscnt[i] == k, and POTRF(i)'s fix hook on the chain waits for rhscnt[i] == i - 1.
   df_drain();
   __syncthreads();
   if (tid == 0) {
@@ -515,13 +515,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               }
             }
           }
-          // (2) L_b,j (worker TRSM(b,j)), L_k,j (the other chain workgroup's TRSM, published inside its POTRF(k)) and
-          // the rhs block with TRSM(b, i <= j)'s updates
+          // (2) L_b,j (worker TRSM(b,j)) and L_k,j (the other chain workgroup's TRSM, published inside its POTRF(k));
+          // the rhs block is read in POTRF(b)'s fix hook, which it first feeds
           if (tid == 0) {
-            const int v2 = df_poll(rhscnt + b), v3 = df_poll(state + df_tri(b, j)), v4 = df_poll(state + df_tri(k, j));
+            const int v3 = df_poll(state + df_tri(b, j)), v4 = df_poll(state + df_tri(k, j));
             s_ok = (v3 >= j + 1 || df_wait(state, df_tri(b, j), j + 1, abortw, ctrl)) &&
-                   (v4 >= j + 1 || df_wait(state, df_tri(k, j), j + 1, abortw, ctrl)) &&
-                   (v2 >= k || df_wait(rhscnt, b, k, abortw, ctrl));
+                   (v4 >= j + 1 || df_wait(state, df_tri(k, j), j + 1, abortw, ctrl));
           }
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           __syncthreads();
@@ -531,8 +530,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             f64x2 vl[NB * NB / 512], vk[NB * NB / 512];
             df_load(vl, Sc1Mem(L + (size_t)b * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
             df_load(vk, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
-            const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-            for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
             df_put(ps.X, vl);  // (POTRF's L^-1 workspace and tile: free until the reset / the batch below)
             df_put(ps.S, vk);
           }
@@ -558,14 +555,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           mark(k, 0, 3);  // trace: the b-2 panel applied (field 3 of POTRF(k)'s record)
         } else {
-        // A_b,k and D_b with every panel < k applied (state >= k), and the rhs block b with all earlier TRSM
-        // updates: one wait for both states, then every load in flight together (minus L_b,k w_k inside POTRF(b);
-        // POTRF(b-2) of this workgroup is done with ps.B)
+        // A_b,k and D_b with every panel < k applied (state >= k): one wait for both states, then every load in
+        // flight together (the rhs block is read in POTRF(b)'s fix hook)
         if (tid == 0) {  // (the polls in flight together: usually the other inputs are final when the first is)
-          const int v0 = df_poll(state + df_tri(b, k)), v1 = df_poll(state + df_tri(b, b)), v2 = df_poll(rhscnt + b);
+          const int v0 = df_poll(state + df_tri(b, k)), v1 = df_poll(state + df_tri(b, b));
           s_ok = (v0 >= k || df_wait(state, df_tri(b, k), k, abortw, ctrl)) &&
-                 (v1 >= k || df_wait(state, df_tri(b, b), k, abortw, ctrl)) &&
-                 (v2 >= k || df_wait(rhscnt, b, k, abortw, ctrl));  // the rhs block has TRSM(b, j < k)'s updates
+                 (v1 >= k || df_wait(state, df_tri(b, b), k, abortw, ctrl));
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
@@ -589,8 +584,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             }
           }
           if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const Sc1Mem mR(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-          for (int t = tid; t < NB * nrhs; t += 256) ps.B[t] = mR.ld(t);
           df_put(cs.Sa, va);
         }
         }
@@ -793,13 +786,22 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         if (b == 0) return true;
         const int k = b - 1;
         mark(k, 2, 0);
-        if (tid == 0) s_ok = df_wait(state, df_tri(k, k), k + 1, abortw, ctrl);
+        // w_k (POTRF(k) done) and the rhs block b with every worker TRSM(b, j < k)'s update (rhscnt[b] == k)
+        if (tid == 0) {
+          const int v0 = df_poll(state + df_tri(k, k)), v1 = df_poll(rhscnt + b);
+          s_ok = (v0 >= k + 1 || df_wait(state, df_tri(k, k), k + 1, abortw, ctrl)) &&
+                 (v1 >= k || df_wait(rhscnt, b, k, abortw, ctrl));
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
         if (!s_ok) return false;
         mark(k, 2, 1);
         const Sc1Mem mW(rhs + (size_t)k * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
-        for (int t = tid; t < NB * nrhs; t += 256) cs.V[t] = mW.ld(t);
+        const Sc1Mem mRb(rhs + (size_t)b * NB * nrhs, (unsigned)(NB * nrhs) * 8u);
+        for (int t = tid; t < NB * nrhs; t += 256) {
+          cs.V[t] = mW.ld(t);
+          ps.B[t] = mRb.ld(t);
+        }
         __syncthreads();
         for (int t0 = 0; t0 < NB * nrhs * 4; t0 += 256) {
           const int t = t0 + tid, q = t & 3, e = t >> 2;
