@@ -510,6 +510,7 @@ def run_full_solve(args):
         ph_sum, ph_cnt = np.zeros(8), np.zeros(8)  # per phase: summed ms over its occurrences, occurrences
         if timed:
             eng.set_timing(True, all_phases=True)
+        c0 = eng.counters()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         while True:  # BarrierSolver.scala:70-117: center at t, gap = m / t, stop below tolSolver, else t *= mu
@@ -538,6 +539,7 @@ def run_full_solve(args):
             t *= 10.0
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        c1 = eng.counters()
         if timed:
             ms, cnt = eng.phase_stats()
             ph_sum += ms * cnt
@@ -548,7 +550,7 @@ def run_full_solve(args):
         return dict(elapsed=el, steps=steps, per_center=per_center, hist=hist, reg=reg, fb=fb, full=full,
                     phases=(ph_sum / max(steps, 1)).tolist(),
                     phases_occ=(ph_sum / np.maximum(ph_cnt, 1)).tolist(), occ=ph_cnt.tolist(), x=eng.get_x(),
-                    small_piv=small_piv)
+                    small_piv=small_piv, counters={k: c1[k] - c0[k] for k in c1})
 
     a = solve(False)
     b = solve(True)
@@ -574,6 +576,7 @@ def run_full_solve(args):
            "phase_occurrences_timed_solve": {"assembly_prefetched": b["occ"][5], "assembly_inline": b["occ"][0],
                                              "cholesky_fused_fwd": b["occ"][2]},
            "first_attempt_stop_rows": _hist(a["small_piv"]),
+           "factorization_counters": a["counters"],
            "timed_solve_s": b["elapsed"], "timed_solve_same_x": same}
     return out
 

@@ -111,6 +111,7 @@ SIGNATURES = {
     "cvxg_set_timing": (C.c_int, [_P, C.c_int]),
     "cvxg_get_phase_times": (C.c_int, [_P, _D, C.c_int]),
     "cvxg_get_phase_stats": (C.c_int, [_P, _D, C.POINTER(C.c_int), C.c_int]),
+    "cvxg_get_counters": (C.c_int, [_P, C.POINTER(C.c_longlong), C.c_int]),
     "cvxg_chol_schedule": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_uint), C.c_int]),
     "cvxg_set_ruiz_lookahead": (C.c_int, [_P, C.c_int, C.POINTER(C.c_longlong)]),
 }

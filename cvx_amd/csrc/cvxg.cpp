@@ -205,6 +205,7 @@ struct cvxg_ctx {
   hipStream_t s3 = nullptr;
   hipEvent_t ev_p0 = nullptr, ev_p1 = nullptr;
   long long spec_pairs = 0, spec_pairs_used = 0;  // pairs launched / pairs whose second attempt was the one used
+  long long n_attempts = 0, n_regularized = 0;
   bool h_valid = false;
   // The line search's setup (A s, P s, their dots) and first trial batch, enqueued behind each factorization attempt
   // of a Newton step with s = dx (the trust radius does not clamp in the common case), so the attempt's host read
@@ -829,6 +830,7 @@ static void ruiz_learn(cvxg_ctx* ctx, int sweeps) {
 template <class F, class G>
 static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G after) {
   hipStream_t s = ctx->s;
+  ++ctx->n_attempts;
   launch_factor_prep(s, ctx->ctrl, reg, ctx->df_work, chol_dataflow_work_ints(ctx->nblk));  // reg, chol fields, work
   fill_rhs();
   // the whole factorization as one persistent launch over the 64 x 64 tile DAG (k_dataflow.hip); Q = (d d') o H
@@ -944,6 +946,7 @@ static int regularized_cholesky_spec(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* r
   hipStream_t s = ctx->s;
   CHK(spec_alloc(ctx));
   ++ctx->spec_pairs;
+  ctx->n_attempts += 2;
   launch_factor_prep(s, ctx->ctrl, 0.0, ctx->df_work, chol_dataflow_work_ints(ctx->nblk));
   launch_spec_prep2(s, ctx->ctrl2, ctx->ctrl, 1e-10);
   HIPC(ctx, hipMemsetAsync(ctx->df_work2, 0, chol_dataflow_work_ints(ctx->nblk) * sizeof(int), s));
@@ -1054,6 +1057,7 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
                ? regularized_cholesky_spec(ctx, 1, fill, &reg, &mind, solve_and_residual)
                : regularized_cholesky(ctx, 1, fill, &reg, &mind, solve_and_residual);
   ctx->prev_reg = reg;
+  ctx->n_regularized += reg;
   info->ruiz_sweeps = ctx->hctrl->ruiz_sweeps;
   if (info->ruiz_sweeps >= 0) ruiz_learn(ctx, info->ruiz_sweeps);
   info->regularized = reg;
@@ -2531,6 +2535,14 @@ int cvxg_set_timing(cvxg_ctx* ctx, int enabled) {
 }
 
 int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count) { return cvxg_get_phase_stats(ctx, ms, nullptr, count); }
+
+int cvxg_get_counters(cvxg_ctx* ctx, long long* out, int count) {
+  if (!ctx || !out) return CVXG_E_ARG;
+  const long long v[5] = {ctx->ruiz_relaunches, ctx->spec_pairs, ctx->spec_pairs_used, ctx->n_attempts,
+                          ctx->n_regularized};
+  for (int i = 0; i < count && i < 5; ++i) out[i] = v[i];
+  return CVXG_OK;
+}
 
 int cvxg_get_phase_stats(cvxg_ctx* ctx, double* ms, int* occurrences, int count) {
   if (!ctx || !ms) return CVXG_E_ARG;

@@ -277,6 +277,13 @@ class Engine:
         self._check(self.lib.cvxg_get_phase_stats(self.h, _dp(ms), cnt, 8))
         return ms, np.array(list(cnt), dtype=np.int64)
 
+    def counters(self):
+        """cvxg_get_counters: {ruiz_extensions, spec_pairs, spec_pairs_used, factor_attempts, regularized}."""
+        out = (C.c_longlong * 5)()
+        self._check(self.lib.cvxg_get_counters(self.h, out, 5))
+        return dict(zip(("ruiz_extensions", "spec_pairs", "spec_pairs_used", "factor_attempts", "regularized"),
+                        (int(v) for v in out)))
+
 
 def batch_barrier_solve(engines, pars, termination: int = 0):
     """cvxg_batch_barrier_solve: the barrier solves of independent engines (one per GPU, config C5) concurrently from

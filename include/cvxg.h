@@ -298,6 +298,10 @@ int cvxg_get_phase_times(cvxg_ctx* ctx, double* ms, int count);
 /* cvxg_get_phase_times plus, per phase, the number of recorded occurrences its mean is over (occurrences may be NULL):
  * a phase that not every step runs (the inline assembly [0]) is then weighted by its occurrences, not by steps. */
 int cvxg_get_phase_stats(cvxg_ctx* ctx, double* ms, int* occurrences, int count);
+/* Diagnostic counters since cvxg_create (up to count of them): [0] Ruiz lookahead extensions, [1] speculative
+ * regularized pairs launched (chol(Q) and chol(Q + 1e-10 I) side by side after a regularized direction), [2] pairs
+ * whose second attempt was the one kept, [3] factorization attempts, [4] regularized directions. */
+int cvxg_get_counters(cvxg_ctx* ctx, long long* out, int count);
 
 /* The Newton step's Ruiz lookahead (cholesky_solve, MatrixUtils.scala:240-268 as restated in k_vec.hip): the next
  * step first launches `sweeps` Ruiz sweeps (the last step's count + 1 by default, RUIZ_MAX = 20 on a fresh

@@ -128,7 +128,7 @@ def test_jni_glue_binds_every_scala_native_and_every_step_entry():
 
 
 # C-ABI entry points a Scala caller has no use for: instrumentation and the host-only schedule dump
-_JNI_EXEMPT = {"cvxg_set_timing", "cvxg_get_phase_times", "cvxg_get_phase_stats", "cvxg_set_ruiz_lookahead",
+_JNI_EXEMPT = {"cvxg_set_timing", "cvxg_get_phase_times", "cvxg_get_phase_stats", "cvxg_get_counters", "cvxg_set_ruiz_lookahead",
                "cvxg_chol_schedule"}
 
 
