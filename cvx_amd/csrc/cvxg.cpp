@@ -386,7 +386,7 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
 constexpr bool CHAIN_OWN_B2_DEFAULT = true;
 static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles, int near = 0,
                                                  double boost = 0.0, int band = 0, bool eager = true,
-                                                 bool own_b2 = false) {
+                                                 bool own_b2 = false, bool group8 = false) {
   struct Task {
     int type, i, j, k, cnt;
     double dur, bl, avail;
@@ -410,7 +410,8 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   // (measured ~22 us per block), UPDATE4 for its measured ~14 us plus the contention of a full chip.  With the
   // former 18 / 10 the simulated chain ran slower and the workers faster than on the device, so the emitted order
   // put TRSM(k+2, k) -- which the chain needs next -- behind trailing updates: 1.77 -> 1.57 ms per factorization.
-  const double d_potrf = 10.0, d_trsm = 6.0, d_upd = 5.5, d_upd4 = 16.0;
+  // (group8: UPDATE8, eight panels per read-modify-write where a whole aligned group of eight fits before the singles)
+  const double d_potrf = 10.0, d_trsm = 6.0, d_upd = 5.5, d_upd4 = 16.0, d_upd8 = 29.0;
   for (int k = 0; k < nb; ++k) {  // (k, type) order is a topological order
     potrf_id[k] = (int)T.size();
     T.push_back({0, k, k, k, 1, d_potrf, 0, 0, k > 0 ? 1 : 0});
@@ -421,14 +422,21 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
     for (int j = k + 1; j < nb; ++j)
       for (int i = j; i < nb; ++i) {
         const bool band = i - j < near;  // near-diagonal tiles: single updates (each panel as soon as it is done)
-        const bool grp = group && !band && (k % 4 == 0) && (k + 4 <= j - singles);
-        const bool inside = group && !band && (k % 4 != 0) && ((k & ~3) + 4 <= j - singles);
-        if (inside) continue;  // covered by the group starting at k & ~3
-        const int cnt = grp ? 4 : 1;
+        // the group covering panel k: aligned eight, else aligned four, else single
+        int gs = k, cnt = 1;
+        if (group8 && !band && (k & ~7) + 8 <= j - singles) {
+          gs = k & ~7;
+          cnt = 8;
+        } else if (group && !band && (k & ~3) + 4 <= j - singles) {
+          gs = k & ~3;
+          cnt = 4;
+        }
+        if (gs != k) continue;  // covered by the group starting at gs
         const int id = (int)T.size();
         for (int kk = k; kk < k + cnt; ++kk) upd_id[upd_base[tri(i, j)] + kk] = id;
         const int npanel = (i == j) ? cnt : 2 * cnt;
-        T.push_back({grp ? 3 : 2, i, j, k, cnt, (grp ? d_upd4 : d_upd) * (i == j ? 0.75 : 1.0), 0, 0,
+        T.push_back({cnt == 8 ? 4 : cnt == 4 ? 3 : 2, i, j, k, cnt,
+                     (cnt == 8 ? d_upd8 : cnt == 4 ? d_upd4 : d_upd) * (i == j ? 0.75 : 1.0), 0, 0,
                      npanel + (k > 0 ? 1 : 0)});
       }
   }
@@ -467,8 +475,8 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   pending.push({0.0, potrf_id[0]});
   std::vector<unsigned> order;
   order.reserve(T.size());
-  auto code = [](const Task& x) {
-    return ((unsigned)x.type << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j;
+  auto code = [](const Task& x) {  // task word: type 1 TRSM, 2 UPDATE, 3 UPDATE4, 0 UPDATE8 (POTRF is never listed)
+    return ((unsigned)(x.type & 3) << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j;
   };
   // own_b2: the chain workgroups also apply panel b-2 to block row b (UPDATE(k+2,k+2,k), UPDATE(k+2,k+1,k); always
   // single-panel tasks: the groups of four end two panels before the diagonal)
@@ -527,7 +535,8 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
 // of 100 us for the near-diagonal updates and next-row TRSMs the chain waits on (band 3).  A/B at C3 (boost 0 /
 // band 2 -> 100 / 3): Cholesky 1.553, 1.552, 1.556 -> 1.498, 1.529, 1.502 ms.
 static std::vector<unsigned> chol_schedule(int nblk, int workers, bool own_b2) {
-  return build_chol_schedule(nblk, workers, 1, 2, 0, 100.0, 3, true, own_b2);
+  const char* g8 = getenv("CVXG_DF_GROUP8");  // eight-panel update groups (UPDATE8)
+  return build_chol_schedule(nblk, workers, 1, 2, 0, 100.0, 3, true, own_b2, g8 && atoi(g8) != 0);
 }
 
 extern "C" int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* relaunches) {

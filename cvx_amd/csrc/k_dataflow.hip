@@ -94,6 +94,30 @@ __device__ bool df_wait(const int* state, int idx, int want, int* abortw, DevCtr
   }
 }
 
+// Thread 0 waits until p0[0] >= w0, p1[0] >= w1 and p2[0] >= w2 (p2 may be null) -- the worker's dependency test.  The
+// polls are loaded together, so a task whose inputs are already final starts after one memory round trip instead of one
+// per input; only the words still short are polled again.  Same exits as df_wait (the abort word every 16th spin).
+__device__ bool df_wait3(const int* p0, int w0, const int* p1, int w1, const int* p2, int w2, int* abortw, DevCtrl* ctrl) {
+  const unsigned long long t0 = spin_clock();
+  bool n0 = true, n1 = true, n2 = p2 != nullptr;
+  for (unsigned spins = 0;; ++spins) {
+    const int v0 = n0 ? df_poll(p0) : w0;
+    const int v1 = n1 ? df_poll(p1) : w1;
+    const int v2 = n2 ? df_poll(p2) : w2;
+    n0 = v0 < w0;
+    n1 = v1 < w1;
+    n2 = v2 < w2;
+    if (!(n0 || n1 || n2)) return true;
+    if ((spins & 15) == 15 && df_poll(abortw)) return false;
+    if (spin_expired(spins, t0)) {
+      __hip_atomic_store(abortw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicExch(&ctrl->df_status, 2);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // Stage a 64 x 64 tile (descriptor m, leading dimension ld) into LDS [64][DF_SP]: 8 x 16-B sc1 loads per thread.
 __device__ __forceinline__ void df_stage(double* __restrict__ dst, const Sc1Mem& m, int ld) {
   const int tid = threadIdx.x;
@@ -218,9 +242,11 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
   }
 }
 
-// UPDATE4(i,j,k0): A_ij -= sum_{k=k0}^{k0+3} L_ik L_jk^T — one read-modify-write of the tile for four panels,
-// with the operand tiles of panel k+1 loaded into registers while the MFMAs of panel k run (two LDS buffers).
-__device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0, double* smem, const QFold& qf) {
+// UPDATE4 / UPDATE8 (G = 4, 8)(i,j,k0): A_ij -= sum_{k=k0}^{k0+G-1} L_ik L_jk^T — one read-modify-write of the tile
+// for G panels, with the operand tiles of panel k+1 loaded into registers while the MFMAs of panel k run (two LDS
+// buffers).  The accumulator is the FP64 tile itself, so G panels in one task are the same bits as in G / 4 tasks.
+template <int G>
+__device__ void df_updateg(double* __restrict__ L, int ld, int i, int j, int k0, double* smem, const QFold& qf) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const bool active = !(i == j && wc > wr);
@@ -235,16 +261,16 @@ __device__ void df_update4(double* __restrict__ L, int ld, int i, int j, int k0,
   df_put(smem, vi);
   if (!diag) df_put(smem + NB * DF_SP, vj);
 #pragma unroll 1
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < G; ++q) {
     double* Pi = smem + (q & 1) * 2 * NB * DF_SP;
     double* Pj = diag ? Pi : Pi + NB * DF_SP;
-    if (q < 3) {
+    if (q < G - 1) {
       df_load(vi, tile(i, k0 + q + 1), ld);
       if (!diag) df_load(vj, tile(j, k0 + q + 1), ld);
     }
     __syncthreads();  // panel q staged; every wave is done with panel q - 1 (the other buffer)
     if (active) df_mfma(acc, Pi, Pj, -1.0, wr, wc, lane);
-    if (q < 3) {
+    if (q < G - 1) {
       double* Ni = smem + ((q + 1) & 1) * 2 * NB * DF_SP;
       df_put(Ni, vi);
       if (!diag) df_put(Ni + NB * DF_SP, vj);
@@ -847,6 +873,10 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     return;
   }
   // ---- roles 2..: claim the remaining tasks in the host-built order ---------------------------
+  // The dependency polls of a task are loaded together (df_wait3): a task whose inputs are final starts one memory
+  // round trip after its claim instead of three (A/B at C3: Cholesky 1.29 -> 1.09 ms; taking the next claim during the
+  // previous task's drain as well gave nothing more, and claiming a whole task ahead made it 1.84 ms: a claimed task
+  // then waits behind its worker's current one).
   int my_idx = -1;  // thread 0: claimed task index (trace)
   for (;;) {
     if (tid == 0) {
@@ -866,13 +896,13 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     if (tid == 0) {
       bool ok;
       if (type == 1) {  // all of Linv_kk published (w_k is awaited inside the task)
-        ok = df_wait(cflag, k, 4, abortw, ctrl) && df_wait(state, df_tri(i, k), k, abortw, ctrl);
-      } else if (type == 3) {  // panels k..k+3: TRSM(., k+3) done implies the earlier ones (tile order)
-        ok = df_wait(state, df_tri(i, k + 3), k + 4, abortw, ctrl) &&
-             df_wait(state, df_tri(j, k + 3), k + 4, abortw, ctrl) && df_wait(state, df_tri(i, j), k, abortw, ctrl);
+        ok = df_wait3(cflag + k, 4, state + df_tri(i, k), k, nullptr, 0, abortw, ctrl);
+      } else if (type == 3 || type == 0) {  // panels k..k+G-1: TRSM(., k+G-1) done implies the earlier ones
+        const int g = type == 3 ? 4 : 8;
+        ok = df_wait3(state + df_tri(i, k + g - 1), k + g, state + df_tri(j, k + g - 1), k + g, state + df_tri(i, j), k,
+                      abortw, ctrl);
       } else {
-        ok = df_wait(state, df_tri(i, k), k + 1, abortw, ctrl) && df_wait(state, df_tri(j, k), k + 1, abortw, ctrl) &&
-             df_wait(state, df_tri(i, j), k, abortw, ctrl);
+        ok = df_wait3(state + df_tri(i, k), k + 1, state + df_tri(j, k), k + 1, state + df_tri(i, j), k, abortw, ctrl);
       }
       s_ok = ok;
       if (trace) trace[4 * my_idx + 1] = __builtin_amdgcn_s_memrealtime();
@@ -885,9 +915,13 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       if (!df_trsm(L, ld, i, k, rhs, nrhs, Linv, smem, state, rhscnt, abortw, ctrl, &s_ok, qf)) break;
       done_idx = df_tri(i, k);
     } else if (type == 3) {
-      df_update4(L, ld, i, j, k, smem, qf);
+      df_updateg<4>(L, ld, i, j, k, smem, qf);
       done_idx = df_tri(i, j);
       done_val = k + 4;
+    } else if (type == 0) {
+      df_updateg<8>(L, ld, i, j, k, smem, qf);
+      done_idx = df_tri(i, j);
+      done_val = k + 8;
     } else {
       df_update(L, ld, i, j, k, smem, qf);
       done_idx = df_tri(i, j);
