@@ -96,7 +96,8 @@ __device__ bool df_wait(const int* state, int idx, int want, int* abortw, DevCtr
 
 // Thread 0 waits until p0[0] >= w0, p1[0] >= w1 and p2[0] >= w2 (p2 may be null) -- the worker's dependency test.  The
 // polls are loaded together, so a task whose inputs are already final starts after one memory round trip instead of one
-// per input; only the words still short are polled again.  Same exits as df_wait (the abort word every 16th spin).
+// per input; only the words still short are polled again.  Same exits as df_wait (the abort word at the first spin
+// that finds an input short, then every 16th).
 __device__ bool df_wait3(const int* p0, int w0, const int* p1, int w1, const int* p2, int w2, int* abortw, DevCtrl* ctrl) {
   const unsigned long long t0 = spin_clock();
   bool n0 = true, n1 = true, n2 = p2 != nullptr;
@@ -108,7 +109,7 @@ __device__ bool df_wait3(const int* p0, int w0, const int* p1, int w1, const int
     n1 = v1 < w1;
     n2 = v2 < w2;
     if (!(n0 || n1 || n2)) return true;
-    if ((spins & 15) == 15 && df_poll(abortw)) return false;
+    if ((spins & 15) == 0 && df_poll(abortw)) return false;
     if (spin_expired(spins, t0)) {
       __hip_atomic_store(abortw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       atomicExch(&ctrl->df_status, 2);
@@ -444,7 +445,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   __shared__ int s_ok;
   __shared__ int s_next;
   int* counter = work;
-  int* abortw = work + 1;
+  int* abortw = work + 32;  // own cache line: the claim counter's line takes every worker's atomic
   int* state = work + 64;  // own cache lines
   int* cflag = work + 64 + nblk * (nblk + 1) / 2;  // cflag[k]: row-blocks of L_kk^-1 published (0..4)
   int* rhscnt = cflag + nblk;  // rhscnt[i]: worker TRSM(i, .) rhs updates applied to rhs block i (in panel order)
@@ -873,20 +874,18 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
     return;
   }
   // ---- roles 2..: claim the remaining tasks in the host-built order ---------------------------
-  // The dependency polls of a task are loaded together (df_wait3): a task whose inputs are final starts one memory
-  // round trip after its claim instead of three (A/B at C3: Cholesky 1.29 -> 1.09 ms; taking the next claim during the
-  // previous task's drain as well gave nothing more, and claiming a whole task ahead made it 1.84 ms: a claimed task
-  // then waits behind its worker's current one).
+  // The claim is one atomic on the counter; the abort word lives on its own cache line and is read only by the waits
+  // (a task that finds an input short), not before every claim.  With the abort word beside the counter, every
+  // worker's claim-time poll queued behind the other workers' atomics on that one line: Cholesky 1.29 -> 1.09 ms at
+  // C3 once it moved.  The dependency polls of a task go out together (df_wait3).
   int my_idx = -1;  // thread 0: claimed task index (trace)
   for (;;) {
     if (tid == 0) {
       unsigned t = 0xffffffffu;
-      if (!df_poll(abortw)) {
-        const int idx = atomicAdd(counter, 1);
-        if (idx < ntasks) t = tasks[idx];
-        my_idx = idx;
-        if (trace && idx < ntasks) trace[4 * idx] = __builtin_amdgcn_s_memrealtime();
-      }
+      const int idx = atomicAdd(counter, 1);
+      if (idx < ntasks) t = tasks[idx];
+      my_idx = idx;
+      if (trace && idx < ntasks) trace[4 * idx] = __builtin_amdgcn_s_memrealtime();
       s_task = t;
     }
     __syncthreads();
@@ -938,7 +937,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   }
 }
 
-// work: [0] counter, [1] abort word, [2] role ticket, [64 ..) one state word per lower tile, then one chain flag and
+// work: [0] counter, [2] role ticket, [32] abort word, [64 ..) one state word per lower tile, then one chain flag and
 // one rhs counter per diagonal block; zeroed before every launch.
 bool chol_dataflow_variant_ok(int v) { return v == 0 || v == 1 || v == 2 || v == 3 || v == 7 || v == 11 || v == 15; }
 size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + 2 * (size_t)nblk; }

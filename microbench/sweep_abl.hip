@@ -7,6 +7,7 @@
 //   M4  M1 with the reciprocal replaced by the pivot itself: the update issue alone (numerically meaningless)
 //   M5  M4 with plain v_fma_f64 (no DPP) on the updates: the DPP cost
 //   M6  M1 with the off-chain updates of column j issued in two halves around the next pivot's reciprocal
+//   M7  M1 with the reciprocal's seven steps as asm statements and the off-chain updates spread between them
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off microbench/sweep_abl.hip -o microbench/sweep_abl
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -44,6 +45,41 @@ __device__ __forceinline__ double rcp_fma(double p) {
   return y;
 }
 
+// the reciprocal's steps as separate asm statements (the same instructions rcp_nr compiles to: v_rcp_f64, then twice
+// t = p y; u = 2 - t; y = y u), so that they stay where they are written among the update fmacs
+__device__ __forceinline__ double a_rcp(double p) {
+  double y;
+  asm volatile("v_rcp_f64 %0, %1\n\ts_nop 1" : "=v"(y) : "v"(p));  // (trans -> VALU use: wait states)
+  return y;
+}
+__device__ __forceinline__ double a_mul(double x, double y) {
+  double r;
+  asm volatile("v_mul_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+__device__ __forceinline__ double a_two_minus(double t) {
+  double r;
+  asm volatile("v_add_f64 %0, -%1, 2.0" : "=v"(r) : "v"(t));
+  return r;
+}
+// the I-th of the 2 R off-chain updates of column J (R = 14 - J columns c = J + 2 .., a then b)
+template <int J, int I>
+__device__ __forceinline__ void rest_one(double (&a)[16], double (&b)[16], double nta, double ntb) {
+  constexpr int NR = (J + 2 < 16 ? 14 - J : 0);
+  if constexpr (I < 2 * NR) {
+    constexpr int c = J + 2 + I / 2;
+    if constexpr (I % 2 == 0) fmac_bc<c>(a[c], a[J], nta);
+    else fmac_bc<c>(b[c], a[J], ntb);
+  }
+}
+template <int J, int I0, int N>
+__device__ __forceinline__ void rest_range(double (&a)[16], double (&b)[16], double nta, double ntb) {
+  if constexpr (N > 0) {
+    rest_one<J, I0>(a, b, nta, ntb);
+    rest_range<J, I0 + 1, N - 1>(a, b, nta, ntb);
+  }
+}
+
 template <int M, int J, int... Cs>
 __device__ __forceinline__ void rest(double (&a)[16], double (&b)[16], double nta, double ntb, int lo,
                                      std::integer_sequence<int, Cs...>) {
@@ -72,7 +108,24 @@ __device__ __forceinline__ void step(double (&a)[16], double (&b)[16], double& p
         fmac_bc<J + 1>(b[J + 1], a[J], ntb);
       }
       piv = bc<J + 1>(a[J + 1]);
-      if constexpr (M == 6) {
+      if constexpr (M == 7) {
+        // the reciprocal chain with the off-chain updates spread between its seven steps (K per gap)
+        constexpr int K = (2 * NR + 6) / 7;
+        double y = a_rcp(piv);
+        rest_range<J, 0 * K, K>(a, b, nta, ntb);
+        double t = a_mul(piv, y);
+        rest_range<J, 1 * K, K>(a, b, nta, ntb);
+        double u = a_two_minus(t);
+        rest_range<J, 2 * K, K>(a, b, nta, ntb);
+        y = a_mul(y, u);
+        rest_range<J, 3 * K, K>(a, b, nta, ntb);
+        t = a_mul(piv, y);
+        rest_range<J, 4 * K, K>(a, b, nta, ntb);
+        u = a_two_minus(t);
+        rest_range<J, 5 * K, K>(a, b, nta, ntb);
+        rinv = a_mul(y, u);
+        rest_range<J, 6 * K, 2 * NR - 6 * K>(a, b, nta, ntb);
+      } else if constexpr (M == 6) {
         // first half of the off-chain updates, then the reciprocal, then the second half
         rest<M, J>(a, b, nta, ntb, 0, std::make_integer_sequence<int, NR / 2>{});
         rinv = rcp_nr(piv);
@@ -86,7 +139,7 @@ __device__ __forceinline__ void step(double (&a)[16], double (&b)[16], double& p
         else rinv = rcp_nr(piv);
       }
     }
-    if constexpr (M != 3 && M != 6) rest<M, J>(a, b, nta, ntb, 0, std::make_integer_sequence<int, NR>{});
+    if constexpr (M != 3 && M != 6 && M != 7) rest<M, J>(a, b, nta, ntb, 0, std::make_integer_sequence<int, NR>{});
     step<M, J + 1>(a, b, piv, rinv, sv, pmin, firstbad);
   }
 }
@@ -191,5 +244,6 @@ int main() {
   run<4>(dD, dP, dO, dc, L);
   run<5>(dD, dP, dO, dc, L);
   run<6>(dD, dP, dO, dc, L);
+  run<7>(dD, dP, dO, dc, L);
   return 0;
 }
