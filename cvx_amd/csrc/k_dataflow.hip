@@ -399,8 +399,10 @@ __device__ __forceinline__ d4f ch_trsm(const double (&af)[16], const double* E, 
   return acc0 + acc1;
 }
 // the 10 lower 16 x 16 blocks of a 64 x 64 tile, 3 / 3 / 2 / 2 per wave (-1: none)
-constexpr int kChIB[4][3] = {{0, 3, 3}, {1, 3, 2}, {1, 3, -1}, {2, 2, -1}};
-constexpr int kChJB[4][3] = {{0, 0, 3}, {0, 1, 2}, {1, 2, -1}, {0, 1, -1}};
+// (wave 0 holds only D_00, which POTRF's first sweep reads: with a deferred publication it goes from its last slice
+// straight into the sweep while waves 1..3 finish and store the other nine blocks, ps.cntD)
+constexpr int kChIB[4][3] = {{0, -1, -1}, {1, 1, 2}, {2, 2, 3}, {3, 3, 3}};
+constexpr int kChJB[4][3] = {{0, -1, -1}, {0, 1, 2}, {0, 1, 3}, {0, 1, 2}};
 // UPDATE slice: D -= L'[:, 16 cb..] L'[:, 16 cb..]^T on wave W's blocks (compile-time, so fragments are picked
 // statically); Lp = L' with row stride DF_SP
 template <int W>
@@ -632,6 +634,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           }
         }
         potrf64w_reset(ps);  // the slices leave POTRF's L^-1 workspace and flags alone: clear them off the chain
+        if (kDefer && tid == 0) cs.lpub = 0;  // (POTRF(b-2)'s pre hook is long done; the barrier below orders it)
         mark(k, 1, 1);
         // L_b,k, row stride DF_SP: written over A_b,k in Sa (every wave holds its row-block of A in af before the first
         // slice's barrier), where it stays for the rhs correction at the end of POTRF(b) — no copy before POTRF
@@ -797,10 +800,14 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           if (ib >= 0) c16_store(ps.S + 16 * ib * P64_SP + 16 * jb, P64_SP, dacc[q], lane);
         }
         // L_b,k goes to HBM off the chain: waves 1..3 of POTRF(b) store it from Sa and raise state(b, k) (pre hook
-        // below), while wave 0 runs the first sweep -- no drain round trip between the last slice and POTRF(b)
+        // below), while wave 0 runs the first sweep -- no drain round trip between the last slice and POTRF(b).  No
+        // barrier either: wave 0 starts the sweep on its own D_00, and waves 1..3 count their stored blocks into
+        // ps.cntD, which POTRF's first T / U and phase A wait for.
         if (kDefer) {
-          if (tid == 0) cs.lpub = 0;
-          __syncthreads();
+          if (wv > 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) p64w_add(&ps.cntD);
+          }
         } else {
           publish(df_tri(b, k), k + 1);  // L_b,k stored
         }
@@ -862,7 +869,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       };
       if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre,
                                    kTag ? ltag : nullptr, tag_gen, kDpp,
-                                   trace ? trace + 4 * (size_t)(ntasks + 5 * b + 3) : nullptr)) {
+                                   trace ? trace + 4 * (size_t)(ntasks + 5 * b + 3) : nullptr, kDefer && b > 0)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }

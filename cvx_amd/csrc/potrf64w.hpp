@@ -39,6 +39,7 @@ struct Potrf64wSmem {
   int fail;
   int fP, fT;                 // wave 0: steps whose P / T are published
   int cntT[4], cntU[4];       // waves 1..3 done with phase A / B of step kb
+  int cntD;                   // (wait_d) waves 1..3 done storing their blocks of the staged tile
 };
 
 __device__ __forceinline__ int p64w_load(const int* f) {
@@ -351,7 +352,8 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
                                                 Fix fix = Fix(), double early_min = 0.0, Pre pre = Pre(),
                                                 double* ltag = nullptr, unsigned long long tag_gen = 0,
-                                                bool dpp_sweep = false, unsigned long long* rb_stamp = nullptr) {
+                                                bool dpp_sweep = false, unsigned long long* rb_stamp = nullptr,
+                                                bool wait_d = false) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -372,7 +374,9 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_publish(&sm.fP, kb + 1);
       if (kb < 3) {
-        if (kb >= 1 && !p64w_wait(sm, &sm.cntU[kb - 1], 3)) {
+        // (wait_d: the caller entered without a barrier behind the staged tile; wave 0 factored its own block D_00
+        // and waits here for waves 1..3's blocks before the first T / U)
+        if ((kb >= 1 && !p64w_wait(sm, &sm.cntU[kb - 1], 3)) || (kb == 0 && wait_d && !p64w_wait(sm, &sm.cntD, 3))) {
           ok = false;
           break;
         }
@@ -390,7 +394,8 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
     pre(w, lane);
 #pragma unroll 1
     for (int kb = 0; kb < 4 && ok; ++kb) {
-      ok = p64w_wait(sm, &sm.fP, kb + 1) && (kb == 0 || p64w_wait(sm, &sm.cntU[kb - 1], 3));
+      ok = p64w_wait(sm, &sm.fP, kb + 1) && (kb == 0 ? (!wait_d || p64w_wait(sm, &sm.cntD, 3))
+                                                      : p64w_wait(sm, &sm.cntU[kb - 1], 3));
       if (!ok) break;
       P64_STAMP(1 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -475,6 +480,7 @@ __device__ __forceinline__ void potrf64w_reset(Potrf64wSmem& sm) {
     sm.cntU[tid] = 0;
   }
   if (tid == 0) {
+    sm.cntD = 0;
     sm.fail = 0;
     sm.fP = 0;
     sm.fT = 0;
