@@ -384,9 +384,13 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
 // that task's dependents in the emitted order, which keeps the launch deadlock-free.
 // the main factorization's chain workgroups apply panel b-2 to block row b themselves (k_dataflow.hip, own_b2)
 constexpr bool CHAIN_OWN_B2_DEFAULT = true;
+struct SchedTimes {  // estimated task times of the list scheduler (us)
+  double potrf = 10.0, trsm = 6.0, upd = 5.5, upd4 = 16.0, upd8 = 29.0;
+};
 static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles, int near = 0,
                                                  double boost = 0.0, int band = 0, bool eager = true,
-                                                 bool own_b2 = false, bool group8 = false) {
+                                                 bool own_b2 = false, bool group8 = false,
+                                                 SchedTimes st = SchedTimes()) {
   struct Task {
     int type, i, j, k, cnt;
     double dur, bl, avail;
@@ -411,7 +415,7 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   // former 18 / 10 the simulated chain ran slower and the workers faster than on the device, so the emitted order
   // put TRSM(k+2, k) -- which the chain needs next -- behind trailing updates: 1.77 -> 1.57 ms per factorization.
   // (group8: UPDATE8, eight panels per read-modify-write where a whole aligned group of eight fits before the singles)
-  const double d_potrf = 10.0, d_trsm = 6.0, d_upd = 5.5, d_upd4 = 16.0, d_upd8 = 29.0;
+  const double d_potrf = st.potrf, d_trsm = st.trsm, d_upd = st.upd, d_upd4 = st.upd4, d_upd8 = st.upd8;
   for (int k = 0; k < nb; ++k) {  // (k, type) order is a topological order
     potrf_id[k] = (int)T.size();
     T.push_back({0, k, k, k, 1, d_potrf, 0, 0, k > 0 ? 1 : 0});
@@ -536,7 +540,12 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
 // band 2 -> 100 / 3): Cholesky 1.553, 1.552, 1.556 -> 1.498, 1.529, 1.502 ms.
 static std::vector<unsigned> chol_schedule(int nblk, int workers, bool own_b2) {
   const char* g8 = getenv("CVXG_DF_GROUP8");  // eight-panel update groups (UPDATE8)
-  return build_chol_schedule(nblk, workers, 1, 2, 0, 100.0, 3, true, own_b2, g8 && atoi(g8) != 0);
+  SchedTimes st;
+  double boost = 100.0;
+  int band = 3, singles = 2;
+  if (const char* e = getenv("CVXG_DF_SCHED"))  // (experiments) "potrf,trsm,upd,upd4,boost,band,singles"
+    sscanf(e, "%lf,%lf,%lf,%lf,%lf,%d,%d", &st.potrf, &st.trsm, &st.upd, &st.upd4, &boost, &band, &singles);
+  return build_chol_schedule(nblk, workers, 1, singles, 0, boost, band, true, own_b2, g8 && atoi(g8) != 0, st);
 }
 
 extern "C" int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* relaunches) {
