@@ -543,8 +543,9 @@ static std::vector<unsigned> chol_schedule(int nblk, int workers, bool own_b2) {
   SchedTimes st;
   double boost = 100.0;
   int band = 3, singles = 2;
-  if (const char* e = getenv("CVXG_DF_SCHED"))  // (experiments) "potrf,trsm,upd,upd4,boost,band,singles"
-    sscanf(e, "%lf,%lf,%lf,%lf,%lf,%d,%d", &st.potrf, &st.trsm, &st.upd, &st.upd4, &boost, &band, &singles);
+  if (const char* e = getenv("CVXG_DF_SCHED"))  // (experiments) "potrf:trsm:upd:upd4:boost:band:singles"
+    sscanf(e, "%lf:%lf:%lf:%lf:%lf:%d:%d", &st.potrf, &st.trsm, &st.upd, &st.upd4, &boost, &band, &singles);
+  singles = std::max(singles, 2);  // the chain's own panel b-2 tasks must stay single-panel
   return build_chol_schedule(nblk, workers, 1, singles, 0, boost, band, true, own_b2, g8 && atoi(g8) != 0, st);
 }
 
