@@ -385,7 +385,10 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
 // the main factorization's chain workgroups apply panel b-2 to block row b themselves (k_dataflow.hip, own_b2)
 constexpr bool CHAIN_OWN_B2_DEFAULT = true;
 struct SchedTimes {  // estimated task times of the list scheduler (us)
-  double potrf = 10.0, trsm = 6.0, upd = 5.5, upd4 = 16.0, upd8 = 29.0;
+  // round 5, after the worker fix: the measured medians (TRSM 5.7, UPDATE 4.1, UPDATE4 12.3 us) and a chain period of
+  // potrf + trsm + 0.75 upd = 15 us.  Against the former 10 / 6 / 5.5 / 16: Cholesky 1.083 -> 1.066 ms (same-box A/B,
+  // profiles/r05/ab_sched)
+  double potrf = 7.0, trsm = 5.0, upd = 4.0, upd4 = 12.5, upd8 = 24.0;
 };
 static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles, int near = 0,
                                                  double boost = 0.0, int band = 0, bool eager = true,
@@ -543,7 +546,7 @@ static std::vector<unsigned> chol_schedule(int nblk, int workers, bool own_b2) {
   SchedTimes st;
   double boost = 100.0;
   int band = 3, singles = 2;
-  if (const char* e = getenv("CVXG_DF_SCHED"))  // (experiments) "potrf:trsm:upd:upd4:boost:band:singles"
+  if (const char* e = getenv("CVXG_DF_SCHED"))  // (experiments) "potrf:trsm:upd:upd4:boost:band:singles" (all seven)
     sscanf(e, "%lf:%lf:%lf:%lf:%lf:%d:%d", &st.potrf, &st.trsm, &st.upd, &st.upd4, &boost, &band, &singles);
   singles = std::max(singles, 2);  // the chain's own panel b-2 tasks must stay single-panel
   return build_chol_schedule(nblk, workers, 1, singles, 0, boost, band, true, own_b2, g8 && atoi(g8) != 0, st);
