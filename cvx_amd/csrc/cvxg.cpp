@@ -385,10 +385,11 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
 // the main factorization's chain workgroups apply panel b-2 to block row b themselves (k_dataflow.hip, own_b2)
 constexpr bool CHAIN_OWN_B2_DEFAULT = true;
 struct SchedTimes {  // estimated task times of the list scheduler (us)
-  // round 5, after the worker fix: the measured medians (TRSM 5.7, UPDATE 4.1, UPDATE4 12.3 us) and a chain period of
-  // potrf + trsm + 0.75 upd = 15 us.  Against the former 10 / 6 / 5.5 / 16: Cholesky 1.083 -> 1.066 ms (same-box A/B,
-  // profiles/r05/ab_sched)
-  double potrf = 7.0, trsm = 5.0, upd = 4.0, upd4 = 12.5, upd8 = 24.0;
+  // round 5, after the worker fix: the measured medians (TRSM 5.7, UPDATE 4.1, UPDATE4 12.3 us) and a simulated chain
+  // period potrf + trsm + 0.75 upd = 14 us.  Same-box A/Bs (profiles/r05/ab_sched, ab_sched2): the former 10 / 6 /
+  // 5.5 / 16 1.083 ms, 7 / 5 / 4 / 12.5 1.064 ms, 6 / 5 / 4 / 12.5 1.048 ms; the order is sensitive to the ratio of the
+  // simulated chain period to UPDATE4 (1.36: 1.094 ms, 1.04: 1.085 ms)
+  double potrf = 6.0, trsm = 5.0, upd = 4.0, upd4 = 12.5, upd8 = 24.0;
 };
 static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles, int near = 0,
                                                  double boost = 0.0, int band = 0, bool eager = true,

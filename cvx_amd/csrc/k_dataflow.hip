@@ -156,6 +156,9 @@ __device__ __forceinline__ void df_put(double* __restrict__ dst, const f64x2 (&v
   }
 }
 
+#ifndef CVXG_DF_MFMA_PIPE  // (experiment switch)
+#define CVXG_DF_MFMA_PIPE 0
+#endif
 // acc (wave (wr, wc): 32 x 32 block = 2 x 2 MFMA tiles) += sgn * P_i[rows] . P_j[cols]^T over K = 64.
 __device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, const double* Pj, double sgn, int wr,
                                         int wc, int lane) {
@@ -173,7 +176,29 @@ __device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, cons
       for (int nj = 0; nj < 2; ++nj)
         acc[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi], fb[nj], acc[mi][nj], 0, 0, 0);
   }
+#if CVXG_DF_MFMA_PIPE
+  // issue order for the unrolled loop (the LDS reads of two k-steps pair into ds_read2): the next pair's four reads
+  // right after the first two MFMAs of the current pair, so their round trip hides behind the other six
+  __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+  for (int p = 0; p < NB / 8; ++p) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    if (p + 1 < NB / 8) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+  }
+#endif
 }
+
+// (CVXG_DF_MFMA_PIPE: the updates run df_mfma on the negated tile with sgn = +1, df_neg before and after -- with
+// round-to-nearest every step of the MFMA's sum is symmetric under a sign flip, so -((-C) + sum a b) is
+// C + sum (-a) b bit for bit -- and the inner loop has no sign flip between an LDS read and its MFMA)
+__device__ __forceinline__ void df_neg(d4f (&acc)[2][2]) {
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = -acc[mi][nj];
+}
+constexpr double DF_UPD_SGN = CVXG_DF_MFMA_PIPE ? 1.0 : -1.0;
 
 // UPDATE(i,j,k): A_ij -= L_ik L_jk^T.  On a diagonal tile the strictly-upper 32 x 32 wave block is skipped.
 // The tile's C operand in MFMA accumulator layout: from L, or on its first touch (k == 0) Q from H.
@@ -230,7 +255,9 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
   }
   __syncthreads();
   if (active) {
-    df_mfma(acc, Pi, Pj, -1.0, wr, wc, lane);
+    if (CVXG_DF_MFMA_PIPE) df_neg(acc);
+    df_mfma(acc, Pi, Pj, DF_UPD_SGN, wr, wc, lane);
+    if (CVXG_DF_MFMA_PIPE) df_neg(acc);
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -255,6 +282,7 @@ __device__ void df_updateg(double* __restrict__ L, int ld, int i, int j, int k0,
   const Sc1Mem mC(L + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
   d4f acc[2][2];
   df_load_c(acc, mC, ld, i, j, qf.H && k0 == 0, qf, wr, wc, lane);
+  if (CVXG_DF_MFMA_PIPE) df_neg(acc);
   f64x2 vi[NB * NB / 512], vj[NB * NB / 512];
   auto tile = [&](int r, int k) { return Sc1Mem(L + (size_t)r * NB * ld + (size_t)k * NB, tile_bytes(ld)); };
   df_load(vi, tile(i, k0), ld);
@@ -270,7 +298,7 @@ __device__ void df_updateg(double* __restrict__ L, int ld, int i, int j, int k0,
       if (!diag) df_load(vj, tile(j, k0 + q + 1), ld);
     }
     __syncthreads();  // panel q staged; every wave is done with panel q - 1 (the other buffer)
-    if (active) df_mfma(acc, Pi, Pj, -1.0, wr, wc, lane);
+    if (active) df_mfma(acc, Pi, Pj, DF_UPD_SGN, wr, wc, lane);
     if (q < G - 1) {
       double* Ni = smem + ((q + 1) & 1) * 2 * NB * DF_SP;
       df_put(Ni, vi);
@@ -278,6 +306,7 @@ __device__ void df_updateg(double* __restrict__ L, int ld, int i, int j, int k0,
     }
   }
   if (active) {
+    if (CVXG_DF_MFMA_PIPE) df_neg(acc);
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
