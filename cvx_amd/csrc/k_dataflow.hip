@@ -94,6 +94,41 @@ __device__ bool df_wait(const int* state, int idx, int want, int* abortw, DevCtr
   }
 }
 
+#ifndef CVXG_DF_POLL_DEPTH  // (experiment switch) polls of the chain's flag waits kept in flight at once
+#define CVXG_DF_POLL_DEPTH 1
+#endif
+// Thread 0 waits until state[idx] >= want with CVXG_DF_POLL_DEPTH loads of the word in flight, issued a few hundred
+// cycles apart: the word is seen a fraction of a round trip after it lands instead of up to a whole one.  Same exits
+// as df_wait.
+__device__ bool df_wait_pipe(const int* state, int idx, int want, int* abortw, DevCtrl* ctrl) {
+  constexpr int D = CVXG_DF_POLL_DEPTH;
+  if constexpr (D <= 1) {
+    return df_wait(state, idx, want, abortw, ctrl);
+  } else {
+    const int* p = state + idx;
+    int v[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      v[q] = df_poll(p);
+      if (q + 1 < D) __builtin_amdgcn_s_sleep(4);
+    }
+    const unsigned long long t0 = spin_clock();
+    for (unsigned spins = 0;; ++spins) {
+      if (v[0] >= want) return true;  // (waits for the oldest load only)
+      if ((spins & 15) == 15 && df_poll(abortw)) return false;
+      if (spin_expired(spins, t0)) {
+        __hip_atomic_store(abortw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicExch(&ctrl->df_status, 2);
+        return false;
+      }
+#pragma unroll
+      for (int q = 0; q + 1 < D; ++q) v[q] = v[q + 1];
+      __builtin_amdgcn_s_sleep(4);
+      v[D - 1] = df_poll(p);
+    }
+  }
+}
+
 // Thread 0 waits until p0[0] >= w0, p1[0] >= w1 and p2[0] >= w2 (p2 may be null) -- the worker's dependency test.  The
 // polls are loaded together, so a task whose inputs are already final starts after one memory round trip instead of one
 // per input; only the words still short are polled again.  Same exits as df_wait (the abort word at the first spin
@@ -508,7 +543,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       if (tid == 0) __hip_atomic_store(state + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto wait = [&](const int* base, int idx, int want) -> bool {
-      if (tid == 0) s_ok = df_wait(base, idx, want, abortw, ctrl);
+      if (tid == 0) s_ok = df_wait_pipe(base, idx, want, abortw, ctrl);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       __syncthreads();
       return s_ok;
