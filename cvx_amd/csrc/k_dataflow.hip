@@ -94,41 +94,6 @@ __device__ bool df_wait(const int* state, int idx, int want, int* abortw, DevCtr
   }
 }
 
-#ifndef CVXG_DF_POLL_DEPTH  // (experiment switch) polls of the chain's flag waits kept in flight at once
-#define CVXG_DF_POLL_DEPTH 1
-#endif
-// Thread 0 waits until state[idx] >= want with CVXG_DF_POLL_DEPTH loads of the word in flight, issued a few hundred
-// cycles apart: the word is seen a fraction of a round trip after it lands instead of up to a whole one.  Same exits
-// as df_wait.
-__device__ bool df_wait_pipe(const int* state, int idx, int want, int* abortw, DevCtrl* ctrl) {
-  constexpr int D = CVXG_DF_POLL_DEPTH;
-  if constexpr (D <= 1) {
-    return df_wait(state, idx, want, abortw, ctrl);
-  } else {
-    const int* p = state + idx;
-    int v[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-      v[q] = df_poll(p);
-      if (q + 1 < D) __builtin_amdgcn_s_sleep(4);
-    }
-    const unsigned long long t0 = spin_clock();
-    for (unsigned spins = 0;; ++spins) {
-      if (v[0] >= want) return true;  // (waits for the oldest load only)
-      if ((spins & 15) == 15 && df_poll(abortw)) return false;
-      if (spin_expired(spins, t0)) {
-        __hip_atomic_store(abortw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        atomicExch(&ctrl->df_status, 2);
-        return false;
-      }
-#pragma unroll
-      for (int q = 0; q + 1 < D; ++q) v[q] = v[q + 1];
-      __builtin_amdgcn_s_sleep(4);
-      v[D - 1] = df_poll(p);
-    }
-  }
-}
-
 // Thread 0 waits until p0[0] >= w0, p1[0] >= w1 and p2[0] >= w2 (p2 may be null) -- the worker's dependency test.  The
 // polls are loaded together, so a task whose inputs are already final starts after one memory round trip instead of one
 // per input; only the words still short are polled again.  Same exits as df_wait (the abort word at the first spin
@@ -191,9 +156,6 @@ __device__ __forceinline__ void df_put(double* __restrict__ dst, const f64x2 (&v
   }
 }
 
-#ifndef CVXG_DF_MFMA_PIPE  // (experiment switch)
-#define CVXG_DF_MFMA_PIPE 0
-#endif
 // acc (wave (wr, wc): 32 x 32 block = 2 x 2 MFMA tiles) += sgn * P_i[rows] . P_j[cols]^T over K = 64.
 __device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, const double* Pj, double sgn, int wr,
                                         int wc, int lane) {
@@ -211,7 +173,6 @@ __device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, cons
       for (int nj = 0; nj < 2; ++nj)
         acc[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi], fb[nj], acc[mi][nj], 0, 0, 0);
   }
-#if CVXG_DF_MFMA_PIPE
   // issue order for the unrolled loop (the LDS reads of two k-steps pair into ds_read2): the next pair's four reads
   // right after the first two MFMAs of the current pair, so their round trip hides behind the other six
   __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
@@ -221,19 +182,18 @@ __device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, cons
     if (p + 1 < NB / 8) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
   }
-#endif
 }
 
-// (CVXG_DF_MFMA_PIPE: the updates run df_mfma on the negated tile with sgn = +1, df_neg before and after -- with
-// round-to-nearest every step of the MFMA's sum is symmetric under a sign flip, so -((-C) + sum a b) is
-// C + sum (-a) b bit for bit -- and the inner loop has no sign flip between an LDS read and its MFMA)
+// The updates run df_mfma on the negated tile with sgn = +1, df_neg before and after: with round-to-nearest every
+// step of the MFMA's sum is symmetric under a sign flip, so -((-C) + sum a b) is C + sum (-a) b bit for bit, and the
+// inner loop has no sign flip between an LDS read and its MFMA (with the issue order in df_mfma: Cholesky 1.052 ->
+// 1.043 ms, the same fingerprints; profiles/r05/ab_pipe)
 __device__ __forceinline__ void df_neg(d4f (&acc)[2][2]) {
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = -acc[mi][nj];
 }
-constexpr double DF_UPD_SGN = CVXG_DF_MFMA_PIPE ? 1.0 : -1.0;
 
 // UPDATE(i,j,k): A_ij -= L_ik L_jk^T.  On a diagonal tile the strictly-upper 32 x 32 wave block is skipped.
 // The tile's C operand in MFMA accumulator layout: from L, or on its first touch (k == 0) Q from H.
@@ -290,9 +250,9 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
   }
   __syncthreads();
   if (active) {
-    if (CVXG_DF_MFMA_PIPE) df_neg(acc);
-    df_mfma(acc, Pi, Pj, DF_UPD_SGN, wr, wc, lane);
-    if (CVXG_DF_MFMA_PIPE) df_neg(acc);
+    df_neg(acc);
+    df_mfma(acc, Pi, Pj, 1.0, wr, wc, lane);
+    df_neg(acc);
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -317,7 +277,7 @@ __device__ void df_updateg(double* __restrict__ L, int ld, int i, int j, int k0,
   const Sc1Mem mC(L + (size_t)i * NB * ld + (size_t)j * NB, tile_bytes(ld));
   d4f acc[2][2];
   df_load_c(acc, mC, ld, i, j, qf.H && k0 == 0, qf, wr, wc, lane);
-  if (CVXG_DF_MFMA_PIPE) df_neg(acc);
+  df_neg(acc);
   f64x2 vi[NB * NB / 512], vj[NB * NB / 512];
   auto tile = [&](int r, int k) { return Sc1Mem(L + (size_t)r * NB * ld + (size_t)k * NB, tile_bytes(ld)); };
   df_load(vi, tile(i, k0), ld);
@@ -333,7 +293,7 @@ __device__ void df_updateg(double* __restrict__ L, int ld, int i, int j, int k0,
       if (!diag) df_load(vj, tile(j, k0 + q + 1), ld);
     }
     __syncthreads();  // panel q staged; every wave is done with panel q - 1 (the other buffer)
-    if (active) df_mfma(acc, Pi, Pj, DF_UPD_SGN, wr, wc, lane);
+    if (active) df_mfma(acc, Pi, Pj, 1.0, wr, wc, lane);
     if (q < G - 1) {
       double* Ni = smem + ((q + 1) & 1) * 2 * NB * DF_SP;
       df_put(Ni, vi);
@@ -341,7 +301,7 @@ __device__ void df_updateg(double* __restrict__ L, int ld, int i, int j, int k0,
     }
   }
   if (active) {
-    if (CVXG_DF_MFMA_PIPE) df_neg(acc);
+    df_neg(acc);
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -543,7 +503,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       if (tid == 0) __hip_atomic_store(state + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto wait = [&](const int* base, int idx, int want) -> bool {
-      if (tid == 0) s_ok = df_wait_pipe(base, idx, want, abortw, ctrl);
+      if (tid == 0) s_ok = df_wait(base, idx, want, abortw, ctrl);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       __syncthreads();
       return s_ok;
