@@ -258,14 +258,17 @@ __device__ __forceinline__ void p64w_dstep(double (&a)[16], double (&b)[16], dou
 __device__ __forceinline__ bool p64w_eliminate_dpp(Potrf64wSmem& sm, int kb, int base, DevCtrl* ctrl, double& mind,
                                                    int lane, double early_min) {
   const int o = 16 * kb, r = lane & 15, g = lane >> 4;
+  // The row's entries above the diagonal (c > r) are loaded as they are and never masked: they only ever feed other
+  // entries above the diagonal (lane r's multiplier for column j > r is its own a[j], c > j > r), never a pivot, an
+  // entry on or below the diagonal, or a broadcast (lane c's a[j], j < c), and the stores below keep c <= r only.
   double a[16], b[16];
   {
     const double* src = sm.S + (o + r) * P64_SP + o;
 #pragma unroll
     for (int c = 0; c < 16; c += 2) {
       const f64x2 v = *reinterpret_cast<const f64x2*>(src + c);
-      a[c] = (c <= r) ? v[0] : 0.0;
-      a[c + 1] = (c + 1 <= r) ? v[1] : 0.0;
+      a[c] = v[0];
+      a[c + 1] = v[1];
       b[c] = (g == 0 && c == r) ? 1.0 : 0.0;
       b[c + 1] = (g == 0 && c + 1 == r) ? 1.0 : 0.0;
     }
