@@ -237,11 +237,18 @@ __device__ __forceinline__ void p64w_rest(double (&a)[16], double (&b)[16], doub
                                           std::integer_sequence<int, Cs...>) {
   ((p64w_fmac_bc<J + 2 + Cs>(a[J + 2 + Cs], a[J], nta), p64w_fmac_bc<J + 2 + Cs>(b[J + 2 + Cs], a[J], ntb)), ...);
 }
+// (the per-column bookkeeping stays off wave-uniform branches: the minimum pivot is one v_min_f64 per column -- IEEE
+// minNum, as fmin for the quiet values a pivot can take -- and the first bad pivot is found after the sweep from the
+// pivots the lanes keep, by one ballot)
+__device__ __forceinline__ double p64w_vmin(double x, double y) {
+  double r;
+  asm volatile("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
 template <int J>
 __device__ __forceinline__ void p64w_dstep(double (&a)[16], double (&b)[16], double& piv, double& rinv, double& mypiv,
                                            int r, double& pmin, int& firstbad) {
   if constexpr (J < 16) {
-    if (!(piv > 0.0) && firstbad < 0) firstbad = J;
     pmin = fmin(pmin, piv);
     if (r == J) mypiv = piv;
     const double nta = -(a[J] * rinv), ntb = -(b[J] * rinv);
@@ -279,15 +286,21 @@ __device__ __forceinline__ bool p64w_eliminate_dpp(Potrf64wSmem& sm, int kb, int
   double pmin = piv;
   double mypiv = 1.0;
   p64w_dstep<0>(a, b, piv, rinv, mypiv, r, pmin, firstbad);
+  {  // the first column whose pivot is not > 0 (lane r of lane-row 0 holds p_r)
+    const unsigned long long bad = __ballot(!(mypiv > 0.0)) & 0xffffull;
+    if (bad) firstbad = __builtin_ctzll(bad);
+  }
   const double bmin = pmin * rsqrt_nr(pmin);
   mind = fmin(mind, bmin);
   if (lane < 16) {
     sm.SV[kb][r] = rsqrt_nr(mypiv);
     double* dS = sm.S + (o + r) * P64_SP + o;
     double* dE = sm.ET[kb] + r * P64_EP;
+    // (the entries above the diagonal go out as they are: nothing reads the upper part of a diagonal block of S,
+    // and potrf64w_store_L keeps c <= r)
 #pragma unroll
     for (int c = 0; c < 16; c += 2) {
-      *reinterpret_cast<f64x2*>(dS + c) = f64x2{(c <= r) ? a[c] : 0.0, (c + 1 <= r) ? a[c + 1] : 0.0};
+      *reinterpret_cast<f64x2*>(dS + c) = f64x2{a[c], a[c + 1]};
       *reinterpret_cast<f64x2*>(dE + c) = f64x2{b[c], b[c + 1]};
     }
   }
