@@ -98,9 +98,6 @@ __device__ bool df_wait(const int* state, int idx, int want, int* abortw, DevCtr
 // polls are loaded together, so a task whose inputs are already final starts after one memory round trip instead of one
 // per input; only the words still short are polled again.  Same exits as df_wait (the abort word at the first spin
 // that finds an input short, then every 16th).
-#ifndef CVXG_DF_NOBATCH  // (experiment switch) 1: no batch, every L^-1 row-block in its own slice
-#define CVXG_DF_NOBATCH 0
-#endif
 __device__ bool df_wait3(const int* p0, int w0, const int* p1, int w1, const int* p2, int w2, int* abortw, DevCtrl* ctrl) {
   const unsigned long long t0 = spin_clock();
   bool n0 = true, n1 = true, n2 = p2 != nullptr;
@@ -646,7 +643,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         if (tid == 0) s_next = pv;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
-        const int nbat = CVXG_DF_NOBATCH ? 0 : min(s_next, 4);
+        const int nbat = min(s_next, 4);
         {
           f64x2 vb[8];
 #pragma unroll
