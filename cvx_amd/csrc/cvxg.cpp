@@ -393,7 +393,7 @@ struct SchedTimes {  // estimated task times of the list scheduler (us)
 };
 static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles, int near = 0,
                                                  double boost = 0.0, int band = 0, bool eager = true,
-                                                 bool own_b2 = false, bool group8 = false,
+                                                 bool own_b2 = false, int group8 = 0,
                                                  SchedTimes st = SchedTimes()) {
   struct Task {
     int type, i, j, k, cnt;
@@ -432,7 +432,7 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
         const bool band = i - j < near;  // near-diagonal tiles: single updates (each panel as soon as it is done)
         // the group covering panel k: aligned eight, else aligned four, else single
         int gs = k, cnt = 1;
-        if (group8 && !band && (k & ~7) + 8 <= j - singles) {
+        if (j < group8 && !band && (k & ~7) + 8 <= j - singles) {  // (group8: tiles of block columns j < group8)
           gs = k & ~7;
           cnt = 8;
         } else if (group && !band && (k & ~3) + 4 <= j - singles) {
@@ -550,7 +550,9 @@ static std::vector<unsigned> chol_schedule(int nblk, int workers, bool own_b2) {
   if (const char* e = getenv("CVXG_DF_SCHED"))  // (experiments) "potrf:trsm:upd:upd4:boost:band:singles" (all seven)
     sscanf(e, "%lf:%lf:%lf:%lf:%lf:%d:%d", &st.potrf, &st.trsm, &st.upd, &st.upd4, &boost, &band, &singles);
   singles = std::max(singles, 2);  // the chain's own panel b-2 tasks must stay single-panel
-  return build_chol_schedule(nblk, workers, 1, singles, 0, boost, band, true, own_b2, g8 && atoi(g8) != 0, st);
+  // CVXG_DF_GROUP8: 1 = eight-panel groups on every tile, n > 1 = on the tiles of block columns j < n only
+  const int g8v = g8 ? atoi(g8) : 0;
+  return build_chol_schedule(nblk, workers, 1, singles, 0, boost, band, true, own_b2, g8v == 1 ? nblk : g8v, st);
 }
 
 extern "C" int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* relaunches) {
