@@ -25,10 +25,6 @@
 
 namespace cvxg {
 
-#ifndef P64W_DIRECT3  // (experiment switch) the last L^-1 row-block stored by the waves that compute it
-#define P64W_DIRECT3 0
-#endif
-
 #ifndef PUBLISH_ONLY
 #define PUBLISH_ONLY (reinterpret_cast<int*>(1))  // lflag: store the L^-1 row-blocks progressively, raise no flag
 #endif
@@ -421,20 +417,6 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       p64w_phaseA(sm, kb, w, lane, to);
       P64_STAMP(2 + 4 * kb);
-      // the last row-block (the chain's hop) goes out from each wave as soon as its blocks are in LDS -- w1 X_3,0,
-      // w2 X_3,1, w3 X_3,2 and X_3,3 -- drained before the wave counts itself, so the flag follows the count at once
-      const bool direct = P64W_DIRECT3 && kb == 3 && lflag && lflag != PUBLISH_ONLY;
-      if (direct) {
-        const int c0 = 16 * (w - 1), half = (w == 3) ? 16 : 8;  // columns c0.., half f64x2 per row
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (q < half / 4) {
-            const int e = lane + 64 * q, rr = 48 + e / half, cc = c0 + 2 * (e % half);
-            mI.st2(rr * NB + cc, *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc));
-          }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_add(&sm.cntT[kb]);
       if (lflag && w == 3) {  // row-block kb of L^-1 is final once every wave's phase A is
@@ -443,12 +425,10 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
           break;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (!direct) {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int e = lane + 64 * q, rr = 16 * kb + (e >> 5), cc = 2 * (e & 31);
-            mI.st2(rr * NB + cc, *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc));
-          }
+        for (int q = 0; q < 8; ++q) {
+          const int e = lane + 64 * q, rr = 16 * kb + (e >> 5), cc = 2 * (e & 31);
+          mI.st2(rr * NB + cc, *reinterpret_cast<const f64x2*>(sm.X + rr * P64_SP + cc));
         }
         if (lflag != PUBLISH_ONLY) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
