@@ -114,7 +114,12 @@ SIGNATURES = {
     "cvxg_get_counters": (C.c_int, [_P, C.POINTER(C.c_longlong), C.c_int]),
     "cvxg_chol_schedule": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_uint), C.c_int]),
     "cvxg_set_ruiz_lookahead": (C.c_int, [_P, C.c_int, C.POINTER(C.c_longlong)]),
+    "cvxg_set_option": (C.c_int, [_P, C.c_int, C.c_longlong]),
 }
+
+# cvxg_set_option's options (include/cvxg.h)
+OPTIONS = {"sparse_rows": 1, "early_abort": 2, "h_lower": 3, "kkt_fused_rhs": 4, "spec_reg": 5, "ruiz_loop": 6,
+           "ruiz_wg": 7}
 
 
 def load(path: str = LIB_PATH) -> C.CDLL:

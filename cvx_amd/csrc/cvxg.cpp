@@ -75,7 +75,7 @@ struct cvxg_ctx {
   double *eqd = nullptr, *eqtmp = nullptr;  // b - Aeq x
   // KKT equality block (k_kkt.hip): X = Q^-1 [B' | Dq] in kY (np x kY_ld, row-major; the fused forward solve's rhs
   // and the backward solve's sol buffers instead when p + 1 <= kkt_fused_rhs), R = B X partials, S / z, w
-  int kkt_fused_rhs = MAX_RHS;  // set at creation; CVXG_KKT_FUSED_RHS overrides (1: the many-column solves)
+  int kkt_fused_rhs = MAX_RHS;  // set at creation; CVXG_OPT_KKT_FUSED_RHS overrides (1: the many-column solves)
   double *kY = nullptr, *kYg = nullptr, *kgram = nullptr, *kS = nullptr, *kzp = nullptr;
   int kY_ld = 0, kY_chunks = 0, fm_gen = 0;
   // p > 64: S factored by the dataflow Cholesky on its own buffers (pS = p rounded up to 64), w by its backward solve
@@ -107,24 +107,19 @@ struct cvxg_ctx {
   int slots = 512;     // SYRK workgroup slots (2 per CU)
   // Sparse constraint rows (<= SPARSE_NNZ nonzeros: bounds, phase-I bound rows, box rows).  Their Hessian
   // terms are per-entry sums (k_sparse_hess); only the dense rows, packed into As, go through the SYRK.
-  int sparse_rows = 1;          // CVXG_SPARSE_ROWS=0 disables the split (A/B)
-  int early_abort = 1;          // regularizedCholesky's first attempt stops at min diag(L) <= 1e-7 (CVXG_EARLY_ABORT=0: off)
+  int sparse_rows = 1;          // CVXG_OPT_SPARSE_ROWS 0 disables the split (A/B)
+  int early_abort = 1;          // regularizedCholesky's first attempt stops at min diag(L) <= 1e-7 (CVXG_OPT_EARLY_ABORT)
   // The Newton-step assembly with p == 0 stores H's lower triangle (and its diagonal tiles whole) only: Ruiz, the
   // Cholesky and the residual (a lower-triangle symv) read nothing else; consumers of the full matrix (eigen fallback,
-  // KKT paths, cvxg_barrier_eval, the primal-dual solver) mirror it first (ensure_h_full).  CVXG_H_LOWER=0: always mirror
+  // KKT paths, cvxg_barrier_eval, the primal-dual solver) mirror it first (ensure_h_full).  CVXG_OPT_H_LOWER 0: mirror
   int h_lower = 1;
-  bool chain_b2 = true;         // the chain workgroups apply panel b-2 to block row b (CVXG_CHAIN_B2=0: the workers)
-  bool chain_defer = true;      // L_b,b-1 stored / published inside POTRF(b) (CVXG_CHAIN_DEFER=0: before it)
-  double* ltag = nullptr;       // CVXG_CHAIN_TAG=1: L_kk^-1 row-blocks also as data-tagged granules for the chain
-  unsigned long long tag_gen = 0;
-  bool chain_dpp = true;        // POTRF's column sweep with DPP broadcasts (CVXG_CHAIN_DPP=0: v_readlane)
   bool h_full = true;           // the current H holds its upper triangle too
   double* hsv_part = nullptr;   // symv partials (nblk x np)
-  // Ruiz: every sweep in one persistent launch (k_ruiz.hip; CVXG_RUIZ_LOOP=0: two launches per sweep)
+  // Ruiz: every sweep in one persistent launch (k_ruiz.hip; CVXG_OPT_RUIZ_LOOP; 0: two launches per sweep)
   int ruiz_loop = 0;            // (opt-in until it beats the multi-launch form: DESIGN.md §7)
   unsigned long long* ruiz_trace = nullptr;  // CVXG_RUIZ_TRACE=<file>: per-workgroup sweep stamps of the last loop
   std::string ruiz_trace_path;
-  int ruiz_wg = 0;              // its workgroups (0: one per CU; CVXG_RUIZ_WG, tests: fewer -> streamed tiles)
+  int ruiz_wg = 0;              // its workgroups (0: one per CU; CVXG_OPT_RUIZ_WG, tests: fewer -> streamed tiles)
   double* ruiz_S = nullptr;     // its data-tagged granules (ruiz_loop_doubles)
   unsigned long long ruiz_gen = 0;  // its launch generation (the granules' tags)
   int* ruiz_work = nullptr;     // its counters and flags (ruiz_loop_work_ints)
@@ -195,7 +190,7 @@ struct cvxg_ctx {
   hipStream_t s2 = nullptr;
   hipEvent_t ev_w = nullptr, ev_h = nullptr;
   // speculative regularized pair (regularized_cholesky_spec): after a regularized Newton direction the next one runs
-  // chol(Q) and chol(Q + 1e-10 I) side by side, each on half of the CUs (CVXG_SPEC_REG=0: one after the other)
+  // chol(Q) and chol(Q + 1e-10 I) side by side, each on half of the CUs (CVXG_OPT_SPEC_REG 0: one after the other)
   int spec_reg = 1;
   int prev_reg = 0;
   bool pair_active = false;
@@ -382,18 +377,15 @@ static std::vector<int> syrk_tile_plan(int nt, int slots, int* nmain) {
 // back by its group.  The critical chain tasks POTRF(k), TRSM(k+1,k), UPDATE(k+1,k+1,k) are simulated but
 // not emitted (workgroup 0 runs them in sequence); every transitive dependency of a chain task still precedes
 // that task's dependents in the emitted order, which keeps the launch deadlock-free.
-// the main factorization's chain workgroups apply panel b-2 to block row b themselves (k_dataflow.hip, own_b2)
-constexpr bool CHAIN_OWN_B2_DEFAULT = true;
 struct SchedTimes {  // estimated task times of the list scheduler (us)
   // round 5, after the worker fix: the measured medians (TRSM 5.7, UPDATE 4.1, UPDATE4 12.3 us) and a simulated chain
   // period potrf + trsm + 0.75 upd = 14 us.  Same-box A/Bs (profiles/r05/ab_sched, ab_sched2): the former 10 / 6 /
   // 5.5 / 16 1.083 ms, 7 / 5 / 4 / 12.5 1.064 ms, 6 / 5 / 4 / 12.5 1.048 ms; the order is sensitive to the ratio of the
   // simulated chain period to UPDATE4 (1.36: 1.094 ms, 1.04: 1.085 ms)
-  double potrf = 6.0, trsm = 5.0, upd = 4.0, upd4 = 12.5, upd8 = 24.0;
+  double potrf = 6.0, trsm = 5.0, upd = 4.0, upd4 = 12.5;
 };
 static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group, int singles, int near = 0,
                                                  double boost = 0.0, int band = 0, bool eager = true,
-                                                 bool own_b2 = false, int group8 = 0,
                                                  SchedTimes st = SchedTimes()) {
   struct Task {
     int type, i, j, k, cnt;
@@ -418,8 +410,7 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   // (measured ~22 us per block), UPDATE4 for its measured ~14 us plus the contention of a full chip.  With the
   // former 18 / 10 the simulated chain ran slower and the workers faster than on the device, so the emitted order
   // put TRSM(k+2, k) -- which the chain needs next -- behind trailing updates: 1.77 -> 1.57 ms per factorization.
-  // (group8: UPDATE8, eight panels per read-modify-write where a whole aligned group of eight fits before the singles)
-  const double d_potrf = st.potrf, d_trsm = st.trsm, d_upd = st.upd, d_upd4 = st.upd4, d_upd8 = st.upd8;
+  const double d_potrf = st.potrf, d_trsm = st.trsm, d_upd = st.upd, d_upd4 = st.upd4;
   for (int k = 0; k < nb; ++k) {  // (k, type) order is a topological order
     potrf_id[k] = (int)T.size();
     T.push_back({0, k, k, k, 1, d_potrf, 0, 0, k > 0 ? 1 : 0});
@@ -430,12 +421,9 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
     for (int j = k + 1; j < nb; ++j)
       for (int i = j; i < nb; ++i) {
         const bool band = i - j < near;  // near-diagonal tiles: single updates (each panel as soon as it is done)
-        // the group covering panel k: aligned eight, else aligned four, else single
+        // the group covering panel k: aligned four, else single
         int gs = k, cnt = 1;
-        if (j < group8 && !band && (k & ~7) + 8 <= j - singles) {  // (group8: tiles of block columns j < group8)
-          gs = k & ~7;
-          cnt = 8;
-        } else if (group && !band && (k & ~3) + 4 <= j - singles) {
+        if (group && !band && (k & ~3) + 4 <= j - singles) {
           gs = k & ~3;
           cnt = 4;
         }
@@ -443,8 +431,7 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
         const int id = (int)T.size();
         for (int kk = k; kk < k + cnt; ++kk) upd_id[upd_base[tri(i, j)] + kk] = id;
         const int npanel = (i == j) ? cnt : 2 * cnt;
-        T.push_back({cnt == 8 ? 4 : cnt == 4 ? 3 : 2, i, j, k, cnt,
-                     (cnt == 8 ? d_upd8 : cnt == 4 ? d_upd4 : d_upd) * (i == j ? 0.75 : 1.0), 0, 0,
+        T.push_back({cnt == 4 ? 3 : 2, i, j, k, cnt, (cnt == 4 ? d_upd4 : d_upd) * (i == j ? 0.75 : 1.0), 0, 0,
                      npanel + (k > 0 ? 1 : 0)});
       }
   }
@@ -483,14 +470,14 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
   pending.push({0.0, potrf_id[0]});
   std::vector<unsigned> order;
   order.reserve(T.size());
-  auto code = [](const Task& x) {  // task word: type 1 TRSM, 2 UPDATE, 3 UPDATE4, 0 UPDATE8 (POTRF is never listed)
+  auto code = [](const Task& x) {  // task word: type 1 TRSM, 2 UPDATE, 3 UPDATE4 (POTRF is never listed)
     return ((unsigned)(x.type & 3) << 30) | ((unsigned)x.k << 20) | ((unsigned)x.i << 10) | (unsigned)x.j;
   };
-  // own_b2: the chain workgroups also apply panel b-2 to block row b (UPDATE(k+2,k+2,k), UPDATE(k+2,k+1,k); always
+  // the chain workgroups also apply panel b-2 to block row b (UPDATE(k+2,k+2,k), UPDATE(k+2,k+1,k); always
   // single-panel tasks: the groups of four end two panels before the diagonal)
-  auto is_chain = [own_b2](const Task& x) {
+  auto is_chain = [](const Task& x) {
     return x.type == 0 || (x.type == 1 && x.i == x.k + 1) || (x.type == 2 && x.i == x.j && x.j == x.k + 1) ||
-           (own_b2 && x.type == 2 && x.i == x.k + 2 && (x.j == x.i || x.j == x.i - 1));
+           (x.type == 2 && x.i == x.k + 2 && (x.j == x.i || x.j == x.i - 1));
   };
   // the worker tasks the chain's staging of block k+2 waits on -- TRSM(k+2,k), UPDATE(k+2,k+1,k), UPDATE(k+2,k+2,k)
   // -- are emitted as soon as their last dependency is (not at their simulated start), so a worker claims them early
@@ -542,17 +529,10 @@ static std::vector<unsigned> build_chol_schedule(int nb, int workers, int group,
 // The production schedule: four-panel update groups (the last two panels of a tile single) and a priority boost
 // of 100 us for the near-diagonal updates and next-row TRSMs the chain waits on (band 3).  A/B at C3 (boost 0 /
 // band 2 -> 100 / 3): Cholesky 1.553, 1.552, 1.556 -> 1.498, 1.529, 1.502 ms.
-static std::vector<unsigned> chol_schedule(int nblk, int workers, bool own_b2) {
-  const char* g8 = getenv("CVXG_DF_GROUP8");  // eight-panel update groups (UPDATE8)
-  SchedTimes st;
-  double boost = 100.0;
-  int band = 3, singles = 2;
-  if (const char* e = getenv("CVXG_DF_SCHED"))  // (experiments) "potrf:trsm:upd:upd4:boost:band:singles" (all seven)
-    sscanf(e, "%lf:%lf:%lf:%lf:%lf:%d:%d", &st.potrf, &st.trsm, &st.upd, &st.upd4, &boost, &band, &singles);
-  singles = std::max(singles, 2);  // the chain's own panel b-2 tasks must stay single-panel
-  // CVXG_DF_GROUP8: 1 = eight-panel groups on every tile, n > 1 = on the tiles of block columns j < n only
-  const int g8v = g8 ? atoi(g8) : 0;
-  return build_chol_schedule(nblk, workers, 1, singles, 0, boost, band, true, own_b2, g8v == 1 ? nblk : g8v, st);
+// (singles >= 2: the chain's own panel b-2 tasks must stay single-panel.  Eight-panel groups and other estimates were
+// measured in round 5 and not kept: DESIGN.md §7.)
+static std::vector<unsigned> chol_schedule(int nblk, int workers) {
+  return build_chol_schedule(nblk, workers, 1, 2, 0, 100.0, 3, true, SchedTimes());
 }
 
 extern "C" int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* relaunches) {
@@ -562,9 +542,63 @@ extern "C" int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* rel
   return CVXG_OK;
 }
 
+// The one-launch Ruiz loop's buffers (and, with CVXG_RUIZ_TRACE, its stamp buffer for every CU), on first use.
+static int ruiz_loop_alloc(cvxg_ctx* ctx) {
+  if (!ctx->ruiz_S) {
+    CHK(dalloc(ctx, &ctx->ruiz_S, ruiz_loop_doubles(ctx->nblk)));
+    CHK(dalloc(ctx, &ctx->ruiz_work, ruiz_loop_work_ints(ctx->nblk)));
+  }
+  if (!ctx->ruiz_trace_path.empty() && !ctx->ruiz_trace)
+    CHK(dalloc(ctx, &ctx->ruiz_trace, (size_t)std::max(ctx->ncu, 1) * RUIZ_MAX * 4));
+  return CVXG_OK;
+}
+
+extern "C" int cvxg_set_option(cvxg_ctx* ctx, int option, long long value) {
+  if (!ctx) return CVXG_E_ARG;
+  const bool bin = value == 0 || value == 1;
+  switch (option) {
+    case CVXG_OPT_SPARSE_ROWS:
+      if (!bin) break;
+      if (ctx->have_ineq) return set_err(ctx, CVXG_E_ARG, "CVXG_OPT_SPARSE_ROWS must be set before cvxg_set_ineq");
+      ctx->sparse_rows = (int)value;
+      return CVXG_OK;
+    case CVXG_OPT_EARLY_ABORT:
+      if (!bin) break;
+      ctx->early_abort = (int)value;
+      return CVXG_OK;
+    case CVXG_OPT_H_LOWER:
+      if (!bin) break;
+      ctx->h_lower = (int)value;
+      ctx->h_valid = false;  // (a prefetched assembly in the other form is not reused)
+      return CVXG_OK;
+    case CVXG_OPT_KKT_FUSED_RHS:
+      if (value < 1 || value > MAX_RHS) break;
+      ctx->kkt_fused_rhs = (int)value;
+      return CVXG_OK;
+    case CVXG_OPT_SPEC_REG:
+      if (!bin) break;
+      ctx->spec_reg = (int)value;
+      return CVXG_OK;
+    case CVXG_OPT_RUIZ_LOOP:
+      if (!bin) break;
+      if (value && !ruiz_loop_fits(ctx->nblk))
+        return set_err(ctx, CVXG_E_UNSUPPORTED, "the one-launch Ruiz loop holds at most its register batch of tiles");
+      if (value) CHK(ruiz_loop_alloc(ctx));
+      ctx->ruiz_loop = (int)value;
+      return CVXG_OK;
+    case CVXG_OPT_RUIZ_WG:
+      if (value < 0 || value > ctx->ncu) break;
+      ctx->ruiz_wg = (int)value;
+      return CVXG_OK;
+    default:
+      return set_err(ctx, CVXG_E_ARG, "cvxg_set_option: unknown option %d", option);
+  }
+  return set_err(ctx, CVXG_E_ARG, "cvxg_set_option: value %lld out of range for option %d", value, option);
+}
+
 extern "C" int cvxg_chol_schedule(int nblk, int workers, unsigned* order, int cap) {
   if (nblk < 1 || nblk > 1023 || workers < 1 || cap < 0 || (cap > 0 && !order)) return CVXG_E_ARG;
-  const std::vector<unsigned> o = chol_schedule(nblk, workers, CHAIN_OWN_B2_DEFAULT);
+  const std::vector<unsigned> o = chol_schedule(nblk, workers);
   for (size_t t = 0; t < o.size() && (int)t < cap; ++t) order[t] = o[t];
   return (int)o.size();
 }
@@ -848,6 +882,17 @@ static void ruiz_learn(cvxg_ctx* ctx, int sweeps) {
   ctx->ruiz_launch = std::max(1, std::min(RUIZ_MAX, sweeps + RUIZ_MARGIN));
 }
 
+// The device-side failures an attempt's host read can carry (both forms of regularizedCholesky check them): a timed-out
+// dependency wait of the dataflow Cholesky, or of the one-launch Ruiz loop it is gated on (ruiz_sweeps == -2; the
+// factorization and the backward solve then left at once, so dx is stale).
+static int attempt_status(cvxg_ctx* ctx) {
+  if (ctx->hctrl->df_status != 0)
+    return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
+  if (ctx->hctrl->ruiz_sweeps == -2)
+    return set_err(ctx, CVXG_E_HIP, "Ruiz loop: dependency wait timed out (abort word 0x%x)", ctx->hctrl->ruiz_abort);
+  return CVXG_OK;
+}
+
 // One factorisation attempt of Q = DHD (+reg I) with the fused forward solve of nrhs right-hand sides,
 // which `fill_rhs` writes into ctx->rhs first.  `after` enqueues the work that consumes the factor (the back
 // substitution) before the one host read of the attempt, which returns chol_info / min_diag via hctrl; a caller
@@ -866,8 +911,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
     (void)hipMemsetAsync(ctx->df_trace, 0, (size_t)4 * (ctx->df_ntasks + 5 * ctx->nblk) * 8, s);
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
                        ctx->df_ntasks, ctx->ncu, ctx->df_trace, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending,
-                       (reg == 0.0 && ctx->early_abort) ? 1e-7 : 0.0, ctx->chain_b2, ctx->chain_defer, ctx->ltag,
-                       ctx->ltag ? ++ctx->tag_gen : 0, ctx->chain_dpp);
+                       (reg == 0.0 && ctx->early_abort) ? 1e-7 : 0.0);
   ctx->spec_launched = false;
   after();
   HIPC(ctx, hipGetLastError());
@@ -890,10 +934,7 @@ static int factor_attempt(cvxg_ctx* ctx, double reg, int nrhs, F fill_rhs, G aft
   ctx->spec_eval_have = ctx->spec_launched && ctx->spec_eval_launched;
   ctx->spec_launched = false;
   ctx->spec_eval_launched = false;
-  if (ctx->hctrl->df_status != 0)
-    return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
-  if (ctx->hctrl->ruiz_sweeps == -2)
-    return set_err(ctx, CVXG_E_HIP, "Ruiz loop: dependency wait timed out (abort word 0x%x)", ctx->hctrl->ruiz_abort);
+  CHK(attempt_status(ctx));
   if (ctx->df_trace) {  // instrumentation only: task order + timeline of this factorization
     std::vector<unsigned long long> tr((size_t)4 * (ctx->df_ntasks + 5 * ctx->nblk));
     std::vector<unsigned> ord(ctx->df_ntasks);
@@ -943,19 +984,46 @@ static void backward_solve(cvxg_ctx* ctx, int nrhs, BwdEpilogue epi = {}) {
                       ++ctx->bwd_gen, ctx->ctrl, epi, alt);
 }
 
-// The buffers of the speculative pair's second attempt (allocated on first use: 134 MB of L at C3).
+// The buffers of the speculative pair's second attempt (allocated on first use: 134 MB of L at C3).  All or nothing:
+// ctx->L2 is set only once every piece exists, and a failure frees what was made (the caller then runs the sequential
+// form, which needs none of it).
+static void spec_free(double* L2, double* Linv2, double* rhs2, int* w2, DevCtrl* c2, hipStream_t s3, hipEvent_t e0,
+                      hipEvent_t e1) {
+  for (void* p : {(void*)L2, (void*)Linv2, (void*)rhs2, (void*)w2, (void*)c2})
+    if (p) (void)hipFree(p);
+  if (s3) (void)hipStreamDestroy(s3);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+}
 static int spec_alloc(cvxg_ctx* ctx) {
   if (ctx->L2) return CVXG_OK;
   const size_t np = ctx->np;
-  CHK(dalloc(ctx, &ctx->L2, np * np));
-  CHK(dalloc(ctx, &ctx->Linv2, (size_t)ctx->nblk * NB * NB));
-  CHK(dalloc(ctx, &ctx->rhs2, np * MAX_RHS));
-  CHK(dalloc(ctx, &ctx->df_work2, chol_dataflow_work_ints(ctx->nblk)));
-  HIPC(ctx, hipMalloc((void**)&ctx->ctrl2, sizeof(DevCtrl)));
-  HIPC(ctx, hipMemset(ctx->ctrl2, 0, sizeof(DevCtrl)));
-  HIPC(ctx, hipStreamCreateWithFlags(&ctx->s3, hipStreamNonBlocking));
-  HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_p0, hipEventDisableTiming));
-  HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_p1, hipEventDisableTiming));
+  double *L2 = nullptr, *Linv2 = nullptr, *rhs2 = nullptr;
+  int* w2 = nullptr;
+  DevCtrl* c2 = nullptr;
+  hipStream_t s3 = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = dalloc(ctx, &L2, np * np);
+  if (rc == CVXG_OK) rc = dalloc(ctx, &Linv2, (size_t)ctx->nblk * NB * NB);
+  if (rc == CVXG_OK) rc = dalloc(ctx, &rhs2, np * MAX_RHS);
+  if (rc == CVXG_OK) rc = dalloc(ctx, &w2, chol_dataflow_work_ints(ctx->nblk));
+  if (rc == CVXG_OK) rc = dalloc(ctx, &c2, 1);
+  if (rc == CVXG_OK && hipStreamCreateWithFlags(&s3, hipStreamNonBlocking) != hipSuccess) rc = CVXG_E_HIP;
+  if (rc == CVXG_OK && hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess) rc = CVXG_E_HIP;
+  if (rc == CVXG_OK && hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess) rc = CVXG_E_HIP;
+  if (rc != CVXG_OK) {
+    spec_free(L2, Linv2, rhs2, w2, c2, s3, e0, e1);
+    (void)hipGetLastError();  // (an allocation failure is not a sticky error for the sequential form)
+    return rc;
+  }
+  ctx->Linv2 = Linv2;
+  ctx->rhs2 = rhs2;
+  ctx->df_work2 = w2;
+  ctx->ctrl2 = c2;
+  ctx->s3 = s3;
+  ctx->ev_p0 = e0;
+  ctx->ev_p1 = e1;
+  ctx->L2 = L2;  // last: the pair's buffers are complete
   return CVXG_OK;
 }
 
@@ -982,10 +1050,10 @@ static int regularized_cholesky_spec(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* r
   const int half = std::max(3, ctx->ncu / 2);
   launch_chol_dataflow(s, ctx->L, ctx->np, ctx->rhs, nrhs, ctx->Linv, ctx->ctrl, ctx->df_work, ctx->nblk, ctx->df_tasks,
                        ctx->df_ntasks, half, nullptr, false, ctx->H, ctx->dfin, ctx->n, ctx->ruiz_pending,
-                       ctx->early_abort ? 1e-7 : 0.0, ctx->chain_b2, ctx->chain_defer, nullptr, 0, ctx->chain_dpp);
+                       ctx->early_abort ? 1e-7 : 0.0);
   launch_chol_dataflow(ctx->s3, ctx->L2, ctx->np, ctx->rhs2, nrhs, ctx->Linv2, ctx->ctrl2, ctx->df_work2, ctx->nblk,
                        ctx->df_tasks, ctx->df_ntasks, half, nullptr, false, ctx->H, ctx->dfin, ctx->n,
-                       ctx->ruiz_pending, 0.0, ctx->chain_b2, ctx->chain_defer, nullptr, 0, ctx->chain_dpp);
+                       ctx->ruiz_pending, 0.0);
   HIPC(ctx, hipEventRecord(ctx->ev_p1, ctx->s3));
   HIPC(ctx, hipStreamWaitEvent(s, ctx->ev_p1, 0));
   launch_spec_select(s, ctx->ctrl, ctx->ctrl2);
@@ -1012,8 +1080,7 @@ static int regularized_cholesky_spec(cvxg_ctx* ctx, int nrhs, F fill_rhs, int* r
   ctx->spec_eval_have = ctx->spec_launched && ctx->spec_eval_launched;
   ctx->spec_launched = false;
   ctx->spec_eval_launched = false;
-  if (ctx->hctrl->df_status != 0)
-    return set_err(ctx, CVXG_E_HIP, "dataflow Cholesky: dependency wait timed out (status %d)", ctx->hctrl->df_status);
+  CHK(attempt_status(ctx));
   if (!ctx->hctrl->spec_sel) {
     *regularized = 0;
     ctx->small_piv = 0;
@@ -1078,6 +1145,8 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
     }
   };
   auto fill = [&]() { launch_scaled_col(s, ctx->dfin, ctx->y, -1.0, ctx->n, ctx->np, 1, 0, ctx->rhs); };
+  // the speculative pair needs 134 MB more at C3 (allocated on first use); without it the sequential form runs
+  if (ctx->spec_reg && ctx->prev_reg && !ctx->df_trace && spec_alloc(ctx) != CVXG_OK) ctx->spec_reg = 0;
   int rc = (ctx->spec_reg && ctx->prev_reg && !ctx->df_trace)
                ? regularized_cholesky_spec(ctx, 1, fill, &reg, &mind, solve_and_residual)
                : regularized_cholesky(ctx, 1, fill, &reg, &mind, solve_and_residual);
@@ -1254,7 +1323,7 @@ static int kkt_alloc(cvxg_ctx* ctx, bool fused) {
       CHK(dalloc(ctx, &ctx->sLinv, (size_t)ctx->s_nblk * NB * NB));
       CHK(dalloc(ctx, &ctx->kzp, (size_t)ps));
       CHK(dalloc(ctx, &ctx->sw, (size_t)ps));
-      std::vector<unsigned> order = chol_schedule(ctx->s_nblk, ctx->ncu, false);
+      std::vector<unsigned> order = chol_schedule(ctx->s_nblk, ctx->ncu);
       ctx->s_ntasks = (int)order.size();
       CHK(dalloc(ctx, &ctx->s_tasks, std::max<size_t>(order.size(), 1)));
       if (!order.empty())
@@ -1801,22 +1870,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   {  // dataflow Cholesky: task order for this tile count, work words
     (void)hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device);
     ctx->ncu = std::max(ctx->ncu, 1);
-    ctx->chain_b2 = CHAIN_OWN_B2_DEFAULT;
-    if (const char* e = getenv("CVXG_CHAIN_B2")) ctx->chain_b2 = atoi(e) != 0;
-    if (const char* e = getenv("CVXG_CHAIN_DEFER")) ctx->chain_defer = atoi(e) != 0;
-    if (const char* e = getenv("CVXG_CHAIN_DPP")) ctx->chain_dpp = atoi(e) != 0;
-    {
-      const bool tag = getenv("CVXG_CHAIN_TAG") && atoi(getenv("CVXG_CHAIN_TAG")) != 0;
-      const int v = (ctx->chain_b2 ? 1 : 0) | (ctx->chain_defer ? 2 : 0) | (tag ? 4 : 0) | (ctx->chain_dpp ? 8 : 0);
-      if (!chol_dataflow_variant_ok(v))
-        return set_err(ctx, CVXG_E_UNSUPPORTED, "CVXG_CHAIN_* variant %d of the dataflow Cholesky is not built", v);
-    }
-    if (const char* e = getenv("CVXG_CHAIN_TAG"))
-      if (atoi(e) != 0) {
-        CHK(dalloc(ctx, &ctx->ltag, (size_t)ctx->nblk * NB * NB * 2));
-        HIPC(ctx, hipMemset(ctx->ltag, 0, (size_t)ctx->nblk * NB * NB * 16));
-      }
-    std::vector<unsigned> order = chol_schedule(ctx->nblk, ctx->ncu, ctx->chain_b2);
+    std::vector<unsigned> order = chol_schedule(ctx->nblk, ctx->ncu);
     ctx->df_ntasks = (int)order.size();
     CHK(dalloc(ctx, &ctx->df_tasks, order.size()));
     CHK(copy_sync(ctx, ctx->df_tasks, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
@@ -1836,13 +1890,9 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
   const int slots = 2 * std::max(ncu, 1);
   ctx->slots = slots;
-  if (const char* e = getenv("CVXG_SPARSE_ROWS")) ctx->sparse_rows = atoi(e) != 0;
-  if (const char* e = getenv("CVXG_EARLY_ABORT")) ctx->early_abort = atoi(e) != 0;
-  if (const char* e = getenv("CVXG_H_LOWER")) ctx->h_lower = atoi(e) != 0;
   // the fused forward solve carries the KKT columns only on small problems: at C3 (64 blocks) the many-column solves
   // cost less than the 9-column chain (C3EQ8: 204.5 vs 191.5 solves/s)
   ctx->kkt_fused_rhs = ctx->nblk < 8 ? MAX_RHS : 1;
-  if (const char* e = getenv("CVXG_KKT_FUSED_RHS")) ctx->kkt_fused_rhs = std::max(1, atoi(e));
   const int kchunks = (int)(mp / KC);
   std::vector<int> tl = syrk_tile_plan(nt, slots, &ctx->ntiles_main);
   ctx->ntiles = (int)tl.size();
@@ -1854,24 +1904,10 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     part = std::max(part, (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE);
   CHK(dalloc(ctx, &ctx->part, part));
   CHK(dalloc(ctx, &ctx->hsv_part, (size_t)ctx->nblk * np));
-  if (const char* e = getenv("CVXG_RUIZ_LOOP")) ctx->ruiz_loop = atoi(e) != 0;
-  if (const char* e = getenv("CVXG_RUIZ_WG")) ctx->ruiz_wg = std::max(0, atoi(e));
-  if (const char* e = getenv("CVXG_RUIZ_TRACE")) {
-    ctx->ruiz_trace_path = e;
-    const int nwg = ctx->ruiz_wg > 0 ? ctx->ruiz_wg : std::max(ctx->ncu, 1);
-    CHK(dalloc(ctx, &ctx->ruiz_trace, (size_t)nwg * RUIZ_MAX * 4));
-    HIPC(ctx, hipMemset(ctx->ruiz_trace, 0, (size_t)nwg * RUIZ_MAX * 4 * 8));
-  }
-  if (!ruiz_loop_fits((n + NB - 1) / NB)) ctx->ruiz_loop = 0;
-  if (ctx->ruiz_loop) {
-    CHK(dalloc(ctx, &ctx->ruiz_S, ruiz_loop_doubles(ctx->nblk)));
-    HIPC(ctx, hipMemset(ctx->ruiz_S, 0, ruiz_loop_doubles(ctx->nblk) * sizeof(double)));
-    CHK(dalloc(ctx, &ctx->ruiz_work, ruiz_loop_work_ints(ctx->nblk)));
-  }
+  if (const char* e = getenv("CVXG_RUIZ_TRACE")) ctx->ruiz_trace_path = e;  // instrumentation only (the loop's stamps)
   CHK(dalloc(ctx, &ctx->spart,
              ctx->nsplit > 1 ? (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE : (size_t)1));
   HIPC(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
-  if (const char* e = getenv("CVXG_SPEC_REG")) ctx->spec_reg = atoi(e) != 0;
   HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_w, hipEventDisableTiming));
   HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_h, hipEventDisableTiming));
   const int lsb = ls_blocks(std::max(m, 1));
@@ -1905,7 +1941,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
   void* ptrs[] = {ctx->P, ctx->a0, ctx->A, ctx->r, ctx->ub, ctx->Aeq, ctx->beq, ctx->x, ctx->y, ctx->dx, ctx->sdir,
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
-                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->ruiz_S, ctx->ltag, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
+                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->ruiz_S, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
                   ctx->ls_log, ctx->ls_pcnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,

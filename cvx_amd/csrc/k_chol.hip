@@ -27,8 +27,8 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
     L = alt.L;
     Linv = alt.Linv;
     rhs = alt.rhs;
-  } else if (ctrl->chol_info != 0) {
-    return;  // a failed attempt
+  } else if (ctrl->chol_info != 0 || ctrl->small_piv != 0) {
+    return;  // a failed attempt, or a first attempt stopped early (its factor is discarded: the retry's solve follows)
   }
   __shared__ double u[MAX_RHS][NB];
   __shared__ double part[4][MAX_RHS][NB];

@@ -265,9 +265,9 @@ __device__ void df_update(double* __restrict__ L, int ld, int i, int j, int k, d
   }
 }
 
-// UPDATE4 / UPDATE8 (G = 4, 8)(i,j,k0): A_ij -= sum_{k=k0}^{k0+G-1} L_ik L_jk^T — one read-modify-write of the tile
-// for G panels, with the operand tiles of panel k+1 loaded into registers while the MFMAs of panel k run (two LDS
-// buffers).  The accumulator is the FP64 tile itself, so G panels in one task are the same bits as in G / 4 tasks.
+// UPDATE4 (G = 4)(i,j,k0): A_ij -= sum_{k=k0}^{k0+G-1} L_ik L_jk^T — one read-modify-write of the tile for G panels,
+// with the operand tiles of panel k+1 loaded into registers while the MFMAs of panel k run (two LDS buffers).  The
+// accumulator is the FP64 tile itself, so G panels in one task are the same bits as G single-panel tasks.
 template <int G>
 __device__ void df_updateg(double* __restrict__ L, int ld, int i, int j, int k0, double* smem, const QFold& qf) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -451,18 +451,16 @@ __device__ __forceinline__ void ch_update(d4f (&dacc)[3], const double* Lp, int 
                                                        lf[kChJB[W][q] < 0 ? 0 : kChJB[W][q]][st], dacc[q], 0, 0, 0);
 }
 
-// V: compile-time variant bits (each a separate instantiation, so an unused variant costs no registers):
-//   1 the chain applies panel b-2 to block row b, 2 L_b,b-1 stored / published inside POTRF(b), 4 L_kk^-1 row-blocks
-//   handed to the chain as data-tagged granules (ltag), 8 POTRF's column sweep with DPP broadcasts
-template <int V>
+// The chain applies panel b-2 to block row b itself, L_b,b-1 is stored / published inside POTRF(b) by its waves 1..3,
+// and POTRF's column sweep rides its broadcasts in DPP (round 6: the measured-and-rejected variants -- workers applying
+// panel b-2, L_b,b-1 published before POTRF(b), the v_readlane sweep, data-tagged L^-1 row-blocks, eight-panel update
+// groups -- are gone from the product; DESIGN.md §7 keeps their numbers).
 __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L, int ld, double* __restrict__ rhs,
                                                           int nrhs, double* __restrict__ Linv, DevCtrl* ctrl,
                                                           int* __restrict__ work, const unsigned* __restrict__ tasks,
                                                           int ntasks, int nblk, unsigned long long* __restrict__ trace,
                                                           const double* __restrict__ Hq, const double* __restrict__ dq,
-                                                          int nq, int ruiz_gate, double early_min,
-                                                          double* __restrict__ ltag, unsigned long long tag_gen) {
-  constexpr bool kB2 = (V & 1) != 0, kDefer = (V & 2) != 0, kTag = (V & 4) != 0, kDpp = (V & 8) != 0;
+                                                          int nq, int ruiz_gate, double early_min) {
   // the Ruiz loop launched ahead of the factorization without a host read may still be open (k_ruiz_final: -1): then
   // the launch is void and the host finishes the loop and factors again
   if (ruiz_gate && ctrl->ruiz_sweeps < 0) return;
@@ -534,7 +532,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         // batch below
         int pv = 0;
         d4f dacc[NBLK16];
-        if (kB2 && b >= 2) {
+        if (b >= 2) {
           // Panel j = b-2 of block row b on this workgroup (the tasks UPDATE(b,b,j) and UPDATE(b,k,j), not in the
           // worker list), in two waits (below).  The MFMA sequences are the workers' (df_update's K = 0..63 chain), so the factor is
           // bitwise the same; the worker -> state word -> staging hop of both tiles is gone from the chain.
@@ -658,7 +656,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           }
         }
         potrf64w_reset(ps);  // the slices leave POTRF's L^-1 workspace and flags alone: clear them off the chain
-        if (kDefer && tid == 0) cs.lpub = 0;  // (POTRF(b-2)'s pre hook is long done; the barrier below orders it)
+        if (tid == 0) cs.lpub = 0;  // (POTRF(b-2)'s pre hook is long done; the barrier below orders it)
         mark(k, 1, 1);
         // L_b,k, row stride DF_SP: written over A_b,k in Sa (every wave holds its row-block of A in af before the first
         // slice's barrier), where it stays for the rhs correction at the end of POTRF(b) — no copy before POTRF
@@ -673,47 +671,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             const int e = tid + 256 * q;
             er[q] = mI.ld2((16 * cb + (e >> 5)) * NB + 2 * (e & 31));
           }
-        };
-        // ltag: row-block cb polled straight from POTRF(k)'s data-tagged granules (no flag, no drain round trip on
-        // the producer); each thread spins on its own granules until every tag is this launch's.  False: abort.
-        const Sc1Mem mT(ltag ? ltag + (size_t)k * NB * NB * 2 : Linv, (unsigned)(NB * NB * 16));
-        const double tagd = __longlong_as_double((long long)tag_gen);
-        f64x2 tg[2][2];
-        auto tissue = [&](int cb) {
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int e = tid + 256 * q, r = 16 * cb + (e >> 5), c = 2 * (e & 31);
-            if (c < 16 * (cb + 1)) {
-              tg[q][0] = mT.ld2(2 * (r * NB + c));
-              tg[q][1] = mT.ld2(2 * (r * NB + c + 1));
-            } else {
-              tg[q][0] = tg[q][1] = f64x2{0.0, tagd};
-            }
-          }
-        };
-        auto tready = [&]() {
-          bool ok = true;
-#pragma unroll
-          for (int q = 0; q < 2; ++q)
-            ok = ok && __double_as_longlong(tg[q][0][1]) == __double_as_longlong(tagd) &&
-                 __double_as_longlong(tg[q][1][1]) == __double_as_longlong(tagd);
-          return ok;
-        };
-        auto tfinish = [&](int cb) -> bool {  // spin until this thread's granules carry the tag, then er
-          const unsigned long long t0 = spin_clock();
-          for (unsigned spins = 0; !tready(); ++spins) {
-            if ((spins & 15) == 15 && df_poll(abortw)) return false;
-            if (spin_expired(spins, t0)) {
-              __hip_atomic_store(abortw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              atomicExch(&ctrl->df_status, 2);
-              return false;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            tissue(cb);
-          }
-#pragma unroll
-          for (int q = 0; q < 2; ++q) er[q] = f64x2{tg[q][0][0], tg[q][1][0]};
-          return true;
         };
         __syncthreads();  // Sa and the batch's row-blocks in ps.S complete
         mark(k, 4, 0);    // trace: every wave's staging loads landed (record 4: the batch's phases)
@@ -736,7 +693,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               for (int r = 0; r < 4; ++r) {
                 const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
                 Lp[row * DF_SP + col] = acc[cb][r];
-                if (!kDefer) mA.st(row * ld + col, acc[cb][r]);
               }
           __syncthreads();
           for (int cb = 0; cb < nbat; ++cb) {
@@ -749,27 +705,16 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           }
           mark(k, 4, 2);
         }
-        bool tfail = false;
         if (nbat < 4) {
-          if constexpr (kTag) {
-            tissue(nbat);
-            tfail = !tfinish(nbat);
-          } else {
-            if (!wait(cflag, k, nbat + 1)) return;
-            eload(nbat);
-          }
+          if (!wait(cflag, k, nbat + 1)) return;
+          eload(nbat);
         }
         bool have_next = nbat < 4;
 #pragma unroll 1
         for (int cb = nbat; cb < 4; ++cb) {
           double* E = cs.E2[cb & 1];
           if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
-          if constexpr (kTag) {
-            if (cb > nbat) {
-              tissue(cb);
-              tfail = tfail || !tfinish(cb);
-            }
-          } else if (!have_next) {
+          if (!have_next) {
             if (!wait(cflag, k, cb + 1)) return;
             eload(cb);
           }
@@ -777,21 +722,13 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           // non-blocking look at the next row-block: the sc1 poll is issued here and its value consumed only after
           // this slice's MFMAs, so its round trip stays off the chain
           int pollv = 0;
-          if (!kTag && cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q;
             *reinterpret_cast<f64x2*>(E + (e >> 5) * DF_SP + 2 * (e & 31)) = er[q];
           }
-          if constexpr (kTag) {
-            if (tid == 0) s_ok = 1;
-            __syncthreads();
-            if (tfail) s_ok = 0;
-            __syncthreads();
-            if (!s_ok) return;
-          } else {
-            __syncthreads();
-          }
+          __syncthreads();
           {  // L'[16 wv.., 16 cb..] = A[16 wv.., :] L^-1[16 cb.., :]^T, K = 16 (cb + 1), two MFMA chains
             d4f acc;
             switch (cb) {
@@ -804,13 +741,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
             for (int r = 0; r < 4; ++r) {
               const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
               Lp[row * DF_SP + col] = acc[r];
-              if (!kDefer) mA.st(row * ld + col, acc[r]);
             }
           }
           if (tid == 0) s_next = (cb < 3) && pollv >= cb + 2;  // own word: read between this barrier and the next
           __syncthreads();
           have_next = s_next;
-          if (!kTag && have_next) eload(cb + 1);  // lands behind the diagonal update below
+          if (have_next) eload(cb + 1);  // lands behind the diagonal update below
           switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
             case 0: ch_update<0>(dacc, Lp, cb, lane); break;
             case 1: ch_update<1>(dacc, Lp, cb, lane); break;
@@ -827,13 +763,9 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         // below), while wave 0 runs the first sweep -- no drain round trip between the last slice and POTRF(b).  No
         // barrier either: wave 0 starts the sweep on its own D_00, and waves 1..3 count their stored blocks into
         // ps.cntD, which POTRF's first T / U and phase A wait for.
-        if (kDefer) {
-          if (wv > 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) p64w_add(&ps.cntD);
-          }
-        } else {
-          publish(df_tri(b, k), k + 1);  // L_b,k stored
+        if (wv > 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) p64w_add(&ps.cntD);
         }
         mark(k, 1, 2);
       }
@@ -880,7 +812,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         __syncthreads();
       }  // b > 0: reset behind the staging, the tile's LDS stores behind publish()'s barrier
       auto pre = [&](int w, int ln) {  // waves 1..3: L_b,b-1 from Sa to HBM, the last one to drain raises its state
-        if (b == 0 || !kDefer) return;
+        if (b == 0) return;
         const int k = b - 1;
         const Sc1Mem mL(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
         for (int e = 64 * (w - 1) + ln; e < NB * NB / 2; e += 192) {
@@ -892,8 +824,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           __hip_atomic_store(state + df_tri(b, k), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       };
       if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre,
-                                   kTag ? ltag : nullptr, tag_gen, kDpp,
-                                   trace ? trace + 4 * (size_t)(ntasks + 5 * b + 3) : nullptr, kDefer && b > 0)) {
+                                   trace ? trace + 4 * (size_t)(ntasks + 5 * b + 3) : nullptr, b > 0)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
@@ -927,9 +858,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       bool ok;
       if (type == 1) {  // all of Linv_kk published (w_k is awaited inside the task)
         ok = df_wait3(cflag + k, 4, state + df_tri(i, k), k, nullptr, 0, abortw, ctrl);
-      } else if (type == 3 || type == 0) {  // panels k..k+G-1: TRSM(., k+G-1) done implies the earlier ones
-        const int g = type == 3 ? 4 : 8;
-        ok = df_wait3(state + df_tri(i, k + g - 1), k + g, state + df_tri(j, k + g - 1), k + g, state + df_tri(i, j), k,
+      } else if (type == 3) {  // panels k..k+3: TRSM(., k+3) done implies the earlier ones
+        ok = df_wait3(state + df_tri(i, k + 3), k + 4, state + df_tri(j, k + 3), k + 4, state + df_tri(i, j), k,
                       abortw, ctrl);
       } else {
         ok = df_wait3(state + df_tri(i, k), k + 1, state + df_tri(j, k), k + 1, state + df_tri(i, j), k, abortw, ctrl);
@@ -948,10 +878,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       df_updateg<4>(L, ld, i, j, k, smem, qf);
       done_idx = df_tri(i, j);
       done_val = k + 4;
-    } else if (type == 0) {
-      df_updateg<8>(L, ld, i, j, k, smem, qf);
-      done_idx = df_tri(i, j);
-      done_val = k + 8;
     } else {
       df_update(L, ld, i, j, k, smem, qf);
       done_idx = df_tri(i, j);
@@ -970,30 +896,15 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
 
 // work: [0] counter, [2] role ticket, [32] abort word, [64 ..) one state word per lower tile, then one chain flag and
 // one rhs counter per diagonal block; zeroed before every launch.
-bool chol_dataflow_variant_ok(int v) { return v == 0 || v == 1 || v == 2 || v == 3 || v == 7 || v == 11 || v == 15; }
 size_t chol_dataflow_work_ints(int nblk) { return 64 + (size_t)nblk * (nblk + 1) / 2 + 2 * (size_t)nblk; }
 
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace, bool zero_work, const double* Hq, const double* dq, int nq,
-                          bool ruiz_gate, double early_min, bool own_b2, bool defer_pub, double* ltag,
-                          unsigned long long tag_gen, bool dpp_sweep) {
-  const int v = (own_b2 ? 1 : 0) | (defer_pub ? 2 : 0) | (ltag ? 4 : 0) | (dpp_sweep ? 8 : 0);
+                          bool ruiz_gate, double early_min) {
   if (zero_work) (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
-#define CVXG_DF_LAUNCH(VV)                                                                                       \
-  k_chol_dataflow<VV><<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq,  \
-                                          ruiz_gate ? 1 : 0, early_min, ltag, tag_gen)
-  switch (v) {  // the instantiated variants (chol_dataflow_variant_ok)
-    case 0: CVXG_DF_LAUNCH(0); break;
-    case 1: CVXG_DF_LAUNCH(1); break;
-    case 2: CVXG_DF_LAUNCH(2); break;
-    case 3: CVXG_DF_LAUNCH(3); break;
-    case 7: CVXG_DF_LAUNCH(7); break;
-    case 11: CVXG_DF_LAUNCH(11); break;
-    case 15: CVXG_DF_LAUNCH(15); break;
-    default: CVXG_DF_LAUNCH(3); break;
-  }
-#undef CVXG_DF_LAUNCH
+  k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq,
+                                      ruiz_gate ? 1 : 0, early_min);
 }
 
 }  // namespace cvxg

@@ -151,8 +151,6 @@ void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double*
 // k_dataflow.hip: the whole factorization (potrf + trsm + updates + fused forward solve) as one persistent
 // launch over the 64x64 tile DAG in the host-built task order (build_chol_schedule in cvxg.cpp)
 size_t chol_dataflow_work_ints(int nblk);
-// the k_chol_dataflow variants built (bits: 1 own_b2, 2 defer_pub, 4 ltag, 8 dpp_sweep)
-bool chol_dataflow_variant_ok(int v);
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */,
@@ -163,16 +161,9 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                           bool ruiz_gate = false /* true: every workgroup leaves at once when ctrl->ruiz_sweeps < 0
                                                     (a short Ruiz lookahead, cvxg.cpp: factor_attempt) */,
                           double early_min = 0.0 /* > 0: stop (abort word, min_diag and small_piv set) at the first
-                                                    16-column block whose min diag(L) <= early_min */,
-                          bool own_b2 = false /* the chain workgroups apply panel b-2 to block row b themselves
-                                                 (UPDATE(b,b,b-2), UPDATE(b,b-1,b-2) not in `tasks`: chol_schedule
-                                                 with the same flag) */,
-                          bool defer_pub = false /* the chain's TRSM tile L_b,b-1 is stored and published by waves 1..3
-                                                    of POTRF(b) instead of before it */,
-                          double* ltag = nullptr /* nblk x 64 x 64 granules {value, tag} (16 B): the chain polls the
-                                                    L_kk^-1 row-blocks from them instead of the chain flag */,
-                          unsigned long long tag_gen = 0 /* this launch's tag: nonzero, never repeated on the buffer */,
-                          bool dpp_sweep = false /* POTRF's column sweep with DPP broadcasts (bitwise the same) */);
+                                                    16-column block whose min diag(L) <= early_min */);
+// (the chain workgroups apply panel b-2 to block row b themselves: UPDATE(b,b,b-2), UPDATE(b,b-1,b-2) are not in
+// `tasks`, which chol_schedule builds accordingly)
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)
 size_t bwd_work_ints(int nblk);  // flag words + the data-tagged u granules of k_bwd_dataflow
 // Optional epilogue (nrhs = 1): dx = d :* u; with s, also s = dx and x1 = x + s (the speculative line search's

@@ -84,19 +84,6 @@ __device__ __forceinline__ void potrf64w_stage(const double* L, int ld, size_t o
   for (int t = tid; t < NB * nrhs; t += 256) sm.B[t] = mR.ld(t);
 }
 
-// Optional data-tagged copy of L^-1 (the chain's consumer polls it, k_dataflow.hip): granule (r, c) of block k's
-// L^-1 = {value, tag} at base[2 (64 r + c)], stored by whichever wave computes the entry, as soon as it is final.
-// The byte offset is split into a per-lane part (one VGPR for all of a wave's stores) and a wave-uniform part (an
-// SGPR), so the many store sites do not each keep a precomputed per-lane address alive.
-struct TagOut {
-  double* base;  // nullptr: none
-  double tag;
-  __device__ __forceinline__ void put(int lane_bytes, int uni_bytes, double v) const {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f64x2{v, tag}),
-                                           uniform_rsrc(base, (unsigned)(NB * NB * 16)), lane_bytes, uni_bytes, AUX_SC1);
-  }
-};
-
 // 16 x 16 block ops on LDS operands (one wave)
 __device__ __forceinline__ void p64w_T(Potrf64wSmem& sm, int ib, int kb, int lane) {  // L_ib,kb = A_ib,kb L16^-T
   double* C = sm.S + 16 * ib * P64_SP + 16 * kb;
@@ -112,7 +99,7 @@ __device__ __forceinline__ void p64w_U(Potrf64wSmem& sm, int ib, int jb, int kb,
                    lane);
   c16_store(C, P64_SP, acc, lane);
 }
-__device__ __forceinline__ void p64w_X(Potrf64wSmem& sm, int kb, int j, int lane, const TagOut& to) {  // X_kb,j, j < kb
+__device__ __forceinline__ void p64w_X(Potrf64wSmem& sm, int kb, int j, int lane) {  // X_kb,j, j < kb
   d4f T = {0.0, 0.0, 0.0, 0.0};
   for (int m = j; m < kb; ++m)
     T = mfma16_ab(T, sm.S + 16 * kb * P64_SP + 16 * m, P64_SP, sm.X + 16 * m * P64_SP + 16 * j, P64_SP, 1.0, lane);
@@ -124,14 +111,9 @@ __device__ __forceinline__ void p64w_X(Potrf64wSmem& sm, int kb, int j, int lane
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] *= sm.SV[kb][(lane >> 4) + 4 * i];  // row scales (C layout: row (lane>>4) + 4i)
   c16_store(sm.X + 16 * kb * P64_SP + 16 * j, P64_SP, acc, lane);
-  if (to.base) {  // granule (16 kb + (lane >> 4) + 4 i, 16 j + (lane & 15))
-    const int vo = ((lane >> 4) * NB + (lane & 15)) * 16;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) to.put(vo, ((16 * kb + 4 * i) * NB + 16 * j) * 16, acc[i]);
-  }
 }
 // X_kb,kb = (L16^-T)' with the column scales, and the scales of the L16 block of S (L16 = L~16 diag(s))
-__device__ __forceinline__ void p64w_Xdiag(Potrf64wSmem& sm, int kb, int lane, const TagOut& to) {
+__device__ __forceinline__ void p64w_Xdiag(Potrf64wSmem& sm, int kb, int lane) {
   const double* ET = sm.ET[kb];
   const double* sv = sm.SV[kb];
   const int o = 16 * kb;
@@ -140,87 +122,16 @@ __device__ __forceinline__ void p64w_Xdiag(Potrf64wSmem& sm, int kb, int lane, c
     const int e = lane + 64 * i, rr = e >> 4, cc = e & 15;
     const double x = ET[rr * P64_EP + cc] * sv[cc];
     sm.X[(o + cc) * P64_SP + o + rr] = x;
-    if (to.base) to.put(((lane & 15) * NB + (lane >> 4)) * 16, (o * NB + o + 4 * i) * 16, x);  // granule (o + cc, o + rr)
     double* sd = sm.S + (o + rr) * P64_SP + o + cc;
     *sd = (cc <= rr) ? *sd * sv[cc] : 0.0;
   }
 }
 
-// wave 0: eliminate D_kb (S diagonal block kb, all panels < kb applied) -> L16 into S, L16^-T into ET[kb].
-// Returns false on a non-positive pivot (chol_info recorded).
-__device__ __forceinline__ bool p64w_eliminate(Potrf64wSmem& sm, int kb, int base, DevCtrl* ctrl, double& mind,
-                                               int lane, double early_min) {
-  const int o = 16 * kb, r = lane & 15;
-  double a[16];
-  {
-    const double* src = sm.S + (o + r) * P64_SP + o;
-#pragma unroll
-    for (int c = 0; c < 16; c += 2) {
-      const f64x2 v = *reinterpret_cast<const f64x2*>(src + c);
-      a[c] = (lane < 16) ? ((c <= r) ? v[0] : 0.0) : ((lane < 32 && c == r) ? 1.0 : 0.0);
-      a[c + 1] = (lane < 16) ? ((c + 1 <= r) ? v[1] : 0.0) : ((lane < 32 && c + 1 == r) ? 1.0 : 0.0);
-    }
-  }
-  int firstbad = -1;
-  double piv = readlane_d(a[0], 0);
-  double rinv = rcp_nr(piv);
-  double pmin = piv;
-  double mypiv = 1.0;  // lane j keeps p_j: the column scales are formed once, after the sweep, by lanes 0-15
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    double lc[16];
-#pragma unroll
-    for (int c = j + 1; c < 16; ++c) lc[c] = readlane_d(a[j], c);  // D_cj, c > j (lower: lane c, column j)
-    if (!(piv > 0.0) && firstbad < 0) firstbad = j;
-    pmin = fmin(pmin, piv);
-    if (r == j) mypiv = piv;
-    const double rj = rinv;
-    if (j + 1 < 16) {
-      const double dn = readlane_d(a[j + 1], j + 1);
-      piv = fma(-(lc[j + 1] * rj), lc[j + 1], dn);
-      rinv = rcp_nr(piv);
-    }
-    const double t = a[j] * rj;
-#pragma unroll
-    for (int c = j + 1; c < 16; ++c) a[c] = fma(-t, lc[c], a[c]);
-  }
-  const double bmin = pmin * rsqrt_nr(pmin);  // this block's min diag(L) (the value min_diag would take)
-  mind = fmin(mind, bmin);
-  // L~16 (lanes 0-15) and L~16^-T (lanes 16-31) without their column scales; lanes 0-15 publish s_r = p_r^-1/2 (the
-  // consumers scale: p64w_T, p64w_X, p64w_Xdiag)
-  if (lane < 16) sm.SV[kb][r] = rsqrt_nr(mypiv);
-  if (lane < 32) {
-    double* dst = (lane < 16) ? sm.S + (o + r) * P64_SP + o : sm.ET[kb] + r * P64_EP;
-#pragma unroll
-    for (int c = 0; c < 16; c += 2) {
-      f64x2 v;
-      v[0] = (lane >= 16 || c <= r) ? a[c] : 0.0;
-      v[1] = (lane >= 16 || c + 1 <= r) ? a[c + 1] : 0.0;
-      *reinterpret_cast<f64x2*>(dst + c) = v;
-    }
-  }
-  if (firstbad >= 0) {
-    if (lane == 0) atomicCAS(&ctrl->chol_info, 0, base + o + firstbad + 1);
-    return false;
-  }
-  // regularizedCholesky's first attempt (MatrixUtils.scala:458-460): once some diag(L) <= 1e-7 the factor is discarded
-  // and chol(Q + 1e-10 I) taken instead, so the rest of this factorization cannot matter -- stop here.  The test is on
-  // the same value min_diag accumulates, so the host's decision (min_diag <= 1e-7) is the one the full attempt gives.
-  if (early_min > 0.0 && !(bmin > early_min)) {
-    if (lane == 0) {
-      atomic_min_pos(&ctrl->min_diag, bmin);
-      atomicCAS(&ctrl->small_piv, 0, base + o + 1);
-    }
-    return false;
-  }
-  return true;
-}
-
-// The same sweep with the column broadcasts folded into the update instructions (dpp_sweep): every lane-row of 16
-// lanes holds a copy of D_kb (row r in lane r), so D_cj is one DPP row_newbcast:c away and rides in v_fmac_f64_dpp
-// (64-bit DPP, gfx90a+) instead of two v_readlane per broadcast value; the identity border beside it (-> L~16^-T) is
-// a second register row of lane-row 0.  Per entry the same fma as p64w_eliminate -- fma(D_cj, -(a_j r_j), a_c) is
-// fma(-(a_j r_j), D_cj, a_c) -- and the next pivot the same value, so L16, L16^-T and the pivots are bitwise equal.
+// wave 0: eliminate D_kb (S diagonal block kb, all panels < kb applied) -> L~16 into S, L~16^-T into ET[kb], the column
+// scales s_j = p_j^-1/2 into SV[kb] (L16 = L~16 diag(s)).  Returns false on a non-positive pivot (chol_info recorded) or
+// an early stop.  Every lane-row of 16 lanes holds a copy of D_kb (row r in lane r), so D_cj is one DPP row_newbcast:c
+// away and rides in v_fmac_f64_dpp (64-bit DPP, gfx90a+); the identity border beside it (-> L~16^-T) is a second
+// register row of lane-row 0.  (Round 5: bitwise equal to the v_readlane sweep it replaced, 3 170 vs 4 500 cycles.)
 // (microbench/sweep_dpp.hip: 3 600 cycles per 16 columns with 48 panel rows riding along.)
 template <int C>
 __device__ __forceinline__ void p64w_fmac_bc(double& dst, double src, double m) {
@@ -319,25 +230,25 @@ __device__ __forceinline__ bool p64w_eliminate_dpp(Potrf64wSmem& sm, int kb, int
 }
 
 // Phase A / B work of waves 1..3 at step kb (static assignment, see the header).
-__device__ __forceinline__ void p64w_phaseA(Potrf64wSmem& sm, int kb, int w, int lane, const TagOut& to) {
+__device__ __forceinline__ void p64w_phaseA(Potrf64wSmem& sm, int kb, int w, int lane) {
   if (kb == 0) {
     if (w == 1) p64w_T(sm, 2, 0, lane);
     if (w == 2) p64w_T(sm, 3, 0, lane);
-    if (w == 3) p64w_Xdiag(sm, 0, lane, to);
+    if (w == 3) p64w_Xdiag(sm, 0, lane);
   } else if (kb == 1) {
     if (w == 1) p64w_T(sm, 3, 1, lane);
-    if (w == 2) p64w_X(sm, 1, 0, lane, to);
-    if (w == 3) p64w_Xdiag(sm, 1, lane, to);
+    if (w == 2) p64w_X(sm, 1, 0, lane);
+    if (w == 3) p64w_Xdiag(sm, 1, lane);
   } else if (kb == 2) {
-    if (w == 1) p64w_X(sm, 2, 0, lane, to);
-    if (w == 2) p64w_X(sm, 2, 1, lane, to);
-    if (w == 3) p64w_Xdiag(sm, 2, lane, to);
+    if (w == 1) p64w_X(sm, 2, 0, lane);
+    if (w == 2) p64w_X(sm, 2, 1, lane);
+    if (w == 3) p64w_Xdiag(sm, 2, lane);
   } else {
-    if (w == 1) p64w_X(sm, 3, 0, lane, to);
-    if (w == 2) p64w_X(sm, 3, 1, lane, to);
+    if (w == 1) p64w_X(sm, 3, 0, lane);
+    if (w == 2) p64w_X(sm, 3, 1, lane);
     if (w == 3) {
-      p64w_X(sm, 3, 2, lane, to);
-      p64w_Xdiag(sm, 3, lane, to);
+      p64w_X(sm, 3, 2, lane);
+      p64w_Xdiag(sm, 3, lane);
     }
   }
 }
@@ -367,21 +278,17 @@ template <class M, class Fix = NoFix, class Pre = NoPre>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
                                                 Fix fix = Fix(), double early_min = 0.0, Pre pre = Pre(),
-                                                double* ltag = nullptr, unsigned long long tag_gen = 0,
-                                                bool dpp_sweep = false, unsigned long long* rb_stamp = nullptr,
-                                                bool wait_d = false) {
+                                                unsigned long long* rb_stamp = nullptr, bool wait_d = false) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
-  const TagOut to{ltag ? ltag + (size_t)k * NB * NB * 2 : nullptr, __longlong_as_double((long long)tag_gen)};
   double mind = __builtin_inf();
   bool ok = true;
   if (w == 0) {
 #pragma unroll 1
     for (int kb = 0; kb < 4 && ok; ++kb) {
       P64_STAMP(1 + 4 * kb);
-      ok = dpp_sweep ? p64w_eliminate_dpp(sm, kb, base, ctrl, mind, lane, early_min)
-                     : p64w_eliminate(sm, kb, base, ctrl, mind, lane, early_min);
+      ok = p64w_eliminate_dpp(sm, kb, base, ctrl, mind, lane, early_min);
       P64_STAMP(2 + 4 * kb);
       if (!ok) {
         if (lane == 0) __hip_atomic_store(&sm.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -415,7 +322,7 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       if (!ok) break;
       P64_STAMP(1 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      p64w_phaseA(sm, kb, w, lane, to);
+      p64w_phaseA(sm, kb, w, lane);
       P64_STAMP(2 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_add(&sm.cntT[kb]);

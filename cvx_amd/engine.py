@@ -54,7 +54,9 @@ def params_struct(pars) -> L.cvxg_params:
 class Engine:
     """One device context holding the packed problem (P, a, r; A, r_i, ub_i; A_eq, b_eq) and the iterate."""
 
-    def __init__(self, n: int, m: int, p: int = 0, device: int = 0):
+    def __init__(self, n: int, m: int, p: int = 0, device: int = 0, **options):
+        """options: cvxg_set_option settings applied right after creation (before any problem data), e.g.
+        Engine(n, m, early_abort=0); see _lib.OPTIONS."""
         self.lib = L.lib()
         self.n, self.m, self.p = n, m, p
         h = C.c_void_p()
@@ -66,6 +68,12 @@ class Engine:
                 self.lib.cvxg_destroy(h)
                 self.h = C.c_void_p()
             raise CvxgError(rc, f"cvxg_create(n={n}, m={m}, p={p}) failed: {msg}")
+        for name, value in options.items():
+            self.set_option(name, value)
+
+    def set_option(self, name: str, value: int):
+        """cvxg_set_option (include/cvxg.h): name is a key of _lib.OPTIONS."""
+        self._check(self.lib.cvxg_set_option(self.h, L.OPTIONS[name], int(value)))
 
     def close(self):
         if self.h is not None and self.h.value:

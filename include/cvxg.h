@@ -309,6 +309,26 @@ int cvxg_get_counters(cvxg_ctx* ctx, long long* out, int count);
  * loop's.  sweeps <= 0 leaves the setting; *relaunches (if given) receives how many extra batches were launched. */
 int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* relaunches);
 
+/* Engine options.  cvxg_create sets every option to the product default; the other values are measured alternatives
+ * kept for A/B runs and for the tests that hold the default to them.  None changes the reference's semantics, and the
+ * library reads no environment variable that changes arithmetic (tracing aside). */
+enum {
+  CVXG_OPT_SPARSE_ROWS = 1,   /* 1 (default): rows with <= 4 nonzeros are summed per Hessian entry apart from the SYRK;
+                                 0: every row through the SYRK.  Set before cvxg_set_ineq. */
+  CVXG_OPT_EARLY_ABORT = 2,   /* 1 (default): regularizedCholesky's first attempt stops at its first 16-column block with
+                                 min diag(L) <= 1e-7 (MatrixUtils.scala:458-460 discards that factor); 0: it runs on */
+  CVXG_OPT_H_LOWER = 3,       /* 1 (default): the Newton step keeps H's lower triangle only; 0: H is mirrored */
+  CVXG_OPT_KKT_FUSED_RHS = 4, /* 1..9: the KKT columns ride the fused forward solve when p + 1 <= value (default 9 below
+                                 8 Cholesky blocks, else 1: the many-column dataflow solves) */
+  CVXG_OPT_SPEC_REG = 5,      /* 1 (default): after a regularized direction, chol(Q) and chol(Q + 1e-10 I) run side by
+                                 side and the device keeps the one regularizedCholesky keeps; 0: one after the other */
+  CVXG_OPT_RUIZ_LOOP = 6,     /* 0 (default): each Ruiz sweep is a launch pair; 1: the whole loop in one persistent
+                                 launch (CVXG_E_UNSUPPORTED beyond its register batch of tiles) */
+  CVXG_OPT_RUIZ_WG = 7        /* workgroups of the one-launch Ruiz loop (0, the default: one per CU) */
+};
+/* Returns CVXG_E_ARG for an unknown option or a value out of its range. */
+int cvxg_set_option(cvxg_ctx* ctx, int option, long long value);
+
 /* The worker task order of the dataflow Cholesky for nblk diagonal blocks and `workers` simulated workgroups,
  * exactly as cvxg_create builds it (host-only, no device needed): each entry (type << 30) | (k << 20) | (i << 10)
  * | j with type 1 TRSM(i,k), 2 UPDATE(i,j,k), 3 UPDATE4(i,j,k..k+3); the chain tasks are not listed.  Writes at

@@ -38,10 +38,10 @@ __global__ __launch_bounds__(256) void k_p64(double* L, int ld, int k, double* r
     potrf64w_reset(sm);
     __syncthreads();
 #ifdef WITH_LFLAG
-    if (potrf64w_factor<Sc1Mem>(k, rhs, nrhs, Linv, ctrl, sm, &g_lflag, NoFix(), 0.0, NoPre(), nullptr, 0, P64_DPP_ON))
+    if (potrf64w_factor<Sc1Mem>(k, rhs, nrhs, Linv, ctrl, sm, &g_lflag, NoFix(), 0.0, NoPre()))
       potrf64w_store_L<Sc1Mem>(L, ld, k, sm);
 #else
-    if (potrf64w_factor<PlainMem>(k, rhs, nrhs, Linv, ctrl, sm, nullptr, NoFix(), 0.0, NoPre(), nullptr, 0, P64_DPP_ON))
+    if (potrf64w_factor<PlainMem>(k, rhs, nrhs, Linv, ctrl, sm, nullptr, NoFix(), 0.0, NoPre()))
       potrf64w_store_L<PlainMem>(L, ld, k, sm);
 #endif
     __syncthreads();

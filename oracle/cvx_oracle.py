@@ -744,7 +744,7 @@ def equality_line_search(pb: Problem, t: float, x: np.ndarray, d: np.ndarray, q:
 
 def unconstrained_solve(pb: Problem, t: float, x0: np.ndarray, pars: SolverParams,
                         record: bool = False, max_steps: Optional[int] = None, hess="fold",
-                        fast_subst: bool = False) -> Solution:
+                        fast_subst: bool = False, on_step: Optional[Callable] = None) -> Solution:
     """UnconstrainedSolver.scala:34-125 with objF = the barrier objective at parameter t.
 
     Quirks reproduced: rho = 1+1/4 == 1 (integer), so the trust radius stays
@@ -781,6 +781,8 @@ def unconstrained_solve(pb: Problem, t: float, x0: np.ndarray, pars: SolverParam
         it_n += 1
         if record:
             records.append(rec)
+        if on_step is not None:  # instrumentation (long golden runs): observe each finished step
+            on_step(rec)
     return Solution(x=x, newtonDecrement=newtonDecrement, normGrad=normGrad, iter=it_n,
                     maxedOut=it_n >= maxIter, newton_steps=it_n, records=records)
 

@@ -204,9 +204,88 @@ def make_late(states_path):
     print(f"C3LATE: wrote {path} ({os.path.getsize(path) / 1e3:.0f} KB, {time.time() - t0:.0f} s)")
 
 
+def make_whole(threads=6):
+    """C3WHOLE (round 6): the oracle's WHOLE C3 barrier solve with the standard parameters, the reference's t-loop
+    (BarrierSolver.scala:70-117) around UnconstrainedSolver.solve (UnconstrainedSolver.scala:34-125), with the
+    BLAS-ordered Hessian (a per-constraint fold would take minutes per step at n = 4096).  Stored: the per-centering
+    Newton step counts, the x entering every centering, the final x and gap, and one scalar record per Newton step
+    (t, iteration, q, step, both backtracking counters, Ruiz sweeps, regularization flag, fallback, backward error);
+    plus the x and dx of the first two steps of each centering, so the engine's first steps from the oracle's
+    centering start can be compared directly.  A partial file is rewritten after every centering (the three
+    t = 1e10 .. 1e12 centerings run to maxIter, ~1000 steps each)."""
+    from threadpoolctl import threadpool_limits
+    n, m, inst = 4096, 8192, 0
+    t0 = time.time()
+    spec = Z.random_qp(n, m, instance=inst)
+    pb = O.Problem(a0=spec["a0"], r0=spec["r0"], P=spec["P"], A=spec["A"], r=spec["r"], ub=spec["ub"])
+    pars = O.standard_params()
+    sha, psum, a0sum = fingerprint(spec)
+    keys = ("t", "it_n", "q", "f", "step", "kc", "ka", "ruiz", "reg", "fallback", "rel_err")
+    steps = {k: [] for k in keys}
+    first = {"t": [], "it_n": [], "x": [], "dx": []}
+    x_start, per_centering, ts = [], [], []
+    path = os.path.join(HERE, "big", f"C3whole_n{n}_m{m}.npz")
+
+    def save(x, gap, done):
+        arrays = {("step_" + k): np.array(v) for k, v in steps.items()}
+        arrays.update({("first_" + k): np.array(v) for k, v in first.items()})
+        arrays.update(x_start=np.array(x_start), per_centering=np.array(per_centering), t_centering=np.array(ts),
+                      x_final=x, gap=np.array(gap), complete=np.array(done), n=np.array(n), m=np.array(m),
+                      instance=np.array(inst), sha256=np.array(sha), P_sum=np.array(psum), a0_sum=np.array(a0sum),
+                      hess_form=np.array("blas"), blas_threads=np.array(threads))
+        np.savez_compressed(path, **arrays)
+
+    cur = {"t": 1.0}
+
+    def on_step(rc):
+        for k, v in (("t", cur["t"]), ("it_n", rc.it_n), ("q", rc.q), ("f", rc.f), ("step", rc.step),
+                     ("kc", rc.backtracks_c), ("ka", rc.backtracks_armijo), ("ruiz", rc.ruiz_sweeps),
+                     ("reg", rc.regularized), ("fallback", rc.fallback), ("rel_err", rc.rel_err)):
+            steps[k].append(v)
+        if rc.it_n < 2:
+            first["t"].append(cur["t"])
+            first["it_n"].append(rc.it_n)
+            first["x"].append(rc.x.copy())
+            first["dx"].append(rc.dx.copy())
+        if rc.it_n % 50 == 0:
+            print(f"C3WHOLE: t={cur['t']:g} it={rc.it_n} q={rc.q:.3e} step={rc.step:g} reg={rc.regularized} "
+                  f"({time.time() - t0:.0f} s)", flush=True)
+
+    x = spec["x0"].copy()
+    t = 1.0
+    gap = float("inf")
+    if os.path.exists(path):  # resume after the last complete centering of a partial file
+        old = dict(np.load(path))
+        if not bool(old["complete"]) and str(old["sha256"]) == sha:
+            for k in keys:
+                steps[k] = list(old["step_" + k])
+            for k in first:
+                first[k] = list(old["first_" + k])
+            x_start, per_centering, ts = list(old["x_start"]), list(old["per_centering"]), list(old["t_centering"])
+            x, gap, t = old["x_final"].copy(), float(old["gap"]), float(ts[-1]) * 10.0
+            print(f"C3WHOLE: resuming at t={t:g} after {per_centering}", flush=True)
+    with threadpool_limits(threads):
+        while gap >= pars.tolSolver and len(per_centering) < 100:
+            cur["t"] = t
+            x_start.append(x.copy())
+            ts.append(t)
+            sol = O.unconstrained_solve(pb, t, x, pars, hess="blas", fast_subst=True, on_step=on_step)
+            per_centering.append(sol.newton_steps)
+            x = sol.x
+            gap = m / t
+            print(f"C3WHOLE: t={t:g} {sol.newton_steps} steps, counts so far {per_centering} "
+                  f"({time.time() - t0:.0f} s)", flush=True)
+            save(x, gap, gap < pars.tolSolver)
+            t *= 10.0
+    print(f"C3WHOLE: wrote {path} ({os.path.getsize(path) / 1e3:.0f} KB, {time.time() - t0:.0f} s), "
+          f"{sum(per_centering)} Newton steps {per_centering}, gap {gap:.3e}")
+
+
 if __name__ == "__main__":
     for nm in (sys.argv[1:] or ["C2", "C3"]):
-        if nm.startswith("C3LATE"):  # C3LATE=<states.npz from scripts/c3_late_states.py>
+        if nm == "C3WHOLE":
+            make_whole()
+        elif nm.startswith("C3LATE"):  # C3LATE=<states.npz from scripts/c3_late_states.py>
             make_late(nm.split("=", 1)[1] if "=" in nm else os.path.join(HERE, "..", "..", "gpurun_out",
                                                                          "c3_late_states.npz"))
         else:

@@ -66,6 +66,17 @@ def test_bad_arguments_rejected(lib):
     assert lib.cvxg_create(0, 4, 4, 4, C.byref(h)) == _lib.CVXG_E_DIM  # p < n (EqualityConstraint.scala:18-20)
     assert lib.cvxg_create(0, 1023 * 64 + 1, 4, 0, C.byref(h)) == _lib.CVXG_E_UNSUPPORTED
     assert lib.cvxg_newton_step(None, None, None) == _lib.CVXG_E_ARG
+    assert lib.cvxg_set_option(None, _lib.OPTIONS["early_abort"], 0) == _lib.CVXG_E_ARG
+
+
+def test_no_environment_switches_in_the_product():
+    """The library reads no environment variable that changes arithmetic: the engine options go
+    through cvxg_set_option; the only getenv calls left name the two tracing files."""
+    import glob
+    calls = []
+    for f in glob.glob(os.path.join(ROOT, "cvx_amd", "csrc", "*")):
+        calls += re.findall(r'getenv\("(\w+)"\)', open(f).read())
+    assert set(calls) <= {"CVXG_DF_TRACE", "CVXG_RUIZ_TRACE"}, calls
 
 
 # A stand-in for the few (nine) JNI declarations jni/cvxg_jni.c uses, with the JDK's C signatures (jni.h: JNIEnv is a
@@ -127,9 +138,10 @@ def test_jni_glue_binds_every_scala_native_and_every_step_entry():
     assert "GetPrimitiveArrayCritical" not in c_src  # no critical region spans a GPU call
 
 
-# C-ABI entry points a Scala caller has no use for: instrumentation and the host-only schedule dump
+# C-ABI entry points a Scala caller has no use for: instrumentation, the engine's A/B options and the host-only schedule
+# dump
 _JNI_EXEMPT = {"cvxg_set_timing", "cvxg_get_phase_times", "cvxg_get_phase_stats", "cvxg_get_counters", "cvxg_set_ruiz_lookahead",
-               "cvxg_chol_schedule"}
+               "cvxg_chol_schedule", "cvxg_set_option"}
 
 
 def _camel(sym):

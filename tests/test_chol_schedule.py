@@ -3,8 +3,7 @@ claim in order, cvx_amd/csrc/cvxg.cpp build_chol_schedule) -- host-only, no GPU.
 
 Deadlock freedom of the persistent launch rests on two properties checked here for several block counts:
   * coverage: every TRSM / UPDATE of the right-looking tile factorization (MatrixUtils.scala:452-461 as 64 x 64
-    tiles) is either listed exactly once (UPDATE4 / UPDATE8 covering four / eight consecutive panels of one tile, the
-    latter with CVXG_DF_GROUP8=1) or is a chain task
+    tiles) is either listed exactly once (UPDATE4 covering four consecutive panels of one tile) or is a chain task
     (POTRF(k), TRSM(k+1,k), UPDATE(k+1,k+1,k), UPDATE(k+2,k+2,k), UPDATE(k+2,k+1,k): run by the chain workgroups,
     never listed);
   * order: a listed task appears after every listed task it depends on (a claimed task only ever waits on tasks
@@ -35,23 +34,19 @@ def _is_chain(typ, k, i, j):
     return (typ == 1 and i == k + 1) or (typ == 2 and i == j == k + 1) or (typ == 2 and i == k + 2 and j in (i, i - 1))
 
 
-@pytest.mark.parametrize("group8", [False, True])
-@pytest.mark.parametrize("nblk", [2, 4, 10, 16, 64])
-def test_schedule_covers_every_task_once_in_dependency_order(nblk, group8, monkeypatch):
-    monkeypatch.setenv("CVXG_DF_GROUP8", "1" if group8 else "0")
+@pytest.mark.parametrize("nblk", [1, 2, 3, 4, 10, 16, 64])
+def test_schedule_covers_every_task_once_in_dependency_order(nblk):
     order = _order(nblk)
-    if group8 and nblk == 64:
-        assert any(v[0] == 0 for v in order)  # eight-panel groups are used
     pos_trsm = {}    # (i, k) -> position
     pos_upd = {}     # (i, j, panel) -> position of the task applying that panel to tile (i, j)
     for p, (typ, k, i, j) in enumerate(order):
-        assert typ in (0, 1, 2, 3)  # 0: UPDATE8
+        assert typ in (1, 2, 3)
         assert not _is_chain(typ, k, i, j), "chain tasks are run by the chain workgroups, not listed"
         if typ == 1:
             assert i > k and (i, k) not in pos_trsm
             pos_trsm[(i, k)] = p
         else:
-            cnt = {3: 4, 0: 8}.get(typ, 1)
+            cnt = 4 if typ == 3 else 1
             assert k + cnt <= j <= i
             for kk in range(k, k + cnt):
                 assert (i, j, kk) not in pos_upd, "a panel applied twice to a tile"

@@ -36,9 +36,10 @@ def _opb(O, spec):
                      kl_B=spec.get("kl_B"), kl_R=kl_R)
 
 
-def _engine(Engine, spec):
+def _engine(Engine, spec, **options):
+    """An engine holding spec; options: cvxg_set_option settings (include/cvxg.h), applied before the data."""
     p = 0 if spec.get("Aeq") is None else spec["Aeq"].shape[0]
-    e = Engine(spec["a0"].shape[0], spec["A"].shape[0], p)
+    e = Engine(spec["a0"].shape[0], spec["A"].shape[0], p, **options)
     e.load_problem(spec)
     return e
 
@@ -67,16 +68,12 @@ def test_barrier_oracles_match(mods, n, m):
 def test_sparse_rows_hessian_and_direction(mods, n, m):
     """Problems with bound / difference / phase-I style rows: the engine sums their Hessian entries apart from
     the dense-row SYRK.  Barrier oracles vs the oracle (1e-12), the same H as the all-dense SYRK path
-    (CVXG_SPARSE_ROWS=0), and the Newton direction within 1e-8 of the oracle."""
+    (CVXG_OPT_SPARSE_ROWS 0), and the Newton direction within 1e-8 of the oracle."""
     Z, SP, Engine, O = mods
     spec = Z.random_qp_bounds(n, m, instance=5)
     pb = _opb(O, spec)
     eng = _engine(Engine, spec)
-    os.environ["CVXG_SPARSE_ROWS"] = "0"
-    try:
-        eng_dense = _engine(Engine, spec)
-    finally:
-        del os.environ["CVXG_SPARSE_ROWS"]
+    eng_dense = _engine(Engine, spec, sparse_rows=0)
     pars = SP.standardParams()
     rng = np.random.default_rng(4)
     x = 1e-3 * rng.uniform(-1.0, 1.0, n) / np.sqrt(n)
@@ -563,17 +560,16 @@ def test_equality_kkt_direction_vs_oracle(mods):
 
 @pytest.mark.parametrize("n,p,fused", [(200, 1, 9), (200, 8, 9), (200, 8, 1), (200, 9, 9), (200, 12, 9), (200, 64, 9),
                                        (200, 100, 9), (200, 150, 9), (1024, 40, 9), (1024, 130, 9)])
-def test_equality_kkt_direction_any_p(mods, n, p, fused, monkeypatch):
+def test_equality_kkt_direction_any_p(mods, n, p, fused):
     """KKTSystem.solve (KKTSystem.scala:43-167) for any number of equality rows (k_kkt.hip): X = Q^-1 [B' | Dq] from
     the factorization's fused forward solve + the backward solve (p + 1 <= 9) or the many-column dataflow solves with
-    L and L' (p >= 9, and p = 8 with CVXG_KKT_FUSED_RHS=1), S = (R + R')/2 with R = B X factored by one workgroup
+    L and L' (p >= 9, and p = 8 with CVXG_OPT_KKT_FUSED_RHS 1), S = (R + R')/2 with R = B X factored by one workgroup
     (p <= 64) or the dataflow Cholesky (p = 100, 150).  dx within 1e-8 and w within 1e-7 of the oracle's KKTSystem
     at t = 1 and 100."""
-    monkeypatch.setenv("CVXG_KKT_FUSED_RHS", str(fused))
     Z, SP, Engine, O = mods
     spec = Z.random_qp_eq(n, 360 if n == 200 else 2 * n, p, instance=3)
     pb = _opb(O, spec)
-    eng = _engine(Engine, spec)
+    eng = _engine(Engine, spec, kkt_fused_rhs=fused)
     pars = SP.standardParams()
     x = spec["x0"]
     for t in (1.0, 100.0):
@@ -927,7 +923,7 @@ def _kl_centerings(eng, pars, t_max=1e12, on_step=None):
 
 
 @pytest.mark.parametrize("fused,sparse", [("1", "1"), ("9", "1"), ("1", "0"), ("9", "0")])
-def test_kl_direct_solves_vs_oracle_fixture(mods, monkeypatch, fused, sparse):
+def test_kl_direct_solves_vs_oracle_fixture(mods, fused, sparse):
     """The direct KL solves at n = 2048 (kl_1, kl_2: OptimizationProblems.scala:167-210, 271-320, the first solve
     MinimizationTests.runProblems makes, MinimizationTests.scala:23,35) from the oracle's own phase-I point, against the
     oracle's whole solve (tests/golden/make_golden_kl.py), under four settings that give the Newton direction different
@@ -940,14 +936,12 @@ def test_kl_direct_solves_vs_oracle_fixture(mods, monkeypatch, fused, sparse):
     CVXG_E_LINESEARCH (profiles/r05/kl_direct/).  Here: no exception in any setting, the oracle's step counts in every
     centering up to t = 1e4, 13 centerings, the gaps below tolSolver and the final x within 1e-9 of the oracle's."""
     Z, SP, Engine, O = mods
-    monkeypatch.setenv("CVXG_KKT_FUSED_RHS", fused)
-    monkeypatch.setenv("CVXG_SPARSE_ROWS", sparse)
     fx = dict(np.load(_KL_FIXTURE))
     n = int(fx["n"])
     pars = SP.standardParams()
     for kind in ("kl_1", "kl_2"):
         spec = Z.kl_primal_spec(n, kind)
-        eng = Engine(n, spec["A"].shape[0], spec["Aeq"].shape[0])
+        eng = Engine(n, spec["A"].shape[0], spec["Aeq"].shape[0], kkt_fused_rhs=int(fused), sparse_rows=int(sparse))
         eng.load_problem(spec)
         eng.set_x(fx[f"{kind}_x0"])
         per = _kl_centerings(eng, pars)
@@ -1573,12 +1567,12 @@ def test_regularized_cholesky_retry_branch(mods):
     assert np.linalg.norm(dx - dref) <= 64 * u * (w[-1] / w[0]) * np.linalg.norm(dref)
 
 
-def test_regularized_first_attempt_stops_early(mods, monkeypatch):
+def test_regularized_first_attempt_stops_early(mods):
     """regularizedCholesky (MatrixUtils.scala:452-461) discards chol(Q) as soon as min diag(L) <= 1e-7 and factors
     Q + 1e-10 I, so the engine stops its first attempt at the first 16-column block with such a pivot
     (k_chol_dataflow's early_min) instead of running it to the end.  A mid-matrix small pivot -- columns 300 and 301 of
     A nearly parallel, n = 600 (10 Cholesky blocks) -- stops it in the block of rows 289..304 (small_pivot = 289);
-    with the stop disabled (CVXG_EARLY_ABORT=0) the attempt runs on past that block (to its first non-positive pivot,
+    with the stop disabled (CVXG_OPT_EARLY_ABORT 0) the attempt runs on past that block (to its first non-positive pivot,
     which small_pivot then reports, or to the end: 0).  Both give bitwise the same dx, min diag(L) and regularization
     flag (the oracle's), and a whole Newton step from there the same x."""
     Z, SP, Engine, O = mods
@@ -1597,8 +1591,7 @@ def test_regularized_first_attempt_stops_early(mods, monkeypatch):
     assert rec.regularized == 1 and rec.fallback == 0
     out = {}
     for early in ("1", "0"):
-        monkeypatch.setenv("CVXG_EARLY_ABORT", early)
-        eng = _engine(Engine, spec)
+        eng = _engine(Engine, spec, early_abort=int(early))
         dx, _, info = eng.newton_direction(pars, 1.0, x, grad=g)
         eng.set_x(x)
         eng.centering_begin(1.0)
@@ -1613,51 +1606,11 @@ def test_regularized_first_attempt_stops_early(mods, monkeypatch):
     assert abs(a[2] - np.min(rec.diagL)) <= 1e-6 * np.min(rec.diagL)
 
 
-@pytest.mark.parametrize("n,m", [(200, 400), (1024, 2048), (4096, 8192)])
-def test_chain_owned_panel_updates_bitwise(mods, monkeypatch, n, m):
-    """The chain workgroups of k_chol_dataflow apply panel b-2 to block row b themselves (UPDATE(b,b,b-2) and
-    UPDATE(b,b-1,b-2) taken out of the worker list, CVXG_CHAIN_B2=1, the default): the MFMA sequences are the
-    workers' (K = 0..63 in order on the same accumulator), so the factorization is bitwise the one with the workers
-    applying them (CVXG_CHAIN_B2=0).  Likewise the chain's TRSM tile L_b,b-1 stored and published by waves 1..3 of
-    POTRF(b) (CVXG_CHAIN_DEFER=1, the default) or before it (=0), and the L_kk^-1 row-blocks handed to the chain as
-    data-tagged granules (CVXG_CHAIN_TAG=1) or behind the chain flag, and POTRF's column sweep with DPP broadcasts
-    (CVXG_CHAIN_DPP=1, the default: the same fma per entry) or v_readlane.  Checked on dx, min diag(L) and a whole Newton step, at
-    t = 1 and at later t, for every built variant (k_dataflow.hip: chol_dataflow_variant_ok)."""
-    Z, SP, Engine, O = mods
-    spec = Z.random_qp(n, m, instance=3)
-    pars = SP.standardParams()
-    states = [(1.0, spec["x0"], None, 0, float("nan")), (1e8, spec["x0"], None, 0, float("nan"))]
-    if n == 4096:  # plus a late C3 state whose first attempt is discarded (both factorizations through the chain)
-        fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "big", "C3late_n4096_m8192.npz")))
-        spec = Z.random_qp(n, m, instance=int(fx["instance"]))
-        states = [(1.0, spec["x0"], None, 0, float("nan"))] + [
-            (float(fx["t"][k]), fx["x"][k], fx["grad"][k], int(fx["it_n"][k]), float(fx["radius"][k])) for k in (2, 6)]
-    out = {}
-    variants = ("1101", "0000", "0100", "1000", "1100", "1110", "1111")  # (B2, DEFER, TAG, DPP): the built variants
-    for flag in variants:
-        for name, v in zip(("CVXG_CHAIN_B2", "CVXG_CHAIN_DEFER", "CVXG_CHAIN_TAG", "CVXG_CHAIN_DPP"), flag):
-            monkeypatch.setenv(name, v)
-        eng = _engine(Engine, spec)
-        res = []
-        for t, x, g, it_n, radius in states:
-            dx, _, info = eng.newton_direction(pars, t, x, grad=g)
-            eng.set_x(x)
-            eng.centering_resume(t, it_n, radius, grad=g)
-            st = eng.newton_step(pars)
-            res.append((dx, info.min_diag, info.regularized, st.step, eng.get_x()))
-        out[flag] = res
-        eng.close()
-    for other in variants[1:]:
-        for a, b in zip(out["1101"], out[other]):
-            assert np.array_equal(a[0], b[0]) and a[1] == b[1] and a[2] == b[2] and a[3] == b[3], other
-            assert np.array_equal(a[4], b[4]), other
-
-
 @pytest.mark.parametrize("n,m,wg", [(200, 400, 0), (1000, 2000, 0), (1000, 2000, 3), (4096, 8192, 0)])
-def test_ruiz_loop_bitwise(mods, monkeypatch, n, m, wg):
-    """Every Ruiz sweep in one persistent launch (k_ruiz.hip, CVXG_RUIZ_LOOP=1, the default) against the two launches
-    per sweep of k_ruiz_tiles / k_ruiz_rows (CVXG_RUIZ_LOOP=0): the same partial sums in the same order, so the sweep
-    count, min diag(L) and dx are bitwise equal.  n = 1000 has a partial last block; wg = 3 (CVXG_RUIZ_WG) leaves most
+def test_ruiz_loop_bitwise(mods, n, m, wg):
+    """Every Ruiz sweep in one persistent launch (k_ruiz.hip, CVXG_OPT_RUIZ_LOOP 1) against the two launches per sweep
+    of k_ruiz_tiles / k_ruiz_rows (CVXG_OPT_RUIZ_LOOP 0, the default): the same partial sums in the same order, so the
+    sweep count, min diag(L) and dx are bitwise equal.  n = 1000 has a partial last block; wg = 3 (CVXG_OPT_RUIZ_WG) leaves most
     tiles to the claims beyond the register batch, streamed from H every sweep.  At n = 4096 also two late C3 states
     (13 sweeps, t = 1e11 and 1e12, the second regularized)."""
     Z, SP, Engine, O = mods
@@ -1668,12 +1621,9 @@ def test_ruiz_loop_bitwise(mods, monkeypatch, n, m, wg):
         fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "big", "C3late_n4096_m8192.npz")))
         spec = Z.random_qp(n, m, instance=int(fx["instance"]))
         states = [(1.0, spec["x0"], None)] + [(float(fx["t"][k]), fx["x"][k], fx["grad"][k]) for k in (2, 6)]
-    if wg:
-        monkeypatch.setenv("CVXG_RUIZ_WG", str(wg))
     out = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("CVXG_RUIZ_LOOP", flag)
-        eng = _engine(Engine, spec)
+        eng = _engine(Engine, spec, ruiz_loop=int(flag), ruiz_wg=wg)
         out[flag] = []
         for t, x, g in states:
             dx, _, info = eng.newton_direction(pars, t, x, grad=g)
@@ -1685,12 +1635,15 @@ def test_ruiz_loop_bitwise(mods, monkeypatch, n, m, wg):
     print(f"n={n}: Ruiz sweeps {[r[1] for r in out['1']]}")
 
 
-def test_speculative_regularized_pair_bitwise(mods, monkeypatch):
+@pytest.mark.parametrize("ruiz_loop", [0, 1])
+def test_speculative_regularized_pair_bitwise(mods, ruiz_loop):
     """After a regularized Newton direction the next one runs chol(Q) and chol(Q + 1e-10 I) side by side
-    (cvxg.cpp: regularized_cholesky_spec, CVXG_SPEC_REG=1, the default) and the device keeps the one
+    (cvxg.cpp: regularized_cholesky_spec, CVXG_OPT_SPEC_REG 1, the default) and the device keeps the one
     regularizedCholesky keeps (MatrixUtils.scala:452-461).  Over late C3 states -- regularized, regularized,
     regularized, then one that is not (the pair's first attempt kept) and a Newton step from there -- Δx,
-    min diag(L), the regularization flag and the step's x are bitwise those of the one-after-the-other form."""
+    min diag(L), the regularization flag and the step's x are bitwise those of the one-after-the-other form -- with the
+    multi-launch Ruiz lookahead (the pair's launches gated on it) and with the one-launch Ruiz loop (its abort word
+    checked on the pair's host read too)."""
     Z, SP, Engine, O = mods
     fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "big", "C3late_n4096_m8192.npz")))
     spec = Z.random_qp(4096, 8192, instance=int(fx["instance"]))
@@ -1698,8 +1651,7 @@ def test_speculative_regularized_pair_bitwise(mods, monkeypatch):
     seq = (5, 6, 7, 2, 6)
     out = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("CVXG_SPEC_REG", flag)
-        eng = _engine(Engine, spec)
+        eng = _engine(Engine, spec, spec_reg=int(flag), ruiz_loop=ruiz_loop)
         res = []
         for k in seq:
             t, x, g = float(fx["t"][k]), fx["x"][k], fx["grad"][k]
@@ -1908,15 +1860,14 @@ def test_speculative_next_evaluation_bitwise(mods):
 
 
 @pytest.mark.parametrize("n,m", [(384, 700), (1024, 2048)])
-def test_ruiz_lookahead_equals_full_loop(mods, monkeypatch, n, m):
-    """The multi-launch Ruiz form (CVXG_RUIZ_LOOP=0; the one-launch loop has nothing to look ahead of): the Newton
+def test_ruiz_lookahead_equals_full_loop(mods, n, m):
+    """The multi-launch Ruiz form (CVXG_OPT_RUIZ_LOOP 0; the one-launch loop has nothing to look ahead of): the Newton
     step first launches only the sweeps the previous step needed + 1 (cvxg.cpp: ruiz_lookahead) and launches more
     while the loop is not done.  Every lookahead -- all 20 sweeps, one sweep, exactly the count, one short -- gives
     bitwise the same dx and sweep count (MatrixUtils.scala:240-268), and only the short ones launch more."""
     Z, SP, Engine, O = mods
-    monkeypatch.setenv("CVXG_RUIZ_LOOP", "0")
     spec = Z.random_qp(n, m, instance=23)
-    eng = _engine(Engine, spec)
+    eng = _engine(Engine, spec, ruiz_loop=0)
     pars = SP.standardParams()
     x = spec["x0"]
     for t in (1.0, 1e4):
