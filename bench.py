@@ -205,6 +205,15 @@ def pmc_traffic(kernel_prefixes, exclude=()):
     return total, os.path.relpath(PMC_TRAFFIC, ROOT) + ":" + "+".join(used)
 
 
+def engine_options(args):
+    """--opt name=value (repeatable): cvxg_set_option settings for A/B runs (include/cvxg.h; product defaults otherwise)."""
+    out = {}
+    for kv in getattr(args, "opt", None) or []:
+        k, v = kv.split("=", 1)
+        out[k] = int(v)
+    return out
+
+
 def workload_spec(args, rank):
     """The per-rank synthetic instance of the selected workload (seed 20261015 + rank): (spec, n, m, SYRK rows, name)."""
     from cvx_amd import problems as Z
@@ -274,7 +283,7 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
     pars = SolverParams.standardParams()
 
     p_eq = 0 if spec.get("Aeq") is None else spec["Aeq"].shape[0]
-    eng = engine_cls(n, m, p_eq, device=local_rank)
+    eng = engine_cls(n, m, p_eq, device=local_rank, **engine_options(args))
     eng.load_problem(spec)
     eng.set_x(spec["x0"])
     state = {"t": 1.0}
@@ -499,7 +508,7 @@ def run_full_solve(args):
     from cvx_amd import problems as Z
     spec = Z.random_qp(n, m, instance=0)
     pars = SolverParams.standardParams()
-    eng = Engine(n, m, 0, device=0)
+    eng = Engine(n, m, 0, device=0, **engine_options(args))
     eng.load_problem(spec)
 
     def solve(timed):
@@ -587,7 +596,10 @@ def run_shared_gpu(args):
     (the t-loop of BarrierSolver.scala:70-117 per instance); aggregate Newton steps/s over K steps per instance
     against one instance alone on the same box.  Shows how much of the Cholesky chain's idle workers and the
     host/launch gaps a second independent instance reclaims (config C5's independence, one GPU).  Also times the
-    lockstep form, cvxg_batch_newton_step (one call advances every instance by one step)."""
+    lockstep form, cvxg_batch_newton_step (one call advances every instance by one step).
+    --workload C2X (round 6): the same with C2 instances (n = 1024, m = 2048), the form SURVEY.md §8d prescribes for the
+    smaller configuration -- one C2 step leaves most of the chip idle -- with the combined roofline fraction of the
+    aggregate rate beside it."""
     import threading
 
     import torch
@@ -596,12 +608,13 @@ def run_shared_gpu(args):
     from cvx_amd.api import SolverParams
     from cvx_amd.engine import Engine, batch_newton_step
     torch.cuda.set_device(0)
-    n, m, k = args.n or 4096, args.m or 8192, max(2, args.instances)
+    c2 = args.workload == "C2X"
+    n, m, k = args.n or (1024 if c2 else 4096), args.m or (2048 if c2 else 8192), max(2, args.instances)
     pars = SolverParams.standardParams()
     specs = [Z.random_qp(n, m, instance=i) for i in range(k)]
     engs = []
     for spec in specs:
-        e = Engine(n, m, 0, device=0)
+        e = Engine(n, m, 0, device=0, **engine_options(args))
         e.load_problem(spec)
         engs.append(e)
     ts = [1.0] * k
@@ -653,15 +666,22 @@ def run_shared_gpu(args):
     lock = k * args.steps / (time.perf_counter() - t0)
     for e in engs:
         e.close()
+    # SURVEY §8d's combined roofline: the assembly SYRK's and the factorization's flops per step at the aggregate rate
+    flop = m * n * (n + 1) + n ** 3 / 3 + n ** 2 / 2 + n / 6
+    roof = {"bound": "mfma", "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "flop_per_step": flop,
+            "achieved_threaded": flop * agg / 1e12, "frac_threaded": flop * agg / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+            "achieved_lockstep": flop * lock / 1e12, "frac_lockstep": flop * lock / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+            "achieved_one": flop * one / 1e12, "frac_one": flop * one / 1e12 / FP64_MFMA_PEAK_TFLOPS}
+    name = "C2X" if c2 else "C3X2"
     return {"metric": METRIC, "value": agg, "unit": "Newton KKT solves/s", "n_gpus": 1, "steps": args.steps * k,
             "warmup": args.warmup, "ms_per_step": el / (k * args.steps) * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded generators of cvx_amd/problems.py, SURVEY.md §8d)",
-            "config": {"workload": f"C3X2: {k} independent C3 random dense QPs n={n} m={m} sharing one MI355X, one "
+            "config": {"workload": f"{name}: {k} independent random dense QPs n={n} m={m} sharing one MI355X, one "
                                    "context + stream + host thread each, full barrier Newton iterations",
                        "n": n, "m": m, "instances": k},
             "one_instance_steps_per_s": one, "aggregate_over_one": agg / one,
-            "lockstep_batch_steps_per_s": lock}
+            "lockstep_batch_steps_per_s": lock, "roofline": roof}
 
 
 def main():
@@ -670,19 +690,22 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="C3",
-                    choices=["C2", "C3", "C3B", "C3EQ", "C4", "C4P", "C2PD", "C3PD", "C3FULL", "C3X2"],
+                    choices=["C2", "C3", "C3B", "C3EQ", "C4", "C4P", "C2PD", "C3PD", "C3FULL", "C3X2", "C2X"],
                     help="C3 (default, the metric's config): random dense QP n=4096 m=8192; C2: n=1024 m=2048; "
                          "C3B: C3 plus 9216 sparse bound / difference rows; C4: KL dual, 2048 outcomes, k=512; "
                          "C2PD / C3PD: the primal-dual solver (solverType PD) on C2 / C3, steps = its KKT solves; "
                          "C3EQ: C3 with --p equality rows (KKT path); C4P: the direct KL solve, n = 2048; "
                          "C3FULL: one complete C3 barrier solve with standard parameters (steady state over the path); "
-                         "C3X2: --instances independent C3 problems sharing one GPU (aggregate steps/s)")
+                         "C3X2: --instances independent C3 problems sharing one GPU (aggregate steps/s); "
+                         "C2X: the same with C2 problems")
     ap.add_argument("--instances", type=int, default=2, help="instances of C3X2")
     ap.add_argument("--p", type=int, default=64, help="equality rows of C3EQ")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--m", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=30.0)
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option name=value (cvxg_set_option, e.g. ruiz_loop=1); A/B runs only")
     args = ap.parse_args()
 
     from cvx_amd import dist as D
@@ -690,7 +713,7 @@ def main():
     if args.workload == "C3FULL":
         print(json.dumps(run_full_solve(args)), flush=True)
         return
-    if args.workload == "C3X2":
+    if args.workload in ("C3X2", "C2X"):
         print(json.dumps(run_shared_gpu(args)), flush=True)
         return
     out, _ = run_rank(args)

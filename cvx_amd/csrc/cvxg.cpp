@@ -86,6 +86,7 @@ struct cvxg_ctx {
   // matrices
   double *H = nullptr, *L = nullptr, *Linv = nullptr, *Hsave = nullptr;
   double *ruiz0 = nullptr, *ruiz1 = nullptr, *dfin = nullptr, *hdiag = nullptr;
+  double* ruiz_S1 = nullptr;  // Ruiz partials of the odd sweeps (ctx->part holds the even ones)
   double *rhs = nullptr, *sol = nullptr;
   double* part = nullptr;
   size_t part_bytes = 0;
@@ -836,11 +837,10 @@ static void ruiz_sweeps(cvxg_ctx* ctx, int k0, int k1) {
     return;
   }
   if (k0 == 0) launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl);
-  for (int k = k0; k < k1; ++k) {
-    const double* dc = (k & 1) ? ctx->ruiz1 : ctx->ruiz0;
-    double* dn = (k & 1) ? ctx->ruiz0 : ctx->ruiz1;
-    launch_ruiz_sweep_tri(s, ctx->H, ctx->np, ctx->n, ctx->np, dc, dn, ctx->part, ctx->ctrl, k);
-  }
+  // one launch per sweep (k_ruiz_tiles_f: each sweep forms the previous one's d itself) and one row pass for the last
+  double* const dd[2] = {ctx->ruiz0, ctx->ruiz1};
+  double* const SS[2] = {ctx->part, ctx->ruiz_S1};
+  launch_ruiz_sweeps_fused(s, ctx->H, ctx->np, ctx->n, ctx->np, dd, SS, ctx->ctrl, k0, k1);
   launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl, k1);
 }
 static void ruiz(cvxg_ctx* ctx) {
@@ -1004,7 +1004,7 @@ static int spec_alloc(cvxg_ctx* ctx) {
   hipStream_t s3 = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = dalloc(ctx, &L2, np * np);
-  if (rc == CVXG_OK) rc = dalloc(ctx, &Linv2, (size_t)ctx->nblk * NB * NB);
+  if (rc == CVXG_OK) rc = dalloc(ctx, &Linv2, chol_dataflow_linv_doubles(ctx->nblk));
   if (rc == CVXG_OK) rc = dalloc(ctx, &rhs2, np * MAX_RHS);
   if (rc == CVXG_OK) rc = dalloc(ctx, &w2, chol_dataflow_work_ints(ctx->nblk));
   if (rc == CVXG_OK) rc = dalloc(ctx, &c2, 1);
@@ -1320,7 +1320,7 @@ static int kkt_alloc(cvxg_ctx* ctx, bool fused) {
       ctx->s_nblk = ps / NB;
       CHK(dalloc(ctx, &ctx->sL, (size_t)ps * ps));
       HIPC(ctx, hipMemsetAsync(ctx->sL, 0, (size_t)ps * ps * sizeof(double), ctx->s));
-      CHK(dalloc(ctx, &ctx->sLinv, (size_t)ctx->s_nblk * NB * NB));
+      CHK(dalloc(ctx, &ctx->sLinv, chol_dataflow_linv_doubles(ctx->s_nblk)));
       CHK(dalloc(ctx, &ctx->kzp, (size_t)ps));
       CHK(dalloc(ctx, &ctx->sw, (size_t)ps));
       std::vector<unsigned> order = chol_schedule(ctx->s_nblk, ctx->ncu);
@@ -1866,7 +1866,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
   for (double** v : {&ctx->c, &ctx->d, &ctx->invd, &ctx->w, &ctx->logd, &ctx->e}) CHK(dalloc(ctx, v, std::max(mp, np)));
   CHK(dalloc(ctx, &ctx->H, np * np));
   CHK(dalloc(ctx, &ctx->L, np * np));
-  CHK(dalloc(ctx, &ctx->Linv, (size_t)ctx->nblk * NB * NB));
+  CHK(dalloc(ctx, &ctx->Linv, chol_dataflow_linv_doubles(ctx->nblk)));
   {  // dataflow Cholesky: task order for this tile count, work words
     (void)hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device);
     ctx->ncu = std::max(ctx->ncu, 1);
@@ -1904,6 +1904,7 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     part = std::max(part, (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE);
   CHK(dalloc(ctx, &ctx->part, part));
   CHK(dalloc(ctx, &ctx->hsv_part, (size_t)ctx->nblk * np));
+  CHK(dalloc(ctx, &ctx->ruiz_S1, (size_t)ctx->nblk * np));
   if (const char* e = getenv("CVXG_RUIZ_TRACE")) ctx->ruiz_trace_path = e;  // instrumentation only (the loop's stamps)
   CHK(dalloc(ctx, &ctx->spart,
              ctx->nsplit > 1 ? (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE : (size_t)1));
@@ -1941,7 +1942,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
   void* ptrs[] = {ctx->P, ctx->a0, ctx->A, ctx->r, ctx->ub, ctx->Aeq, ctx->beq, ctx->x, ctx->y, ctx->dx, ctx->sdir,
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
-                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->ruiz_S, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
+                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->ruiz_S1, ctx->ruiz_S, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
                   ctx->ls_log, ctx->ls_pcnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,

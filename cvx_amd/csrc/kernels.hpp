@@ -81,6 +81,11 @@ void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl, double* 
 // The same sweep from the lower triangle only (64 x 64 tiles -> partials S[nbn][nbn*64] -> fixed-order row sums).
 void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np, const double* dcur, double* dnext,
                            double* S, DevCtrl* ctrl, int k);
+// Sweeps k0 .. k1-1 with one launch per sweep (k_ruiz_tiles_f) plus one k_ruiz_rows for the last: the same d, rho and
+// sweep count as launch_ruiz_sweep_tri over those sweeps.  d_k lives in d[k & 1]; S[0], S[1] hold alternate sweeps'
+// partials (nbn x nbn*64 each).
+void launch_ruiz_sweeps_fused(hipStream_t s, const double* H, int ld, int n, int np, double* const d[2],
+                              double* const S[2], DevCtrl* ctrl, int k0, int k1);
 void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl, int k1,
                        const int* abortw = nullptr /* k_ruiz_loop's abort word: set -> ruiz_sweeps = -2 */);
 // Every sweep in one persistent launch of nwg workgroups (k_ruiz.hip), then dfin and ruiz_sweeps: the same d, rho
@@ -151,6 +156,14 @@ void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double*
 // k_dataflow.hip: the whole factorization (potrf + trsm + updates + fused forward solve) as one persistent
 // launch over the 64x64 tile DAG in the host-built task order (build_chol_schedule in cvxg.cpp)
 size_t chol_dataflow_work_ints(int nblk);
+// Linv buffer of the dataflow Cholesky: the nblk diagonal-block inverses L_kk^-1 (64 x 64 each, what the solves read),
+// then per block the chain's forward-substitution package (DF_PKG doubles: L rows 48..63 left of the last 16-column
+// block [0, 768); that block's L~16^-T and its column scales as 272 data-tagged 16-B granules [768, 1312);
+// k_dataflow.hip)
+constexpr int DF_PKG = 1344;
+__host__ __device__ constexpr size_t chol_dataflow_linv_doubles(int nblk) {
+  return (size_t)nblk * NB * NB + (size_t)nblk * DF_PKG;
+}
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */,
@@ -162,6 +175,7 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                                                     (a short Ruiz lookahead, cvxg.cpp: factor_attempt) */,
                           double early_min = 0.0 /* > 0: stop (abort word, min_diag and small_piv set) at the first
                                                     16-column block whose min diag(L) <= early_min */);
+// (every launch tags its package granules with a generation of its own: a process-wide launch counter)
 // (the chain workgroups apply panel b-2 to block row b themselves: UPDATE(b,b,b-2), UPDATE(b,b-1,b-2) are not in
 // `tasks`, which chol_schedule builds accordingly)
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)

@@ -247,9 +247,12 @@ def make_whole(threads=6):
             first["it_n"].append(rc.it_n)
             first["x"].append(rc.x.copy())
             first["dx"].append(rc.dx.copy())
-        if rc.it_n % 50 == 0:
+        if rc.it_n % 25 == 0:
             print(f"C3WHOLE: t={cur['t']:g} it={rc.it_n} q={rc.q:.3e} step={rc.step:g} reg={rc.regularized} "
                   f"({time.time() - t0:.0f} s)", flush=True)
+        if rc.it_n % 25 == 24:  # a centering in progress: its steps so far, readable if the run is stopped
+            np.savez_compressed(path.replace(".npz", "_inprogress.npz"), t=np.array(cur["t"]), x_start=x_start[-1],
+                                **{("step_" + k): np.array(v) for k, v in steps.items()})
 
     x = spec["x0"].copy()
     t = 1.0
