@@ -157,10 +157,10 @@ void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double*
 // launch over the 64x64 tile DAG in the host-built task order (build_chol_schedule in cvxg.cpp)
 size_t chol_dataflow_work_ints(int nblk);
 // Linv buffer of the dataflow Cholesky: the nblk diagonal-block inverses L_kk^-1 (64 x 64 each, what the solves read),
-// then per block the chain's forward-substitution package (DF_PKG doubles: L rows 48..63 left of the last 16-column
-// block [0, 768); that block's L~16^-T and its column scales as 272 data-tagged 16-B granules [768, 1312);
-// k_dataflow.hip)
-constexpr int DF_PKG = 1344;
+// then per block the chain's forward-substitution packages 0..3 as 2 624 data-tagged 16-B granules {value, tag}
+// (DF_PKG doubles): package cb = L_kk row-block cb left of its diagonal block (16 x 16 cb), step cb's L~16^-T (16 x 16)
+// and column scales (16); k_dataflow.hip, potrf64w.hpp)
+constexpr int DF_PKG = 2 * 2624;
 __host__ __device__ constexpr size_t chol_dataflow_linv_doubles(int nblk) {
   return (size_t)nblk * NB * NB + (size_t)nblk * DF_PKG;
 }

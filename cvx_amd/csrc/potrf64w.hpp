@@ -274,15 +274,14 @@ __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int
 // stored to rhs block k); Linv[k] = L^-1 is stored row-block by row-block as it becomes final (wave 3), and *lflag
 // (when given) counts the stored row-blocks (sc1 hand-off: the stores drained first).  fix() runs on all threads
 // between the factorization and the forward solve (barrier behind it).  L_kk is not stored (potrf64w_store_L).  With
-// pkg (DF_PKG doubles) the chain's forward-substitution package is stored as its pieces become final: the L rows 48..63
-// left of the last block ([0, 768) row-major, then the flag pkgf[0]) and that block's L~16^-T and column scales (272
-// granules {value, pkg_tag} from 768 on); k_dataflow.hip's last TRSM slice of the next block reads them.
+// pkg (DF_PKG doubles) the chain's forward-substitution packages 0..3 are stored as granules as each becomes final (at
+// the start of step kb's phase A, by wave 1 + kb % 2); k_dataflow.hip's slices of the next block read them.
 template <class M, class Fix = NoFix, class Pre = NoPre>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
                                                 Fix fix = Fix(), double early_min = 0.0, Pre pre = Pre(),
                                                 unsigned long long* rb_stamp = nullptr, bool wait_d = false,
-                                                double* pkg = nullptr, int* pkgf = nullptr, double pkg_tag = 0.0) {
+                                                double* pkg = nullptr, unsigned long long pkg_tag = 0) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -300,18 +299,6 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) p64w_publish(&sm.fP, kb + 1);
-      if (kb == 3 && pkg) {
-        // the package's second part the moment the last sweep ends: L~16^-T of the last 16-column block (ET[3],
-        // granule 16 r + c) and its column scales (SV[3], granules 256 + c) -- wave 0 wrote both itself -- as 272
-        // data-tagged 16-B granules {value, tag} (one sc1 store each, no drain, no flag: the consumer polls them)
-        const M mP(pkg, (unsigned)DF_PKG * 8u);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = lane + 64 * q;
-          mP.st2(768 + 2 * e, f64x2{sm.ET[3][(e >> 4) * P64_EP + (e & 15)], pkg_tag});
-        }
-        if (lane < 16) mP.st2(768 + 2 * (256 + lane), f64x2{sm.SV[3][lane], pkg_tag});
-      }
       if (kb < 3) {
         // (wait_d: the caller entered without a barrier behind the staged tile; wave 0 factored its own block D_00
         // and waits here for waves 1..3's blocks before the first T / U)
@@ -338,6 +325,21 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       if (!ok) break;
       P64_STAMP(1 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (pkg && w == 1 + (kb & 1)) {
+        // package kb (k_dataflow.hip's slice kb of the next block), final now: L row-block kb left of its diagonal
+        // block (the T steps < kb: phase B of step kb - 1 waited for them), and sweep kb's L~16^-T and scales (fP) --
+        // 256 kb + 272 data-tagged 16-B granules {value, pkg_tag | kb}, one sc1 store each, no drain, no flag
+        const M mP(pkg, (unsigned)DF_PKG * 8u);
+        const int g0 = 128 * kb * (kb - 1) + 272 * kb, nl = 256 * kb, nc = 16 * kb;
+        const double tag = __longlong_as_double((long long)(pkg_tag | (unsigned)kb));
+        for (int e = lane; e < nl + 272; e += 64) {
+          double v;
+          if (e < nl) v = sm.S[(16 * kb + e / nc) * P64_SP + e % nc];
+          else if (e < nl + 256) v = sm.ET[kb][((e - nl) >> 4) * P64_EP + ((e - nl) & 15)];
+          else v = sm.SV[kb][e - nl - 256];
+          mP.st2(2 * (g0 + e), f64x2{v, tag});
+        }
+      }
       p64w_phaseA(sm, kb, w, lane);
       P64_STAMP(2 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -362,19 +364,6 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       if (kb < 3) {
         ok = p64w_wait(sm, &sm.fT, kb + 1) && p64w_wait(sm, &sm.cntT[kb], 3);
         if (!ok) break;
-        if (kb == 2 && pkg && w == 3) {
-          // the package's first part (sc1 hand-off, pkgf[0]): L rows 48..63 left of the last 16-column block, final
-          // once wave 0's T(3, 2) is (fT == 3; T(3, 0) and T(3, 1) came with steps 0 and 1's phase A)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          const M mP(pkg, (unsigned)DF_PKG * 8u);
-#pragma unroll
-          for (int q = 0; q < 6; ++q) {
-            const int e = lane + 64 * q, r = e / 24, c = 2 * (e % 24);
-            mP.st2(48 * r + c, *reinterpret_cast<const f64x2*>(sm.S + (48 + r) * P64_SP + c));
-          }
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == 0) __hip_atomic_store(pkgf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
         P64_STAMP(3 + 4 * kb);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         p64w_phaseB(sm, kb, w, lane);

@@ -21,7 +21,9 @@ for k in range(2,nb-2):
     rows.append([us(B-A),us(stg0-A),us(C-A),us(s2-A) if s2>A else np.nan,us(D-A) if D>A else np.nan,us(E-A),us(F-A),us(fix0-F) if fix0>0 else 0, us(fix1-F) if fix1>0 else 0,us(fix2-F) if fix2>0 else 0,
                  us(b2in-A) if b2in>0 else np.nan, us(b2done-A) if b2done>0 else np.nan]+[us(v-A) if v>0 else np.nan for v in rbp]+[us(v-A) if v>0 else np.nan for v in bat])
 r=np.array(rows)
-names=['potrf_done','stage_begin(k+1)','staged(k+1)','slice2done(k+1)','lastrow(k+1)','slices_done(k+1)','potrf_start(k+1)','fix0(k+1)-F','fix1-F','fix2-F','b2_inputs(k+1)','b2_applied(k+1)','rb0_flag(k)','rb1_flag(k)','rb2_flag(k)','rb3_flag(k)','batch_loaded(k+1)','batch_trsm(k+1)','batch_upd(k+1)']
+# (round 6: record 4 = the forward-substitution slices: packages 0..2 in LDS, slice 0 done, slice 1 done; 'lastrow' =
+# package 3 in LDS)
+names=['potrf_done','stage_begin(k+1)','staged(k+1)','slice2done(k+1)','pkg3_in(k+1)','slices_done(k+1)','potrf_start(k+1)','fix0(k+1)-F','fix1-F','fix2-F','b2_inputs(k+1)','b2_applied(k+1)','rb0_flag(k)','rb1_flag(k)','rb2_flag(k)','rb3_flag(k)','pkg012_in(k+1)','slice0_done(k+1)','slice1_done(k+1)']
 for i,nm in enumerate(names):
     print(f"{nm:22s} mean {np.nanmean(r[:,i]):7.2f} med {np.nanmedian(r[:,i]):7.2f} min {np.nanmin(r[:,i]):7.2f} max {np.nanmax(r[:,i]):7.2f}")
 order=np.frombuffer(raw[8:8+4*nq],dtype=np.uint32)
