@@ -164,8 +164,8 @@ def cpu_baseline_blas(spec, steps: int = 3):
 
 
 def latest_profile(name):
-    """The newest committed profile file of that name (profiles/r05, then r04, r03, r02)."""
-    for r in ("r05", "r04", "r03", "r02"):
+    """The newest committed profile file of that name (profiles/r06, then r05, r04, r03, r02)."""
+    for r in ("r06", "r05", "r04", "r03", "r02"):
         p = os.path.join(ROOT, "profiles", r, name)
         if os.path.exists(p):
             return p
@@ -175,7 +175,7 @@ def latest_profile(name):
 PMC_TRAFFIC = latest_profile("pmc_traffic.json")
 # the same rooflines recomputed from the committed rocprofv3 kernel trace of `bench.py --steps 20 --warmup 5
 # --no-cpu-baseline` (scripts/trace_roofline.py: sums of kernel durations over the timed steps)
-TRACE_ROOFLINE = os.path.join(ROOT, "profiles", "r05", "trace_roofline.json")
+TRACE_ROOFLINE = latest_profile("trace_roofline.json")
 
 
 def trace_roofline():

@@ -86,7 +86,6 @@ struct cvxg_ctx {
   // matrices
   double *H = nullptr, *L = nullptr, *Linv = nullptr, *Hsave = nullptr;
   double *ruiz0 = nullptr, *ruiz1 = nullptr, *dfin = nullptr, *hdiag = nullptr;
-  double* ruiz_S1 = nullptr;  // Ruiz partials of the odd sweeps (ctx->part holds the even ones)
   double *rhs = nullptr, *sol = nullptr;
   double* part = nullptr;
   size_t part_bytes = 0;
@@ -117,7 +116,7 @@ struct cvxg_ctx {
   bool h_full = true;           // the current H holds its upper triangle too
   double* hsv_part = nullptr;   // symv partials (nblk x np)
   // Ruiz: every sweep in one persistent launch (k_ruiz.hip; CVXG_OPT_RUIZ_LOOP; 0: two launches per sweep)
-  int ruiz_loop = 0;            // (opt-in until it beats the multi-launch form: DESIGN.md §7)
+  int ruiz_loop = 0;            // (the default up to RUIZ_LOOP_MAX_BLOCKS blocks, cvxg_create)
   unsigned long long* ruiz_trace = nullptr;  // CVXG_RUIZ_TRACE=<file>: per-workgroup sweep stamps of the last loop
   std::string ruiz_trace_path;
   int ruiz_wg = 0;              // its workgroups (0: one per CU; CVXG_OPT_RUIZ_WG, tests: fewer -> streamed tiles)
@@ -543,6 +542,8 @@ extern "C" int cvxg_set_ruiz_lookahead(cvxg_ctx* ctx, int sweeps, long long* rel
   return CVXG_OK;
 }
 
+constexpr int RUIZ_LOOP_MAX_BLOCKS = 16;  // the one-launch Ruiz loop is the default up to this many 64-row blocks
+
 // The one-launch Ruiz loop's buffers (and, with CVXG_RUIZ_TRACE, its stamp buffer for every CU), on first use.
 static int ruiz_loop_alloc(cvxg_ctx* ctx) {
   if (!ctx->ruiz_S) {
@@ -837,10 +838,13 @@ static void ruiz_sweeps(cvxg_ctx* ctx, int k0, int k1) {
     return;
   }
   if (k0 == 0) launch_ruiz_init(s, ctx->ruiz0, ctx->np, ctx->ctrl);
-  // one launch per sweep (k_ruiz_tiles_f: each sweep forms the previous one's d itself) and one row pass for the last
-  double* const dd[2] = {ctx->ruiz0, ctx->ruiz1};
-  double* const SS[2] = {ctx->part, ctx->ruiz_S1};
-  launch_ruiz_sweeps_fused(s, ctx->H, ctx->np, ctx->n, ctx->np, dd, SS, ctx->ctrl, k0, k1);
+  // (one launch per sweep, each forming the previous sweep's d from its partials, was measured in round 6: 0.463 vs
+  // 0.235 ms per Ruiz at C3 -- the partials re-read per tile cost more than the row-pass launch it saves)
+  for (int k = k0; k < k1; ++k) {
+    const double* dc = (k & 1) ? ctx->ruiz1 : ctx->ruiz0;
+    double* dn = (k & 1) ? ctx->ruiz0 : ctx->ruiz1;
+    launch_ruiz_sweep_tri(s, ctx->H, ctx->np, ctx->n, ctx->np, dc, dn, ctx->part, ctx->ctrl, k);
+  }
   launch_ruiz_final(s, ctx->ruiz0, ctx->ruiz1, ctx->np, ctx->dfin, ctx->ctrl, k1);
 }
 static void ruiz(cvxg_ctx* ctx) {
@@ -1904,8 +1908,14 @@ int cvxg_create(int device, int n, int m, int p, cvxg_ctx** out) {
     part = std::max(part, (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE);
   CHK(dalloc(ctx, &ctx->part, part));
   CHK(dalloc(ctx, &ctx->hsv_part, (size_t)ctx->nblk * np));
-  CHK(dalloc(ctx, &ctx->ruiz_S1, (size_t)ctx->nblk * np));
   if (const char* e = getenv("CVXG_RUIZ_TRACE")) ctx->ruiz_trace_path = e;  // instrumentation only (the loop's stamps)
+  // Ruiz by size (round 6): up to 16 blocks (n <= 1024, the triangle <= 4 MB) the one-launch loop
+  // beats the launch pairs -- C2 0.105 vs 0.113 ms, C4 0.131 vs 0.141 ms per Ruiz, the same bits
+  // (profiles/r06/workloads/ruiz_C*.json) -- and at C3 it loses (0.36-0.40 vs 0.245 ms, round 5)
+  if (ctx->nblk <= RUIZ_LOOP_MAX_BLOCKS && ruiz_loop_fits(ctx->nblk)) {
+    CHK(ruiz_loop_alloc(ctx));
+    ctx->ruiz_loop = 1;
+  }
   CHK(dalloc(ctx, &ctx->spart,
              ctx->nsplit > 1 ? (size_t)ctx->nsplit * (ctx->ntiles - ctx->ntiles_main) * TILE * TILE : (size_t)1));
   HIPC(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
@@ -1942,7 +1952,7 @@ void cvxg_destroy(cvxg_ctx* ctx) {
   void* ptrs[] = {ctx->P, ctx->a0, ctx->A, ctx->r, ctx->ub, ctx->Aeq, ctx->beq, ctx->x, ctx->y, ctx->dx, ctx->sdir,
                   ctx->xtmp, ctx->vtmp, ctx->Px, ctx->Ps, ctx->e, ctx->c, ctx->d, ctx->invd, ctx->w, ctx->logd,
                   ctx->eqd, ctx->eqtmp, ctx->H, ctx->L, ctx->Linv, ctx->Hsave, ctx->ruiz0, ctx->ruiz1, ctx->dfin,
-                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->ruiz_S1, ctx->ruiz_S, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
+                  ctx->hdiag, ctx->rhs, ctx->sol, ctx->part, ctx->hsv_part, ctx->ruiz_S, ctx->kB, ctx->kw, ctx->kx, ctx->kz, ctx->ls_plog,
                   ctx->ls_log, ctx->ls_pcnt, ctx->tiles, ctx->ctrl, ctx->df_tasks, ctx->df_work, ctx->df_trace, ctx->bwd_flags,
                   ctx->eig_M, ctx->eig_K, ctx->eig_d, ctx->eig_e, ctx->eig_dots, ctx->eig_a, ctx->eig_z,
                   ctx->eig_b, ctx->eig_x, ctx->eig_part, ctx->eig_info, ctx->KB, ctx->kl_v, ctx->kl_y, ctx->kl_u,

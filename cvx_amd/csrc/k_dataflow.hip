@@ -16,8 +16,6 @@
 // handed-off bytes is an sc1 access (relaxed agent-scope atomics), each storing wave drains with
 // s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane stores the state word; the consumer polls the
 // word with sc1 loads, then a workgroup barrier, then sc1 loads of the data.  One workgroup per CU.
-#include <atomic>
-
 #include "potrf64w.hpp"
 
 namespace cvxg {
@@ -30,6 +28,7 @@ constexpr int DF_SMEM = 4 * NB * (NB + 2) + 2 * 16 * (NB + 2) + 512;  // doubles
 struct ChainSmem {
   Potrf64wSmem p;
   double Sa[NB * (NB + 2)];       // A_b,b-1 during the TRSM slices, then L_b,b-1 (for the last rhs correction)
+  double E2[2][16 * (NB + 2)];    // double-buffered row-blocks of L_b-1,b-1^-1
   double V[NB * MAX_RHS];
   int lpub;                       // waves of POTRF(b) done storing L_b,b-1 (deferred publication)
 };
@@ -181,6 +180,33 @@ __device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, cons
   for (int p = 0; p < NB / 8; ++p) {
     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
     if (p + 1 < NB / 8) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+  }
+}
+
+// df_mfma over the k-steps [32 H, 32 H + 32) only (H = 0, 1): the two halves in order are df_mfma's sum, bit for bit
+template <int H>
+__device__ __forceinline__ void df_mfma_half(d4f (&acc)[2][2], const double* Pi, const double* Pj, double sgn, int wr,
+                                             int wc, int lane) {
+#pragma unroll
+  for (int s = 8 * H; s < 8 * H + 8; ++s) {
+    const int kk = 4 * s + (lane >> 4);
+    double fa[2], fb[2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) fa[mi] = sgn * Pi[(wr * 32 + mi * 16 + (lane & 15)) * DF_SP + kk];
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) fb[nj] = Pj[(wc * 32 + nj * 16 + (lane & 15)) * DF_SP + kk];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+        acc[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi], fb[nj], acc[mi][nj], 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+  for (int p = 0; p < NB / 16; ++p) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    if (p + 1 < NB / 16) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
   }
 }
@@ -405,8 +431,24 @@ __device__ bool df_trsm(double* __restrict__ L, int ld, int i, int k, double* __
   return true;
 }
 
-// ---- chain slices (ping-pong consumer below): every slice's MFMA operands are read from LDS in one batch, then the
-// MFMAs go back to back -- one wave per SIMD cannot hide an LDS round trip behind another wave.
+// ---- chain slices (ping-pong consumer below): operands read from LDS in one batch, then the MFMAs back to back.
+// One wave per SIMD cannot hide an LDS round trip behind another wave, so interleaving reads and MFMAs costs a round
+// trip per MFMA pair (microbench/slices.hip: 4650 -> 2840 cycles per slice).
+// TRSM slice CB: L'[16 w.., 16 CB..] = A[16 w.., :] L^-1[16 CB.., :]^T (K = 16 (CB + 1): L^-1 is lower); af = the
+// wave's row-block of A as MFMA A-fragments (loaded once per block), E = row-block CB of L^-1 (row stride DF_SP).
+template <int CB>
+__device__ __forceinline__ d4f ch_trsm(const double (&af)[16], const double* E, int lane) {
+  double xf[4 * (CB + 1)];
+#pragma unroll
+  for (int s = 0; s < 4 * (CB + 1); ++s) xf[s] = E[(lane & 15) * DF_SP + 4 * s + (lane >> 4)];
+  d4f acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4 * (CB + 1); s += 2) {
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s], xf[s], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s + 1], xf[s + 1], acc1, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
 // the 10 lower 16 x 16 blocks of a 64 x 64 tile, 3 / 3 / 2 / 2 per wave (-1: none)
 // (wave 0 holds only D_00, which POTRF's first sweep reads: with a deferred publication it goes from its last slice
 // straight into the sweep while waves 1..3 finish and store the other nine blocks, ps.cntD)
@@ -445,14 +487,15 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
                                                           int* __restrict__ work, const unsigned* __restrict__ tasks,
                                                           int ntasks, int nblk, unsigned long long* __restrict__ trace,
                                                           const double* __restrict__ Hq, const double* __restrict__ dq,
-                                                          int nq, int ruiz_gate, double early_min,
-                                                          unsigned long long gen) {
+                                                          int nq, int ruiz_gate, double early_min) {
   // the Ruiz loop launched ahead of the factorization without a host read may still be open (k_ruiz_final: -1): then
   // the launch is void and the host finishes the loop and factors again
   if (ruiz_gate && ctrl->ruiz_sweeps < 0) return;
   __shared__ __attribute__((aligned(16))) double smem[DF_SMEM];
   __shared__ unsigned s_task;
   __shared__ int s_ok;
+  __shared__ int s_next;
+  __shared__ int s_kj;  // the chain: L_k,k-2 already published when L_b,k-2 came in
   int* counter = work;
   int* abortw = work + 32;  // own cache line: the claim counter's line takes every worker's atomic
   int* state = work + 64;  // own cache lines
@@ -492,8 +535,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
       return s_ok;
     };
     constexpr int NBLK16 = 3;  // (kChIB / kChJB: this wave's lower 16 x 16 blocks)
-    // the tag of POTRF(kk)'s package granules in this launch (| the package index 0..3)
-    auto pkg_tag = [&](int kk) { return (gen << 12) | ((unsigned long long)kk << 2); };
     for (int b = role; b < nblk; b += 2) {
       if (b == 0) {
         if (qf.H) {
@@ -513,6 +554,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         const int k = b - 1;
         mark(k, 1, 0);
         const Sc1Mem mA(L + (size_t)b * NB * ld + (size_t)k * NB, tile_bytes(ld));
+        const Sc1Mem mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);
+        // the row-blocks of L_kk^-1 already published (cflag, read while the tile loads are in flight) are loaded
+        // at once into ps.S (free until the diagonal tile goes there at the end of the slices) and applied as one
+        // batch below
+        int pv = 0;
         d4f dacc[NBLK16];
         if (b >= 2) {
           // Panel j = b-2 of block row b on this workgroup (the tasks UPDATE(b,b,j) and UPDATE(b,k,j), not in the
@@ -548,23 +594,27 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               }
             }
           }
-          // (2) L_b,j (worker TRSM(b,j)) and L_k,j (the other chain workgroup's TRSM, published inside its POTRF(k));
-          // the rhs block is read in POTRF(b)'s fix hook, which it first feeds
+          // (2) L_b,j (worker TRSM(b,j), published before its rhs update) and L_k,j (the other chain workgroup's TRSM,
+          // published inside its POTRF(k), usually later): D_b -= L_b,j L_b,j^T needs only the first, so it runs as
+          // soon as that tile is in, with L_k,j's loads in flight beside it when it is out too (round 6); the rhs
+          // block is read in POTRF(b)'s fix hook, which it first feeds
           if (tid == 0) {
             const int v3 = df_poll(state + df_tri(b, j)), v4 = df_poll(state + df_tri(k, j));
-            s_ok = (v3 >= j + 1 || df_wait(state, df_tri(b, j), j + 1, abortw, ctrl)) &&
-                   (v4 >= j + 1 || df_wait(state, df_tri(k, j), j + 1, abortw, ctrl));
+            s_ok = v3 >= j + 1 || df_wait(state, df_tri(b, j), j + 1, abortw, ctrl);
+            s_kj = v4 >= j + 1;
           }
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           __syncthreads();
           if (!s_ok) return;
-          mark(k, 2, 3);  // trace: the b-2 panel's inputs are in (field 3 of the fix record)
+          mark(k, 2, 3);  // trace: the b-2 panel's first input is in (field 3 of the fix record)
+          const bool kj_in = s_kj;
           {
             f64x2 vl[NB * NB / 512], vk[NB * NB / 512];
             df_load(vl, Sc1Mem(L + (size_t)b * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
-            df_load(vk, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
+            // (both tiles' loads in flight together; L_k,j's from a clamped descriptor when it is not out, unused then)
+            df_load(vk, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, kj_in ? tile_bytes(ld) : 0u), ld);
             df_put(ps.X, vl);  // (POTRF's L^-1 workspace and tile: free until the reset / the batch below)
-            df_put(ps.S, vk);
+            if (kj_in) df_put(ps.S, vk);
           }
           __syncthreads();
           for (int cb = 0; cb < 4; ++cb) {
@@ -575,7 +625,23 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               default: ch_update<3>(dacc, ps.X, cb, lane); break;
             }
           }
-          df_mfma(acc, ps.X, ps.S, -1.0, wr, wc, lane);  // A_b,k -= L_b,j L_k,j^T
+          if (!kj_in) {  // L_k,j was not out yet: wait for it now
+            if (!wait(state, df_tri(k, j), j + 1)) return;
+            df_stage(ps.S, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
+            __syncthreads();
+          }
+          // the row-blocks of L_kk^-1 published so far: polled between the MFMA phases and read behind them, so the
+          // batch below knows its size the moment this panel is applied (round 6: no poll round trip behind the
+          // MFMAs; the value is at most one MFMA phase old)
+          int pf = 0;
+          if (tid == 0) pf = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          df_mfma_half<0>(acc, ps.X, ps.S, -1.0, wr, wc, lane);  // A_b,k -= L_b,j L_k,j^T, k-steps 0..31
+          if (tid == 0) {
+            pv = pf;
+            pf = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          df_mfma_half<1>(acc, ps.X, ps.S, -1.0, wr, wc, lane);  // k-steps 32..63
+          if (tid == 0) pv = max(pv, pf);
 #pragma unroll
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -613,108 +679,134 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               }
             }
           }
+          if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           df_put(cs.Sa, va);
         }
         }
-        // TRSM(b, k) and UPDATE(b, b, k) by forward substitution, one 16-column slice per step of POTRF(k) (round 6):
-        //   L'[:, cb] = (A[:, cb] - sum_{m < cb} L'[:, m] L_kk[cb, m]^T) L~16_cb^-T diag(s_cb),  D -= L'[:, cb] L'[:, cb]^T,
-        // what POTRF(k)'s own T steps compute for its rows (p64w_T).  The inputs of slice cb are POTRF(k)'s package cb:
-        // L_kk row-block cb left of its diagonal block, final before step cb, and step cb's L~16^-T and scales, final
-        // the moment sweep cb ends -- stored by one of POTRF(k)'s waves 1..3 as data-tagged granules (potrf64w_factor,
-        // pkg): one round trip from publication to use, no flag, no drain, and no wait for L_kk^-1, whose row-blocks
-        // come a phase A, their stores and a drain later (the workers' TRSMs still use those).  Packages 0..2 land
-        // together behind the panel-(b-2) work; package 3 is in flight while slices 0..2 run.
-        const Sc1Mem mP(Linv + (size_t)nblk * NB * NB + (size_t)k * DF_PKG, (unsigned)DF_PKG * 8u);
-        const unsigned long long tagk = pkg_tag(k);
-        constexpr int G3 = 1584, NG012 = (G3 + 255) / 256, NG3 = (1040 + 255) / 256;  // granules of packages 0..2, 3
-        f64x2 ga[NG012], gb[NG3];
-        auto gput = [&](int gi, double v) {  // granule gi of the package -> its place in LDS
-          int cb = 0, g0 = 0;
+        if (tid == 0) s_next = pv;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        const int nbat = min(s_next, 4);
+        {
+          f64x2 vb[8];
 #pragma unroll
-          for (int c = 1; c < 4; ++c)
-            if (gi >= 128 * c * (c - 1) + 272 * c) {
-              cb = c;
-              g0 = 128 * c * (c - 1) + 272 * c;
-            }
-          const int e = gi - g0, nl = 256 * cb;
-          if (e < nl) ps.X[(16 * cb + e / (16 * cb)) * P64_SP + e % (16 * cb)] = v;  // L_kk[cb, 0..cb) -> X lower blocks
-          else if (e < nl + 256) ps.ET[cb][((e - nl) >> 4) * P64_EP + ((e - nl) & 15)] = v;
-          else ps.SV[cb][e - nl - 256] = v;
-        };
-        // every thread until its granules [g0, g1) carry this launch's tag (bounded; the abort word every 16th spin),
-        // then into LDS; false: the launch aborted
-        auto gland = [&](f64x2* gv, int ng, int g0, int g1) -> bool {
-          const unsigned long long t0 = spin_clock();
-          for (unsigned spins = 0;; ++spins) {
-            bool all = true;
-            for (int i = 0; i < ng; ++i) {
-              const int gi = g0 + tid + 256 * i;
-              if (gi < g1 && (unsigned long long)__double_as_longlong(gv[i][1]) != (tagk | (unsigned)(gi >= G3 ? 3 : gi >= 800 ? 2 : gi >= 272 ? 1 : 0))) {
-                all = false;
-                gv[i] = mP.ld2(2 * gi);
-              }
-            }
-            if (all) break;
-            if ((spins & 15) == 15 && df_poll(abortw)) return false;
-            if (spin_expired(spins, t0)) {
-              __hip_atomic_store(abortw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              atomicExch(&ctrl->df_status, 2);
-              return false;
-            }
-            __builtin_amdgcn_s_sleep(1);
+          for (int q = 0; q < 8; ++q) {
+            const int e = tid + 256 * q;
+            if (q < 2 * nbat) vb[q] = mI.ld2((e >> 5) * NB + 2 * (e & 31));
           }
-          for (int i = 0; i < ng; ++i) {
-            const int gi = g0 + tid + 256 * i;
-            if (gi < g1) gput(gi, gv[i][0]);
-          }
-          return true;
-        };
 #pragma unroll
-        for (int i = 0; i < NG012; ++i)
-          if (tid + 256 * i < G3) ga[i] = mP.ld2(2 * (tid + 256 * i));
-        __syncthreads();  // the panel's MFMAs are done with ps.X / ps.S
+          for (int q = 0; q < 8; ++q) {
+            const int e = tid + 256 * q;
+            if (q < 2 * nbat) *reinterpret_cast<f64x2*>(ps.S + (e >> 5) * P64_SP + 2 * (e & 31)) = vb[q];
+          }
+        }
         potrf64w_reset(ps);  // the slices leave POTRF's L^-1 workspace and flags alone: clear them off the chain
         if (tid == 0) cs.lpub = 0;  // (POTRF(b-2)'s pre hook is long done; the barrier below orders it)
         mark(k, 1, 1);
-        // L_b,k, row stride DF_SP: written over A_b,k in Sa slice by slice, where it stays for the rhs correction at
-        // the end of POTRF(b) -- no copy before POTRF
+        // L_b,k, row stride DF_SP: written over A_b,k in Sa (every wave holds its row-block of A in af before the first
+        // slice's barrier), where it stays for the rhs correction at the end of POTRF(b) — no copy before POTRF
         double* Lp = cs.Sa;
-        if (tid == 0) s_ok = 1;
-        __syncthreads();  // (the reset's zeros stay off the package's X lower blocks)
-        if (!gland(ga, NG012, 0, G3)) s_ok = 0;
+        // row-block cb of L_kk^-1 (published by the other workgroup's POTRF(k) as cflag[k] reaches cb + 1) is
+        // loaded into registers one slice ahead when it is already published, so its latency hides behind the
+        // MFMAs of the current slice
+        f64x2 er[2];
+        auto eload = [&](int cb) {
 #pragma unroll
-        for (int i = 0; i < NG3; ++i)  // package 3, in flight during slices 0..2
-          if (tid + 256 * i < 1040) gb[i] = mP.ld2(2 * (G3 + tid + 256 * i));
-        __syncthreads();
-        if (!s_ok) return;
-        mark(k, 4, 0);  // trace: packages 0..2 in LDS
+          for (int q = 0; q < 2; ++q) {
+            const int e = tid + 256 * q;
+            er[q] = mI.ld2((16 * cb + (e >> 5)) * NB + 2 * (e & 31));
+          }
+        };
+        __syncthreads();  // Sa and the batch's row-blocks in ps.S complete
+        mark(k, 4, 0);    // trace: every wave's staging loads landed (record 4: the batch's phases)
+        bool pre = false;  // row-block nbat already loaded into er behind the batch
+        double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments
+#pragma unroll
+        for (int q = 0; q < 16; ++q) af[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
+        if (nbat > 0) {
+          // the batch: the same MFMA sequence per output as the per-slice form below, so the same bits
+          // the next row-block: polled now, loaded behind the batch's diagonal updates when it is out (round 6)
+          int pb = 0;
+          if (nbat < 4 && tid == 0) pb = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          d4f acc[4];
+          acc[0] = ch_trsm<0>(af, ps.S, lane);
+          if (nbat > 1) acc[1] = ch_trsm<1>(af, ps.S + 16 * P64_SP, lane);
+          if (nbat > 2) acc[2] = ch_trsm<2>(af, ps.S + 32 * P64_SP, lane);
+          if (nbat > 3) acc[3] = ch_trsm<3>(af, ps.S + 48 * P64_SP, lane);
+          __syncthreads();  // every wave holds its fragments of A (Sa takes L')
+          mark(k, 4, 1);
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb)
+            if (cb < nbat)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
+                Lp[row * DF_SP + col] = acc[cb][r];
+              }
+          if (tid == 0) s_next = pb;
+          __syncthreads();
+          if (nbat < 4 && s_next >= nbat + 1) {
+            eload(nbat);
+            pre = true;
+          }
+          for (int cb = 0; cb < nbat; ++cb) {
+            switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
+              case 0: ch_update<0>(dacc, Lp, cb, lane); break;
+              case 1: ch_update<1>(dacc, Lp, cb, lane); break;
+              case 2: ch_update<2>(dacc, Lp, cb, lane); break;
+              default: ch_update<3>(dacc, Lp, cb, lane); break;
+            }
+          }
+          mark(k, 4, 2);
+        }
+        if (nbat < 4 && !pre) {
+          if (!wait(cflag, k, nbat + 1)) return;
+          eload(nbat);
+        }
+        bool have_next = nbat < 4;
 #pragma unroll 1
-        for (int cb = 0; cb < 4; ++cb) {
-          if (cb == 3) {
-            mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
-            if (!gland(gb, NG3, G3, G3 + 1040)) s_ok = 0;
-            __syncthreads();
-            if (!s_ok) return;
-            mark(k, 1, 3);  // trace: package 3 in LDS (was: last row-block of L_kk^-1 in hand)
+        for (int cb = nbat; cb < 4; ++cb) {
+          double* E = cs.E2[cb & 1];
+          if (cb == 3) mark(k + 1, 0, 1);  // trace: slice 2 done (field 1 of the next POTRF record)
+          if (!have_next) {
+            if (!wait(cflag, k, cb + 1)) return;
+            eload(cb);
           }
-          {  // this wave's rows of L'[:, cb]
-            double* C = Lp + 16 * wv * DF_SP + 16 * cb;
-            d4f t = c16_load(C, DF_SP, lane);  // A[16 wv.., 16 cb..] (not yet overwritten)
-            for (int m = 0; m < cb; ++m)
-              t = mfma16_abt(t, Lp + 16 * wv * DF_SP + 16 * m, DF_SP, ps.X + 16 * cb * P64_SP + 16 * m, P64_SP, -1.0, lane);
-            c16_store(C, DF_SP, t, lane);  // (read back right below by this wave only)
-            d4f l = mfma16_ab(d4f{0.0, 0.0, 0.0, 0.0}, C, DF_SP, ps.ET[cb], P64_EP, 1.0, lane);
-            l *= ps.SV[cb][lane & 15];  // the column scales (C layout: column = lane & 15)
-            c16_store(C, DF_SP, l, lane);
+          if (cb == 3) mark(k, 1, 3);  // trace: last row-block of L_kk^-1 in hand
+          // non-blocking look at the next row-block: the sc1 poll is issued here and its value consumed only after
+          // this slice's MFMAs, so its round trip stays off the chain
+          int pollv = 0;
+          if (cb < 3 && tid == 0) pollv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int e = tid + 256 * q;
+            *reinterpret_cast<f64x2*>(E + (e >> 5) * DF_SP + 2 * (e & 31)) = er[q];
           }
-          __syncthreads();  // L'[:, cb] complete
+          __syncthreads();
+          {  // L'[16 wv.., 16 cb..] = A[16 wv.., :] L^-1[16 cb.., :]^T, K = 16 (cb + 1), two MFMA chains
+            d4f acc;
+            switch (cb) {
+              case 0: acc = ch_trsm<0>(af, E, lane); break;
+              case 1: acc = ch_trsm<1>(af, E, lane); break;
+              case 2: acc = ch_trsm<2>(af, E, lane); break;
+              default: acc = ch_trsm<3>(af, E, lane); break;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
+              Lp[row * DF_SP + col] = acc[r];
+            }
+          }
+          if (tid == 0) s_next = (cb < 3) && pollv >= cb + 2;  // own word: read between this barrier and the next
+          __syncthreads();
+          have_next = s_next;
+          if (have_next) eload(cb + 1);  // lands behind the diagonal update below
           switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
             case 0: ch_update<0>(dacc, Lp, cb, lane); break;
             case 1: ch_update<1>(dacc, Lp, cb, lane); break;
             case 2: ch_update<2>(dacc, Lp, cb, lane); break;
             default: ch_update<3>(dacc, Lp, cb, lane); break;
           }
-          if (cb < 3) mark(k, 4, cb < 2 ? cb + 1 : 3);
         }
 #pragma unroll
         for (int q = 0; q < NBLK16; ++q) {
@@ -786,8 +878,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           __hip_atomic_store(state + df_tri(b, k), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       };
       if (!potrf64w_factor<Sc1Mem>(b, rhs, nrhs, Linv, ctrl, ps, cflag + b, fix, early_min, pre,
-                                   trace ? trace + 4 * (size_t)(ntasks + 5 * b + 3) : nullptr, b > 0,
-                                   Linv + (size_t)nblk * NB * NB + (size_t)b * DF_PKG, pkg_tag(b))) {
+                                   trace ? trace + 4 * (size_t)(ntasks + 5 * b + 3) : nullptr, b > 0)) {
         if (tid == 0) __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
@@ -865,11 +956,9 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace, bool zero_work, const double* Hq, const double* dq, int nq,
                           bool ruiz_gate, double early_min) {
-  static std::atomic<unsigned long long> launches{0};  // the generation that tags the package granules (never 0)
-  const unsigned long long gen = launches.fetch_add(1) + 1;
   if (zero_work) (void)hipMemsetAsync(work, 0, chol_dataflow_work_ints(nblk) * sizeof(int), s);
   k_chol_dataflow<<<nwg, 256, 0, s>>>(L, ld, rhs, nrhs, Linv, ctrl, work, tasks, ntasks, nblk, trace, Hq, dq, nq,
-                                      ruiz_gate ? 1 : 0, early_min, gen);
+                                      ruiz_gate ? 1 : 0, early_min);
 }
 
 }  // namespace cvxg

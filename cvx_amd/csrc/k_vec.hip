@@ -667,119 +667,6 @@ void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np
   k_ruiz_rows<<<(np + 63) / 64, 256, 0, s>>>(S, nbn, n, np, dcur, dnext, ctrl, k);
 }
 
-// Sweep k >= 1 in ONE launch (round 6): each tile workgroup (I, J) first forms d_k for its own 64 + 64 rows from sweep
-// k-1's partials Sprev and d_{k-1} -- exactly k_ruiz_rows' arithmetic, its partials added in its order (wave q's four
-// interleaved chains, then the four wave sums) -- and the diagonal tiles (I == J) publish d_k and max |1 - u| into
-// rho[k]; then the tile's partials of sweep k with that d_k, as k_ruiz_tiles.  So d, rho and the sweep count are the
-// bits of the two-launch form, and a sweep costs one launch instead of two (k_ruiz_rows sat at the ~4.5 us launch
-// floor, 13 times a step at C3).  Runs iff sweep k-1 ran (rho[k-1] > 1e-6): it computes d_k whenever the reference
-// does; its own partials are wasted on the last sweep.  Sweep 0 is k_ruiz_tiles with d_0 = 1; the last launched
-// sweep's d / rho come from k_ruiz_rows.
-__global__ __launch_bounds__(256) void k_ruiz_tiles_f(const double* __restrict__ H, int ld, int nbn, int n, int np,
-                                                      const double* __restrict__ dprev, double* __restrict__ dk,
-                                                      const double* __restrict__ Sprev, double* __restrict__ S,
-                                                      DevCtrl* ctrl, int k) {
-  const double rho = __longlong_as_double((long long)ctrl->ruiz_rho[k - 1]);
-  if (!(rho > 1e-6)) return;
-  const int t = blockIdx.x;
-  int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-  while ((I + 1) * (I + 2) / 2 <= t) ++I;
-  while (I * (I + 1) / 2 > t) --I;
-  const int J = t - I * (I + 1) / 2;
-  __shared__ double red[4][2 * NB];
-  __shared__ double dsh[2 * NB];  // d_k of rows I*64.. (0..63) and J*64.. (64..127)
-  __shared__ double cred[8][NB];
-  const int tid = threadIdx.x;
-  const int c2 = tid & 31, g = tid >> 5;
-  const double* tile = H + (size_t)I * NB * ld + (size_t)J * NB;
-  vd2 h[8];  // the tile's loads go out first; the partial sums below run behind them
-#pragma unroll
-  for (int q = 0; q < 8; ++q) h[q] = *reinterpret_cast<const vd2*>(tile + (size_t)(g + 8 * q) * ld + 2 * c2);
-  const int ldS = nbn * NB;
-  const int nr = (I == J) ? NB : 2 * NB;  // rows whose d this workgroup needs
-#pragma unroll
-  for (int rep = 0; rep < 2; ++rep) {  // task (row ri, wave class q): k_ruiz_rows' wave q for that row
-    const int task = tid + 256 * rep, ri = task & (2 * NB - 1), q = task >> 7;
-    const int row = (ri < NB ? I : J) * NB + (ri & (NB - 1));
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    if (ri < nr && row < n) {
-      int X = q;
-      for (; X + 12 < nbn; X += 16) {
-        s0 += Sprev[(size_t)X * ldS + row];
-        s1 += Sprev[(size_t)(X + 4) * ldS + row];
-        s2 += Sprev[(size_t)(X + 8) * ldS + row];
-        s3 += Sprev[(size_t)(X + 12) * ldS + row];
-      }
-      for (; X < nbn; X += 4) s0 += Sprev[(size_t)X * ldS + row];
-    }
-    red[q][ri] = (s0 + s1) + (s2 + s3);
-  }
-  __syncthreads();
-  if (tid < nr) {
-    const int row = (tid < NB ? I : J) * NB + (tid & (NB - 1));
-    double m = 0.0, dn = 1.0;
-    if (row < n) {
-      const double ssum = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
-      const double di = dprev[row];
-      const double u = sqrt(di * sqrt(ssum));        // sqrt(norm(Q(i,::)))   MatrixUtils.scala:258
-      const double v = (u > 0) ? 1.0 / u : 1.0;      // :259
-      dn = di * v;                                   // :260
-      m = fabs(1.0 - u);                             // :261-262
-    }
-    dsh[tid] = dn;
-    if (I == J) {  // (tid < 64: wave 0) the diagonal tile publishes d_k of its rows and their max |1 - u|
-      dk[row] = dn;  // (padded rows: 1, as k_ruiz_rows)
-      m = wave_max(m);
-      if (tid == 0 && m > 0.0) atomic_max_pos(&ctrl->ruiz_rho[k], m);
-    }
-  }
-  if (t == 0)  // rows beyond the tiles (np > 64 nbn): 1, as k_ruiz_rows writes them
-    for (int r = nbn * NB + tid; r < np; r += 256) dk[r] = 1.0;
-  __syncthreads();
-  const double* dI = dsh;
-  const double* dJ = (I == J) ? dsh : dsh + NB;
-  const vd2 dj = *reinterpret_cast<const vd2*>(dJ + 2 * c2);
-  vd2 csum = {0.0, 0.0};
-  double rs[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const double di = dI[g + 8 * q];
-    const vd2 a = dj * h[q];
-    rs[q] = a[0] * a[0] + a[1] * a[1];
-    const vd2 b = h[q] * di;
-    csum = __builtin_elementwise_fma(b, b, csum);
-  }
-  rz_rowgroup_sum8(rs);
-  if (c2 == RZ_ROW_LANE) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) S[(size_t)J * ldS + I * NB + g + 8 * q] = rs[q];
-  }
-  if (I == J) return;
-  cred[g][2 * c2] = csum[0];
-  cred[g][2 * c2 + 1] = csum[1];
-  __syncthreads();
-  if (tid < NB) {
-    double v = cred[0][tid];
-#pragma unroll
-    for (int r = 1; r < 8; ++r) v += cred[r][tid];
-    S[(size_t)I * ldS + J * NB + tid] = v;
-  }
-}
-
-void launch_ruiz_sweeps_fused(hipStream_t s, const double* H, int ld, int n, int np, double* const d[2],
-                              double* const S[2], DevCtrl* ctrl, int k0, int k1) {
-  const int nbn = (n + NB - 1) / NB;
-  const int ntile = nbn * (nbn + 1) / 2;
-  for (int k = k0; k < k1; ++k) {  // d_k in d[k & 1], sweep k's partials in S[k & 1]
-    if (k == 0) k_ruiz_tiles<<<ntile, 256, 0, s>>>(H, ld, nbn, d[0], S[0], ctrl, 0);
-    else
-      k_ruiz_tiles_f<<<ntile, 256, 0, s>>>(H, ld, nbn, n, np, d[(k - 1) & 1], d[k & 1], S[(k - 1) & 1], S[k & 1], ctrl,
-                                           k);
-  }
-  if (k1 > k0)  // d / rho of the last launched sweep (k1 - 1) -> d_k1, rho[k1]
-    k_ruiz_rows<<<(np + 63) / 64, 256, 0, s>>>(S[(k1 - 1) & 1], nbn, n, np, d[(k1 - 1) & 1], d[k1 & 1], ctrl, k1 - 1);
-}
-
 // k1 = the sweeps launched so far.  K = the first k < k1 whose rho[k] <= 1e-6 (sweeps K.. exited), else k1;
 // K == k1 < RUIZ_MAX with rho[k1] > 1e-6 means the loop is not done: ruiz_sweeps = -1 (cvxg.cpp: ruiz_lookahead).
 __global__ void k_ruiz_final(const double* __restrict__ d0, const double* __restrict__ d1, int np,

@@ -81,11 +81,6 @@ void launch_ruiz_init(hipStream_t s, double* d0, int np, DevCtrl* ctrl, double* 
 // The same sweep from the lower triangle only (64 x 64 tiles -> partials S[nbn][nbn*64] -> fixed-order row sums).
 void launch_ruiz_sweep_tri(hipStream_t s, const double* H, int ld, int n, int np, const double* dcur, double* dnext,
                            double* S, DevCtrl* ctrl, int k);
-// Sweeps k0 .. k1-1 with one launch per sweep (k_ruiz_tiles_f) plus one k_ruiz_rows for the last: the same d, rho and
-// sweep count as launch_ruiz_sweep_tri over those sweeps.  d_k lives in d[k & 1]; S[0], S[1] hold alternate sweeps'
-// partials (nbn x nbn*64 each).
-void launch_ruiz_sweeps_fused(hipStream_t s, const double* H, int ld, int n, int np, double* const d[2],
-                              double* const S[2], DevCtrl* ctrl, int k0, int k1);
 void launch_ruiz_final(hipStream_t s, const double* d0, const double* d1, int np, double* dfin, DevCtrl* ctrl, int k1,
                        const int* abortw = nullptr /* k_ruiz_loop's abort word: set -> ruiz_sweeps = -2 */);
 // Every sweep in one persistent launch of nwg workgroups (k_ruiz.hip), then dfin and ruiz_sweeps: the same d, rho
@@ -156,14 +151,8 @@ void launch_syrk_assemble(hipStream_t s, const double* A, int lda, const double*
 // k_dataflow.hip: the whole factorization (potrf + trsm + updates + fused forward solve) as one persistent
 // launch over the 64x64 tile DAG in the host-built task order (build_chol_schedule in cvxg.cpp)
 size_t chol_dataflow_work_ints(int nblk);
-// Linv buffer of the dataflow Cholesky: the nblk diagonal-block inverses L_kk^-1 (64 x 64 each, what the solves read),
-// then per block the chain's forward-substitution packages 0..3 as 2 624 data-tagged 16-B granules {value, tag}
-// (DF_PKG doubles): package cb = L_kk row-block cb left of its diagonal block (16 x 16 cb), step cb's L~16^-T (16 x 16)
-// and column scales (16); k_dataflow.hip, potrf64w.hpp)
-constexpr int DF_PKG = 2 * 2624;
-__host__ __device__ constexpr size_t chol_dataflow_linv_doubles(int nblk) {
-  return (size_t)nblk * NB * NB + (size_t)nblk * DF_PKG;
-}
+// Linv buffer of the dataflow Cholesky: the nblk diagonal-block inverses L_kk^-1 (64 x 64 each)
+__host__ __device__ constexpr size_t chol_dataflow_linv_doubles(int nblk) { return (size_t)nblk * NB * NB; }
 void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrhs, double* Linv, DevCtrl* ctrl,
                           int* work, int nblk, const unsigned* tasks, int ntasks, int nwg,
                           unsigned long long* trace /* nullable: per task {claim, ready, done, wg} (100 MHz) */,
@@ -175,7 +164,6 @@ void launch_chol_dataflow(hipStream_t s, double* L, int ld, double* rhs, int nrh
                                                     (a short Ruiz lookahead, cvxg.cpp: factor_attempt) */,
                           double early_min = 0.0 /* > 0: stop (abort word, min_diag and small_piv set) at the first
                                                     16-column block whose min diag(L) <= early_min */);
-// (every launch tags its package granules with a generation of its own: a process-wide launch counter)
 // (the chain workgroups apply panel b-2 to block row b themselves: UPDATE(b,b,b-2), UPDATE(b,b-1,b-2) are not in
 // `tasks`, which chol_schedule builds accordingly)
 // the whole backward substitution in one launch (flags[nblk], published as flags[b] = gen)

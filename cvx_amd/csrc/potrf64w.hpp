@@ -273,15 +273,12 @@ __device__ __forceinline__ void p64w_phaseB(Potrf64wSmem& sm, int kb, int w, int
 // behind.  On return (uniformly true / false) sm.X = L^-1 (exact zeros above the diagonal), sm.W = w = L^-1 b (also
 // stored to rhs block k); Linv[k] = L^-1 is stored row-block by row-block as it becomes final (wave 3), and *lflag
 // (when given) counts the stored row-blocks (sc1 hand-off: the stores drained first).  fix() runs on all threads
-// between the factorization and the forward solve (barrier behind it).  L_kk is not stored (potrf64w_store_L).  With
-// pkg (DF_PKG doubles) the chain's forward-substitution packages 0..3 are stored as granules as each becomes final (at
-// the start of step kb's phase A, by wave 1 + kb % 2); k_dataflow.hip's slices of the next block read them.
+// between the factorization and the forward solve (barrier behind it).  L_kk is not stored (potrf64w_store_L).
 template <class M, class Fix = NoFix, class Pre = NoPre>
 __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs, int nrhs, double* __restrict__ Linv,
                                                 DevCtrl* ctrl, Potrf64wSmem& sm, int* lflag = nullptr,
                                                 Fix fix = Fix(), double early_min = 0.0, Pre pre = Pre(),
-                                                unsigned long long* rb_stamp = nullptr, bool wait_d = false,
-                                                double* pkg = nullptr, unsigned long long pkg_tag = 0) {
+                                                unsigned long long* rb_stamp = nullptr, bool wait_d = false) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int base = k * NB;
   const M mI(Linv + (size_t)k * NB * NB, (unsigned)(NB * NB) * 8u);  // Linv[k]
@@ -325,21 +322,6 @@ __device__ __forceinline__ bool potrf64w_factor(int k, double* __restrict__ rhs,
       if (!ok) break;
       P64_STAMP(1 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (pkg && w == 1 + (kb & 1)) {
-        // package kb (k_dataflow.hip's slice kb of the next block), final now: L row-block kb left of its diagonal
-        // block (the T steps < kb: phase B of step kb - 1 waited for them), and sweep kb's L~16^-T and scales (fP) --
-        // 256 kb + 272 data-tagged 16-B granules {value, pkg_tag | kb}, one sc1 store each, no drain, no flag
-        const M mP(pkg, (unsigned)DF_PKG * 8u);
-        const int g0 = 128 * kb * (kb - 1) + 272 * kb, nl = 256 * kb, nc = 16 * kb;
-        const double tag = __longlong_as_double((long long)(pkg_tag | (unsigned)kb));
-        for (int e = lane; e < nl + 272; e += 64) {
-          double v;
-          if (e < nl) v = sm.S[(16 * kb + e / nc) * P64_SP + e % nc];
-          else if (e < nl + 256) v = sm.ET[kb][((e - nl) >> 4) * P64_EP + ((e - nl) & 15)];
-          else v = sm.SV[kb][e - nl - 256];
-          mP.st2(2 * (g0 + e), f64x2{v, tag});
-        }
-      }
       p64w_phaseA(sm, kb, w, lane);
       P64_STAMP(2 + 4 * kb);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

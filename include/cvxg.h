@@ -322,8 +322,9 @@ enum {
                                  8 Cholesky blocks, else 1: the many-column dataflow solves) */
   CVXG_OPT_SPEC_REG = 5,      /* 1 (default): after a regularized direction, chol(Q) and chol(Q + 1e-10 I) run side by
                                  side and the device keeps the one regularizedCholesky keeps; 0: one after the other */
-  CVXG_OPT_RUIZ_LOOP = 6,     /* 0 (default): each Ruiz sweep is a launch pair; 1: the whole loop in one persistent
-                                 launch (CVXG_E_UNSUPPORTED beyond its register batch of tiles) */
+  CVXG_OPT_RUIZ_LOOP = 6,     /* 1: the whole Ruiz loop in one persistent launch (the default up to n = 1024;
+                                 CVXG_E_UNSUPPORTED beyond its register batch of tiles); 0: each sweep a launch pair
+                                 (the default above n = 1024).  Both give the same bits */
   CVXG_OPT_RUIZ_WG = 7        /* workgroups of the one-launch Ruiz loop (0, the default: one per CU) */
 };
 /* Returns CVXG_E_ARG for an unknown option or a value out of its range. */

@@ -33,6 +33,10 @@ for st in ${STAGES:-smoke tests ab}; do
           timeout -k 10 200 python bench.py --workload $wl --steps 50 --warmup 5 --no-cpu-baseline --opt ruiz_loop=$o > $O/ruiz_${wl}_$o.json 2>$O/ruiz_${wl}_$o.err; chk $? ruiz_${wl}_$o
         done
       done ;;
+    side)  # the side workloads on the current build
+      for wl in C2 C4 C3B C4P C2PD C3PD; do
+        timeout -k 10 300 python bench.py --workload $wl --steps 30 --warmup 3 --no-cpu-baseline > $O/wl_$wl.json 2>$O/wl_$wl.err; chk $? wl_$wl
+      done ;;
     c2x)  # C2 instances sharing one GPU
       for k in 4 8; do
         timeout -k 10 300 python bench.py --workload C2X --instances $k --steps 60 --warmup 5 > $O/wl_C2x$k.json 2>$O/wl_C2x$k.err; chk $? c2x$k
