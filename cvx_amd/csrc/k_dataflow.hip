@@ -184,33 +184,6 @@ __device__ __forceinline__ void df_mfma(d4f (&acc)[2][2], const double* Pi, cons
   }
 }
 
-// df_mfma over the k-steps [32 H, 32 H + 32) only (H = 0, 1): the two halves in order are df_mfma's sum, bit for bit
-template <int H>
-__device__ __forceinline__ void df_mfma_half(d4f (&acc)[2][2], const double* Pi, const double* Pj, double sgn, int wr,
-                                             int wc, int lane) {
-#pragma unroll
-  for (int s = 8 * H; s < 8 * H + 8; ++s) {
-    const int kk = 4 * s + (lane >> 4);
-    double fa[2], fb[2];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) fa[mi] = sgn * Pi[(wr * 32 + mi * 16 + (lane & 15)) * DF_SP + kk];
-#pragma unroll
-    for (int nj = 0; nj < 2; ++nj) fb[nj] = Pj[(wc * 32 + nj * 16 + (lane & 15)) * DF_SP + kk];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int nj = 0; nj < 2; ++nj)
-        acc[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi], fb[nj], acc[mi][nj], 0, 0, 0);
-  }
-  __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-  for (int p = 0; p < NB / 16; ++p) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-    if (p + 1 < NB / 16) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-  }
-}
-
 // The updates run df_mfma on the negated tile with sgn = +1, df_neg before and after: with round-to-nearest every
 // step of the MFMA's sum is symmetric under a sign flip, so -((-C) + sum a b) is C + sum (-a) b bit for bit, and the
 // inner loop has no sign flip between an LDS read and its MFMA (with the issue order in df_mfma: Cholesky 1.052 ->
@@ -495,7 +468,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
   __shared__ unsigned s_task;
   __shared__ int s_ok;
   __shared__ int s_next;
-  __shared__ int s_kj;  // the chain: L_k,k-2 already published when L_b,k-2 came in
   int* counter = work;
   int* abortw = work + 32;  // own cache line: the claim counter's line takes every worker's atomic
   int* state = work + 64;  // own cache lines
@@ -594,27 +566,23 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               }
             }
           }
-          // (2) L_b,j (worker TRSM(b,j), published before its rhs update) and L_k,j (the other chain workgroup's TRSM,
-          // published inside its POTRF(k), usually later): D_b -= L_b,j L_b,j^T needs only the first, so it runs as
-          // soon as that tile is in, with L_k,j's loads in flight beside it when it is out too (round 6); the rhs
-          // block is read in POTRF(b)'s fix hook, which it first feeds
+          // (2) L_b,j (worker TRSM(b,j)) and L_k,j (the other chain workgroup's TRSM, published inside its POTRF(k));
+          // the rhs block is read in POTRF(b)'s fix hook, which it first feeds
           if (tid == 0) {
             const int v3 = df_poll(state + df_tri(b, j)), v4 = df_poll(state + df_tri(k, j));
-            s_ok = v3 >= j + 1 || df_wait(state, df_tri(b, j), j + 1, abortw, ctrl);
-            s_kj = v4 >= j + 1;
+            s_ok = (v3 >= j + 1 || df_wait(state, df_tri(b, j), j + 1, abortw, ctrl)) &&
+                   (v4 >= j + 1 || df_wait(state, df_tri(k, j), j + 1, abortw, ctrl));
           }
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           __syncthreads();
           if (!s_ok) return;
-          mark(k, 2, 3);  // trace: the b-2 panel's first input is in (field 3 of the fix record)
-          const bool kj_in = s_kj;
+          mark(k, 2, 3);  // trace: the b-2 panel's inputs are in (field 3 of the fix record)
           {
             f64x2 vl[NB * NB / 512], vk[NB * NB / 512];
             df_load(vl, Sc1Mem(L + (size_t)b * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
-            // (both tiles' loads in flight together; L_k,j's from a clamped descriptor when it is not out, unused then)
-            df_load(vk, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, kj_in ? tile_bytes(ld) : 0u), ld);
+            df_load(vk, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
             df_put(ps.X, vl);  // (POTRF's L^-1 workspace and tile: free until the reset / the batch below)
-            if (kj_in) df_put(ps.S, vk);
+            df_put(ps.S, vk);
           }
           __syncthreads();
           for (int cb = 0; cb < 4; ++cb) {
@@ -625,23 +593,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
               default: ch_update<3>(dacc, ps.X, cb, lane); break;
             }
           }
-          if (!kj_in) {  // L_k,j was not out yet: wait for it now
-            if (!wait(state, df_tri(k, j), j + 1)) return;
-            df_stage(ps.S, Sc1Mem(L + (size_t)k * NB * ld + (size_t)j * NB, tile_bytes(ld)), ld);
-            __syncthreads();
-          }
-          // the row-blocks of L_kk^-1 published so far: polled between the MFMA phases and read behind them, so the
-          // batch below knows its size the moment this panel is applied (round 6: no poll round trip behind the
-          // MFMAs; the value is at most one MFMA phase old)
-          int pf = 0;
-          if (tid == 0) pf = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          df_mfma_half<0>(acc, ps.X, ps.S, -1.0, wr, wc, lane);  // A_b,k -= L_b,j L_k,j^T, k-steps 0..31
-          if (tid == 0) {
-            pv = pf;
-            pf = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          df_mfma_half<1>(acc, ps.X, ps.S, -1.0, wr, wc, lane);  // k-steps 32..63
-          if (tid == 0) pv = max(pv, pf);
+          df_mfma(acc, ps.X, ps.S, -1.0, wr, wc, lane);  // A_b,k -= L_b,j L_k,j^T
 #pragma unroll
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -649,6 +601,9 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 cs.Sa[(wr * 32 + mi * 16 + (lane >> 4) + 4 * r) * DF_SP + wc * 32 + nj * 16 + (lane & 15)] = acc[mi][nj][r];
+          // the row-blocks of L_kk^-1 published by now (after this panel's MFMAs, so the batch below takes as many as
+          // it can)
+          if (tid == 0) pv = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           mark(k, 0, 3);  // trace: the b-2 panel applied (field 3 of POTRF(k)'s record)
         } else {
         // A_b,k and D_b with every panel < k applied (state >= k): one wait for both states, then every load in
@@ -719,15 +674,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
         };
         __syncthreads();  // Sa and the batch's row-blocks in ps.S complete
         mark(k, 4, 0);    // trace: every wave's staging loads landed (record 4: the batch's phases)
-        bool pre = false;  // row-block nbat already loaded into er behind the batch
         double af[16];  // this wave's row-block of A_b,k as MFMA A-fragments
 #pragma unroll
         for (int q = 0; q < 16; ++q) af[q] = cs.Sa[(16 * wv + (lane & 15)) * DF_SP + 4 * q + (lane >> 4)];
         if (nbat > 0) {
           // the batch: the same MFMA sequence per output as the per-slice form below, so the same bits
-          // the next row-block: polled now, loaded behind the batch's diagonal updates when it is out (round 6)
-          int pb = 0;
-          if (nbat < 4 && tid == 0) pb = __hip_atomic_load(cflag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           d4f acc[4];
           acc[0] = ch_trsm<0>(af, ps.S, lane);
           if (nbat > 1) acc[1] = ch_trsm<1>(af, ps.S + 16 * P64_SP, lane);
@@ -743,12 +694,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
                 const int row = 16 * wv + (lane >> 4) + 4 * r, col = 16 * cb + (lane & 15);
                 Lp[row * DF_SP + col] = acc[cb][r];
               }
-          if (tid == 0) s_next = pb;
           __syncthreads();
-          if (nbat < 4 && s_next >= nbat + 1) {
-            eload(nbat);
-            pre = true;
-          }
           for (int cb = 0; cb < nbat; ++cb) {
             switch (wv) {  // D -= L'[:, cb] L'[:, cb]^T on this wave's lower blocks
               case 0: ch_update<0>(dacc, Lp, cb, lane); break;
@@ -759,7 +705,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_dataflow(double* __restrict__ L
           }
           mark(k, 4, 2);
         }
-        if (nbat < 4 && !pre) {
+        if (nbat < 4) {
           if (!wait(cflag, k, nbat + 1)) return;
           eload(nbat);
         }
