@@ -66,7 +66,7 @@ class cvxg_pd_step_info(C.Structure):
 
 class cvxg_pd_solution(C.Structure):
     _fields_ = [("duality_gap", C.c_double), ("norm_dual_residual", C.c_double), ("objective", C.c_double),
-                ("iter", C.c_int), ("maxed_out", C.c_int), ("newton_steps", C.c_int)]
+                ("iter", C.c_int), ("maxed_out", C.c_int), ("newton_steps", C.c_int), ("equality_gap", C.c_double)]
 
 
 _D = C.POINTER(C.c_double)
@@ -103,7 +103,10 @@ SIGNATURES = {
     "cvxg_pd_direction": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, _D, _D, _D, _D,
                                     C.POINTER(cvxg_pd_step_info)]),
     "cvxg_pd_solve": (C.c_int, [_P, C.POINTER(cvxg_params), C.POINTER(cvxg_pd_solution)]),
+    "cvxg_pd_direction_eq": (C.c_int, [_P, C.POINTER(cvxg_params), C.c_double, _D, _D, _D, _D, _D, _D,
+                                       C.POINTER(cvxg_pd_step_info)]),
     "cvxg_get_lambda": (C.c_int, [_P, _D]),
+    "cvxg_get_nu": (C.c_int, [_P, _D]),
     "cvxg_solution_space": (C.c_int, [C.c_int, C.c_int, C.c_int, _D, C.c_int, C.c_int, _D, _D, _D, C.c_int]),
     "cvxg_affine_from": (C.c_int, [_P, _P, _D, _D, C.c_int]),
     "cvxg_affine_parameter": (C.c_int, [_P, _D, _D]),

@@ -25,7 +25,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from .engine import CvxgError, Engine, NotStrictlyFeasible, solution_space
+from .engine import CvxgError, Engine, NotConvergedException, NotStrictlyFeasible, solution_space
 
 # ------------------------------------------------------------------------------------------------
 
@@ -607,18 +607,26 @@ class BarrierSolver:
         return GpuBarrierSolver(objF, cnts, eqs, pars, device)
 
 
+class LineSearchFailedException(NotConvergedException):
+    """LineSearchFailedException (PrimalDualSolver.scala:369-372, 538-541): the residual line search did not
+    terminate.  .solution holds the last accepted iterate."""
+
+    def __init__(self, code: int, msg: str, solution: Optional[Solution] = None):
+        super().__init__(code, msg)
+        self.solution = solution
+
+
 class GpuPrimalDualSolver:
-    """PrimalDualSolver (PrimalDualSolver.scala:18-460) on the MI355X engine: each iteration's KKT matrix, its
-    SymmetricLinearSystem solve, dlambda and the residual line-search trials run on the device
-    (cvxg_pd_solve).  Quadratic or linear objective, LinearConstraint and QuadraticConstraint members, no equality
-    constraints (the reference's solve_withEQs is not built, see include/cvxg.h)."""
+    """PrimalDualSolver (PrimalDualSolver.scala:18-621) on the MI355X engine: each iteration's KKT matrix, its
+    solve, dlambda and the residual line-search trials run on the device (cvxg_pd_solve).  Quadratic or linear
+    objective, LinearConstraint and QuadraticConstraint members; with equality constraints solve_withEQs as the
+    reference writes it (its KKT right-hand side "FIX ME", :284), whose line search fails like the reference's
+    (LineSearchFailedException, see include/cvxg.h)."""
 
     def __init__(self, objF: ObjectiveFunction, cnts: ConstraintSet, eqs: Optional[EqualityConstraint],
                  pars: SolverParams, device: int = 0):
         if not isinstance(objF, (QuadraticObjectiveFunction, LinearObjectiveFunction)):
             raise TypeError("GPU primal-dual engine: objective must be Quadratic- or LinearObjectiveFunction")
-        if eqs is not None:
-            raise TypeError("GPU primal-dual engine: equality constraints are not supported (solve_withEQs)")
         if cnts.feasiblePoint is None:
             raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
         self.objF, self.cnts, self.eqs, self.pars = objF, cnts, eqs, pars
@@ -626,19 +634,29 @@ class GpuPrimalDualSolver:
         self.dim = cnts.dim
         self.startingPoint = cnts.feasiblePoint
         A, r, ub = cnts.packed()
-        self.engine = Engine(cnts.dim, A.shape[0], 0, device)
+        p = eqs.A.shape[0] if eqs is not None else 0
+        self.engine = Engine(cnts.dim, A.shape[0], p, device)
         self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
         self.engine.set_ineq(A, r, ub)
+        if eqs is not None:
+            self.engine.set_eq(eqs.A, eqs.b)
         qrows, qP = cnts.quadratic()
         if qrows is not None:  # kktMatrix_noEqs adds grad2_gi * lambda_i (PrimalDualSolver.scala:224-238)
             self.engine.set_quad(qrows, qP)
 
     def solve(self, debugLevel: int = 0) -> Solution:
-        """PrimalDualSolver.solve (:628-633): standard criterion gap < tol and |r_dual| < tol."""
+        """PrimalDualSolver.solve (:628-641): standard criterion gap < tol and |r| < tol; solve_noEQs or, with
+        equality constraints, solve_withEQs (:550-621)."""
         self.engine.set_x(self.startingPoint)
-        s = self.engine.pd_solve(self.pars)
-        return Solution(self.engine.get_x(), None, s.duality_gap, None, None, s.iter, bool(s.maxed_out),
-                        s.newton_steps, 0, lambda_=self.engine.get_lambda(), normDualResidual=s.norm_dual_residual)
+        rc, s = self.engine.pd_solve(self.pars, partial=True)
+        eqs = self.eqs is not None
+        sol = Solution(self.engine.get_x(), None, s.duality_gap, s.equality_gap if eqs else None, None, s.iter,
+                       bool(s.maxed_out), s.newton_steps, 0, lambda_=self.engine.get_lambda(),
+                       nu=self.engine.get_nu() if eqs else None, normDualResidual=s.norm_dual_residual)
+        if rc == _lib.CVXG_E_LINESEARCH:
+            raise LineSearchFailedException(rc, self.engine.lib.cvxg_last_error(self.engine.h).decode(), sol)
+        self.engine._check(rc)
+        return sol
 
 
 class PrimalDualSolver:
@@ -767,10 +785,11 @@ class Dist_KL(OptimizationProblem):
 
     def solve(self, debugLevel: int = 0) -> Solution:
         """The direct solve (Dist_KL.scala:309-312): BarrierSolver(objF, ineqsWithFeasiblePoint, Some(eqs)) on the
-        engine's KL primal objective.  "PD" builds the reference's PrimalDualSolver with equalities (solve_withEQs),
-        which this engine does not run (include/cvxg.h)."""
+        engine's KL primal objective.  "PD" builds the reference's PrimalDualSolver with equalities (solve_withEQs)
+        over the KL objective, which the device primal-dual solver does not take (quadratic or linear objectives
+        only, include/cvxg.h)."""
         if self.solverType == "PD":
-            raise TypeError("GPU primal-dual engine: equality constraints are not supported (solve_withEQs)")
+            raise TypeError("GPU primal-dual engine: the KL primal objective is not supported (solverType \"PD\")")
         if self.solver is None:
             self.solver = BarrierSolver.apply(self.objectiveFunction, self.ineqsWithFeasiblePoint, self.eqs, self.pars,
                                               self.device)
@@ -800,4 +819,4 @@ __all__ = ["SolverParams", "Solution", "OptimizationState", "CvxUtils", "Feasibi
            "DualKLObjectiveFunction", "KLPrimalObjectiveFunction", "Dist_KL",
            "LinearConstraint", "QuadraticConstraint", "Constraints", "EqualityConstraint", "ConstraintSet", "GpuBarrierSolver", "BarrierSolver",
            "GpuPrimalDualSolver", "PrimalDualSolver",
-           "OptimizationProblem", "problem_from_spec", "CvxgError", "NotStrictlyFeasible"]
+           "OptimizationProblem", "problem_from_spec", "CvxgError", "NotStrictlyFeasible", "LineSearchFailedException"]

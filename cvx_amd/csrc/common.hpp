@@ -73,6 +73,7 @@ enum {
   SC_TR_KLP,    // the KL primal objective at a fresh trial point xt
   SC_KLA,       // KL dual: sum_j y_j (|B'||z|)_j, the error scale of its exponents at z
   SC_TR_KLSUM,  // KL dual: sum_j R exp(-(B'zt)_j) at a fresh trial point zt
+  SC_PD_CENT,   // primal-dual with equalities: |r_cent(t, x, lambda)|^2 of the state after a step
   SC_COUNT
 };
 static_assert(SC_COUNT <= 40, "DevCtrl::sc too small");

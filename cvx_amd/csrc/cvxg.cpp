@@ -147,6 +147,9 @@ struct cvxg_ctx {
   double *pd_rhs = nullptr, *pd_d1 = nullptr, *pd_R0 = nullptr, *pd_R1 = nullptr, *pd_R2 = nullptr;  // np
   double* pd_tmp = nullptr;
   double *pd_part_rows = nullptr, *pd_part_cols = nullptr, *pd_out = nullptr, *pd_hout = nullptr;
+  // solve_withEQs: nu, dnu, A x - b, A dx (pe); the dual residual + A'nu and its step term (np); trial partials
+  double *pd_nu = nullptr, *pd_dnu = nullptr, *pd_rp = nullptr, *pd_adx = nullptr;
+  double *pd_R0e = nullptr, *pd_R1e = nullptr, *pd_part_eq = nullptr;
   // symSolve / kktSymSolve fallback buffers (allocated on first use; ldm = round_up(n + p, 128))
   int eig_ldm = 0;
   double *eig_M = nullptr, *eig_K = nullptr, *eig_d = nullptr, *eig_e = nullptr, *eig_dots = nullptr;
@@ -1964,7 +1967,8 @@ void cvxg_destroy(cvxg_ctx* ctx) {
                   ctx->Psa, ctx->xtr, ctx->Pxtr, ctx->c_tr, ctx->d_tr, ctx->invd_tr, ctx->w_tr, ctx->logd_tr,
                   ctx->klp_lx, ctx->klp_g0, ctx->klp_hd, ctx->klp_ab, ctx->klp_lxt, ctx->klp_part, ctx->klp_ls,
                   ctx->kl_vabs, ctx->kl_uabs, ctx->kl_vtr, ctx->kl_ytr, ctx->qPxa, ctx->qPsa, ctx->qfabs, ctx->qPx_tr,
-                  ctx->qextra_tr, ctx->x1, ctx->c1, ctx->d1, ctx->invd1, ctx->w1, ctx->logd1, ctx->cabs1};
+                  ctx->qextra_tr, ctx->x1, ctx->c1, ctx->d1, ctx->invd1, ctx->w1, ctx->logd1, ctx->cabs1,
+                  ctx->pd_nu, ctx->pd_dnu, ctx->pd_rp, ctx->pd_adx, ctx->pd_R0e, ctx->pd_R1e, ctx->pd_part_eq};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->kY, (void*)ctx->kYg, (void*)ctx->kgram, (void*)ctx->kS, (void*)ctx->kzp,
@@ -2649,10 +2653,6 @@ int cvxg_get_phase_stats(cvxg_ctx* ctx, double* ms, int* occurrences, int count)
 // ------------------------------------------------------------------------------------------------
 static int pd_check(cvxg_ctx* ctx) {
   CHK(check_ready(ctx));
-  if (ctx->p > 0)
-    return set_err(ctx, CVXG_E_UNSUPPORTED,
-                   "PrimalDualSolver.solve_withEQs is not built (its KKT right-hand side has the opposite sign of "
-                   "the no-equality system, PrimalDualSolver.scala:284)");
   if (ctx->kl || ctx->klp)
     return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: quadratic or linear objective only");
   if (ctx->m == 0) return set_err(ctx, CVXG_E_ARG, "primal-dual solver needs inequality constraints");
@@ -2663,8 +2663,14 @@ static int pd_check(cvxg_ctx* ctx) {
     CHK(dalloc(ctx, v, np));
   CHK(dalloc(ctx, &ctx->pd_part_rows, (size_t)pd_row_blocks(ctx->m) * 2 * LS_TRIALS));
   CHK(dalloc(ctx, &ctx->pd_part_cols, (size_t)((ctx->n + 255) / 256) * LS_TRIALS));
-  CHK(dalloc(ctx, &ctx->pd_out, 3 * LS_TRIALS));
-  HIPC(ctx, hipHostMalloc((void**)&ctx->pd_hout, 3 * LS_TRIALS * sizeof(double), hipHostMallocDefault));
+  CHK(dalloc(ctx, &ctx->pd_out, 4 * LS_TRIALS));
+  if (ctx->p > 0) {
+    const size_t pe = std::max(ctx->p, CVXG_MAX_EQ);
+    for (double** v : {&ctx->pd_nu, &ctx->pd_dnu, &ctx->pd_rp, &ctx->pd_adx}) CHK(dalloc(ctx, v, pe));
+    for (double** v : {&ctx->pd_R0e, &ctx->pd_R1e}) CHK(dalloc(ctx, v, np));
+    CHK(dalloc(ctx, &ctx->pd_part_eq, (size_t)((ctx->p + 255) / 256) * LS_TRIALS));
+  }
+  HIPC(ctx, hipHostMalloc((void**)&ctx->pd_hout, 4 * LS_TRIALS * sizeof(double), hipHostMallocDefault));
   return CVXG_OK;
 }
 
@@ -2676,7 +2682,10 @@ static void pd_dual_residual(cvxg_ctx* ctx, const double* v, const double* a0, c
   if (ctx->nq > 0) launch_quad_grad(ctx->s, ctx->qPx, v, ctx->qrows, ctx->nq, ctx->np, out);
 }
 
-// Search direction at (t, ctx->x, ctx->lam) into ctx->dx / ctx->dlam (PrimalDualSolver.scala:421-425).
+static int pd_delta_lambda(cvxg_ctx* ctx, double t);
+
+// Search direction at (t, ctx->x, ctx->lam[, ctx->pd_nu]) into ctx->dx / ctx->dlam [/ ctx->pd_dnu]
+// (PrimalDualSolver.scala:421-425; with equality rows :590-593).
 static int pd_direction_dev(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg_pd_step_info* info) {
   hipStream_t s = ctx->s;
   const int n = ctx->n, np = ctx->np;
@@ -2688,6 +2697,25 @@ static int pd_direction_dev(cvxg_ctx* ctx, const cvxg_params* pars, double t, cv
   CHK(assemble_hessian(ctx, ctx->pd_w, ctx->lam));
   launch_ctrl_set(s, ctx->ctrl, 0, t);
   ctx->x_eval_valid = 0;  // y is reused below as the rhs of the shared choleskySolve
+  if (ctx->p > 0) {
+    // solve_withEQs (:590-593): kktSystem_withEqs (:271-285) = KKTSystem(H, A, q = rhs1 + A'nu, -(A x - b)),
+    // KKTSystem.solve (H dx + A'dnu = -q, A dx = b - A x; KKTSystem.scala:43-66) -- the shared KKT path of the
+    // equality-constrained barrier step (eqd = b - A x from eval_at_x).  As written: the reference's own "FIX ME"
+    // (:284), q enters with the opposite sign of the no-equality system H dx = rhs1.
+    launch_axpy(s, ctx->eqtmp, ctx->beq, -1.0, ctx->p, ctx->pd_rp);     // A x - b (eqtmp = A x; the KKT check reuses it)
+    launch_btw_plus(s, ctx->Aeq, np, ctx->p, ctx->pd_nu, ctx->pd_rhs, n, ctx->y);  // q = rhs1 + A'nu
+    HIPC(ctx, hipGetLastError());
+    cvxg_step_info si;
+    memset(&si, 0, sizeof(si));
+    const int rc = newton_direction_kkt(ctx, pars, &si);
+    info->fallback = si.fallback;
+    info->regularized = si.regularized;
+    info->rel_err = si.rel_err;
+    info->ruiz_sweeps = si.ruiz_sweeps;
+    CHK(rc);
+    HIPC(ctx, hipMemcpyAsync(ctx->pd_dnu, ctx->kw, (size_t)ctx->p * sizeof(double), hipMemcpyDeviceToDevice, s));
+    return pd_delta_lambda(ctx, t);
+  }
   // SymmetricLinearSystem: d1 = Ruiz(H), Q = (d1 d1') o H, s = d1 o r (SymmetricLinearSystem.scala:20-23).  Q is
   // exactly symmetric (H is mirrored, d_i d_j = d_j d_i), so checkSymmetric(Q, 1e-13) holds and choleskySolve runs.
   tstart(ctx, 1);
@@ -2718,8 +2746,14 @@ static int pd_direction_dev(cvxg_ctx* ctx, const cvxg_params* pars, double t, cv
     HIPC(ctx, hipMemcpyAsync(ctx->dx, ctx->eig_x, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
   }
   launch_scale_vec(s, ctx->dx, ctx->pd_d1, np, ctx->dx);  // x = d :* u  (:54)
-  // deltaLambda (:184-209) with the step bound s0 and the central residual at (x, lambda); w = Dg dx (for a
-  // QuadraticConstraint row (a + P x).dx, with f = dx'P dx kept for the line-search trials)
+  return pd_delta_lambda(ctx, t);
+}
+
+// deltaLambda (:184-209) with the step bound s0 and the central residual at (x, lambda); w = Dg dx (for a
+// QuadraticConstraint row (a + P x).dx, with f = dx'P dx kept for the line-search trials)
+static int pd_delta_lambda(cvxg_ctx* ctx, double t) {
+  hipStream_t s = ctx->s;
+  const int np = ctx->np;
   launch_rowdot(s, ctx->A, np, ctx->mp, np, ctx->dx, ctx->e);
   if (ctx->nq > 0) {
     launch_rowdot(s, ctx->Pq, np, ctx->nq * np, np, ctx->dx, ctx->qPs);
@@ -2732,10 +2766,11 @@ static int pd_direction_dev(cvxg_ctx* ctx, const cvxg_params* pars, double t, cv
 }
 
 // lineSearch_noEQs (PrimalDualSolver.scala:311-374) from (ctx->x, ctx->lam) along (dx, dlam); on success
-// x += s dx, lambda += s dlam.  Needs ctx->c / ctx->Px at x (pd_direction_dev).
+// x += s dx, lambda += s dlam.  With equality rows lineSearch_withEQs (:478-543): the residual adds A'nu to the dual
+// part and the primal part A x - b, nu moves with the step.  Needs ctx->c / ctx->Px at x (pd_direction_dev).
 static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg_pd_step_info* info) {
   hipStream_t s = ctx->s;
-  const int np = ctx->np;
+  const int n = ctx->n, np = ctx->np, p = ctx->p;
   const double* Px = ctx->hasP ? ctx->Px : nullptr;
   pd_dual_residual(ctx, ctx->lam, ctx->a0, Px, ctx->pd_R0);                      // r_dual(x, lambda)
   if (ctx->hasP) launch_rowdot(s, ctx->P, np, np, np, ctx->dx, ctx->pd_tmp);     // P dx
@@ -2745,13 +2780,24 @@ static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg
     HIPC(ctx, hipMemsetAsync(ctx->pd_R2, 0, (size_t)np * sizeof(double), s));
     launch_quad_grad(s, ctx->qPs, ctx->dlam, ctx->qrows, ctx->nq, np, ctx->pd_R2);
   }
-  launch_dot(s, ctx->pd_R0, nullptr, np, ctx->ctrl, SC_RES2);
+  const double* R0 = ctx->pd_R0;
+  const double* R1 = ctx->pd_R1;
+  if (p > 0) {  // + A'(nu + s dnu); A x_s - b = (A x - b) + s A dx
+    launch_btw_plus(s, ctx->Aeq, np, p, ctx->pd_nu, ctx->pd_R0, n, ctx->pd_R0e);
+    launch_btw_plus(s, ctx->Aeq, np, p, ctx->pd_dnu, ctx->pd_R1, n, ctx->pd_R1e);
+    launch_rowdot(s, ctx->Aeq, np, p, np, ctx->dx, ctx->pd_adx);
+    launch_dot(s, ctx->pd_rp, nullptr, p, ctx->ctrl, SC_EQ2);
+    R0 = ctx->pd_R0e;
+    R1 = ctx->pd_R1e;
+  }
+  launch_dot(s, R0, nullptr, p > 0 ? n : np, ctx->ctrl, SC_RES2);
   launch_dot(s, ctx->pd_rc, nullptr, ctx->mp, ctx->ctrl, SC_RES2B);
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
   double s0;
   memcpy(&s0, &ctx->hctrl->pd_s0, sizeof(s0));
-  const double norm_rt = sqrt(ctx->hctrl->sc[SC_RES2] + ctx->hctrl->sc[SC_RES2B]);
+  const double norm_rt =
+      sqrt(ctx->hctrl->sc[SC_RES2] + ctx->hctrl->sc[SC_RES2B] + (p > 0 ? ctx->hctrl->sc[SC_EQ2] : 0.0));
   info->s0 = s0;
   info->norm_residual = norm_rt;
   const double alpha = pars->alpha, beta = pars->beta;
@@ -2760,16 +2806,18 @@ static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg
   double sbase = 0.99 * s0;
   int k = 0, K = -1;
   double sK = 0.0;
+  const int nout = p > 0 ? 4 : 3;
   while (K < 0) {
-    launch_pd_trials(s, ctx->c, ctx->e, ctx->ub, ctx->lam, ctx->dlam, ctx->m, ctx->pd_R0, ctx->pd_R1, ctx->n, sbase,
-                     beta, t, ctx->pd_part_rows, ctx->pd_part_cols, ctx->pd_out, ctx->nq > 0 ? ctx->qf : nullptr,
-                     ctx->nq > 0 ? ctx->pd_R2 : nullptr);
+    launch_pd_trials(s, ctx->c, ctx->e, ctx->ub, ctx->lam, ctx->dlam, ctx->m, R0, R1, ctx->n, sbase, beta, t,
+                     ctx->pd_part_rows, ctx->pd_part_cols, ctx->pd_out, ctx->nq > 0 ? ctx->qf : nullptr,
+                     ctx->nq > 0 ? ctx->pd_R2 : nullptr, ctx->pd_rp, ctx->pd_adx, p, ctx->pd_part_eq);
     HIPC(ctx, hipGetLastError());
-    CHK(copy_sync(ctx, ctx->pd_hout, ctx->pd_out, 3 * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost));
+    CHK(copy_sync(ctx, ctx->pd_hout, ctx->pd_out, nout * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost));
     double sk = sbase;
     for (int j = 0; j < LS_TRIALS; ++j, ++k) {
       const double cent = ctx->pd_hout[2 * j], viol = ctx->pd_hout[2 * j + 1], dual = ctx->pd_hout[2 * LS_TRIALS + j];
-      const bool ok = viol == 0.0 && sqrt(dual + cent) < (1 - alpha * sk) * norm_rt;
+      const double prim = p > 0 ? ctx->pd_hout[3 * LS_TRIALS + j] : 0.0;
+      const bool ok = viol == 0.0 && sqrt(dual + cent + prim) < (1 - alpha * sk) * norm_rt;
       if (ok || k == kmax) {
         K = k;
         sK = sk;
@@ -2785,27 +2833,46 @@ static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg
   if (K >= maxIter) return set_err(ctx, CVXG_E_LINESEARCH, "PrimalDualSolver: Line search unsuccessful.");
   launch_axpy(s, ctx->x, ctx->dx, sK, np, ctx->x);           // x + dx*s
   launch_axpy(s, ctx->lam, ctx->dlam, sK, ctx->mp, ctx->lam);  // lambda + dLambda*s
+  if (p > 0) launch_axpy(s, ctx->pd_nu, ctx->pd_dnu, sK, p, ctx->pd_nu);  // nu + dNu*s
   HIPC(ctx, hipGetLastError());
   ctx->x_eval_valid = 0;
   return CVXG_OK;
 }
 
-// gap = -h(x).lambda (:289-297) and |grad f + A' lambda| at the current (x, lambda)
-static int pd_state(cvxg_ctx* ctx, double* gap, double* norm_dual) {
+// gap = -h(x).lambda (:289-297) and |grad f + A' lambda| at the current (x, lambda); with equality rows (:600-606)
+// the norm of the whole residual_withEqs(t, x, lambda, nu) -- t of the step just taken -- and |A x - b|.
+static int pd_state(cvxg_ctx* ctx, double t, double* gap, double* norm_dual, double* eq_gap) {
   CHK(eval_at_x(ctx));
+  const int p = ctx->p;
   pd_dual_residual(ctx, ctx->lam, ctx->a0, ctx->hasP ? ctx->Px : nullptr, ctx->pd_R0);
+  const double* R0 = ctx->pd_R0;
+  if (p > 0) {
+    launch_btw_plus(ctx->s, ctx->Aeq, ctx->np, p, ctx->pd_nu, ctx->pd_R0, ctx->n, ctx->pd_R0e);
+    launch_pd_central(ctx->s, ctx->c, ctx->ub, ctx->lam, t, ctx->m, ctx->mp, ctx->pd_rc);
+    launch_dot(ctx->s, ctx->pd_rc, nullptr, ctx->mp, ctx->ctrl, SC_PD_CENT);
+    R0 = ctx->pd_R0e;
+  }
   launch_dot(ctx->s, ctx->d, ctx->lam, ctx->mp, ctx->ctrl, SC_RES2B);
-  launch_dot(ctx->s, ctx->pd_R0, nullptr, ctx->np, ctx->ctrl, SC_RES2);
+  launch_dot(ctx->s, R0, nullptr, p > 0 ? ctx->n : ctx->np, ctx->ctrl, SC_RES2);
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
-  *gap = ctx->hctrl->sc[SC_RES2B];
-  *norm_dual = sqrt(ctx->hctrl->sc[SC_RES2]);
+  const double* sc = ctx->hctrl->sc;
+  *gap = sc[SC_RES2B];
+  *norm_dual = p > 0 ? sqrt(sc[SC_RES2] + sc[SC_PD_CENT] + sc[SC_EQ2]) : sqrt(sc[SC_RES2]);
+  if (eq_gap) *eq_gap = p > 0 ? sqrt(sc[SC_EQ2]) : 0.0;
   return CVXG_OK;
 }
 
 int cvxg_pd_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, const double* lambda,
                       double* dx, double* dlambda, cvxg_pd_step_info* info) {
   if (!ctx || !pars || !x || !lambda) return CVXG_E_ARG;
+  if (ctx->p > 0) return set_err(ctx, CVXG_E_ARG, "cvxg_pd_direction: equality rows present (cvxg_pd_direction_eq)");
+  return cvxg_pd_direction_eq(ctx, pars, t, x, lambda, nullptr, dx, dlambda, nullptr, info);
+}
+
+int cvxg_pd_direction_eq(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, const double* lambda,
+                         const double* nu, double* dx, double* dlambda, double* dnu, cvxg_pd_step_info* info) {
+  if (!ctx || !pars || !x || !lambda || (ctx->p > 0 && !nu)) return CVXG_E_ARG;
   HIPC(ctx, hipSetDevice(ctx->dev));
   CHK(pd_check(ctx));
   cvxg_pd_step_info tmp;
@@ -2814,11 +2881,13 @@ int cvxg_pd_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const do
   info->t = t;
   CHK(cvxg_set_x(ctx, x));
   CHK(upload_vec(ctx, ctx->lam, lambda, ctx->m, ctx->mp));
+  if (ctx->p > 0) CHK(upload_vec(ctx, ctx->pd_nu, nu, ctx->p, std::max(ctx->p, CVXG_MAX_EQ)));
   CHK(pd_direction_dev(ctx, pars, t, info));
   CHK(sync_ctrl(ctx));
   memcpy(&info->s0, &ctx->hctrl->pd_s0, sizeof(double));
   if (dx) CHK(copy_sync(ctx, dx, ctx->dx, ctx->n * sizeof(double), hipMemcpyDeviceToHost));
   if (dlambda) CHK(copy_sync(ctx, dlambda, ctx->dlam, ctx->m * sizeof(double), hipMemcpyDeviceToHost));
+  if (dnu && ctx->p > 0) CHK(copy_sync(ctx, dnu, ctx->pd_dnu, ctx->p * sizeof(double), hipMemcpyDeviceToHost));
   return CVXG_OK;
 }
 
@@ -2826,36 +2895,45 @@ int cvxg_pd_solve(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_pd_solution* sol)
   if (!ctx || !pars) return CVXG_E_ARG;
   HIPC(ctx, hipSetDevice(ctx->dev));
   CHK(pd_check(ctx));
+  const bool eqs = ctx->p > 0;
   const double tol = pars->tolSolver, mu = 10.0;
   const double m = ctx->m;
-  // lambda = constraintSet.lambda(x) = -1/h (ConstraintSet.scala:116-120), gap = -h.lambda, t = mu m / gap
+  // lambda = constraintSet.lambda(x) = -1/h (ConstraintSet.scala:116-120), gap = -h.lambda, t = mu m / gap; with
+  // equality rows nu = 0 (:566-568)
   CHK(set_t(ctx, 1.0));
   CHK(eval_at_x(ctx));
   launch_pd_lambda0(ctx->s, ctx->invd, ctx->m, ctx->mp, ctx->lam);
-  double gap = 0.0, norm_dual = 0.0;
-  CHK(pd_state(ctx, &gap, &norm_dual));
+  if (eqs) HIPC(ctx, hipMemsetAsync(ctx->pd_nu, 0, (size_t)ctx->p * sizeof(double), ctx->s));
+  double gap = 0.0, norm_dual = 0.0, eq_gap = 0.0;
+  CHK(pd_state(ctx, 1.0, &gap, &norm_dual, nullptr));
   norm_dual = std::numeric_limits<double>::max();  // OptimizationState(normDualResidual = Double.MaxValue)
+  eq_gap = eqs ? std::numeric_limits<double>::max() : 0.0;
   double t = mu * m / gap;
-  const double maxIter = 2000.0 / mu;
+  const double maxIter = (eqs ? 1500.0 : 2000.0) / mu;  // solve_withEQs :577, solve_noEQs :410
   int iter = 0;
-  while (!(gap < tol && norm_dual < tol) && iter < maxIter) {
-    cvxg_pd_step_info info;
-    memset(&info, 0, sizeof(info));
-    info.t = t;
-    CHK(pd_direction_dev(ctx, pars, t, &info));
-    CHK(pd_line_search(ctx, pars, t, &info));
-    CHK(pd_state(ctx, &gap, &norm_dual));
-    t = mu * m / gap;  // JVM Double semantics: a zero gap gives +Infinity
-    ++iter;
-    timing_collect(ctx);  // phase times of the last iteration (instrumentation, when enabled)
-  }
-  if (sol) {
+  // sol holds the state after the last completed iteration, also when a later one fails (the reference throws)
+  auto fill = [&]() {
+    if (!sol) return;
     sol->duality_gap = gap;
     sol->norm_dual_residual = norm_dual;
     sol->objective = objective_at_x(ctx);
     sol->iter = iter - 1;
     sol->maxed_out = iter == (int)maxIter;
     sol->newton_steps = iter;
+    sol->equality_gap = eq_gap;
+  };
+  fill();
+  while (!(gap < tol && norm_dual < tol) && iter < maxIter) {
+    cvxg_pd_step_info info;
+    memset(&info, 0, sizeof(info));
+    info.t = t;
+    CHK(pd_direction_dev(ctx, pars, t, &info));
+    CHK(pd_line_search(ctx, pars, t, &info));
+    CHK(pd_state(ctx, t, &gap, &norm_dual, &eq_gap));
+    t = mu * m / gap;  // JVM Double semantics: a zero gap gives +Infinity
+    ++iter;
+    fill();
+    timing_collect(ctx);  // phase times of the last iteration (instrumentation, when enabled)
   }
   return CVXG_OK;
 }
@@ -2865,6 +2943,14 @@ int cvxg_get_lambda(cvxg_ctx* ctx, double* lambda) {
   if (!ctx->lam) return set_err(ctx, CVXG_E_ARG, "no primal-dual iterate (call cvxg_pd_solve first)");
   HIPC(ctx, hipSetDevice(ctx->dev));
   return copy_sync(ctx, lambda, ctx->lam, ctx->m * sizeof(double), hipMemcpyDeviceToHost);
+}
+
+int cvxg_get_nu(cvxg_ctx* ctx, double* nu) {
+  if (!ctx || !nu) return CVXG_E_ARG;
+  if (ctx->p == 0 || !ctx->pd_nu)
+    return set_err(ctx, CVXG_E_ARG, "no primal-dual equality multipliers (p = 0 or no cvxg_pd_solve yet)");
+  HIPC(ctx, hipSetDevice(ctx->dev));
+  return copy_sync(ctx, nu, ctx->pd_nu, ctx->p * sizeof(double), hipMemcpyDeviceToHost);
 }
 
 }  // extern "C"

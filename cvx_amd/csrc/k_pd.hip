@@ -163,15 +163,36 @@ __global__ __launch_bounds__(256) void k_pd_trials_cols(const double* __restrict
   }
 }
 int pd_row_blocks(int m) { return m > 0 ? (m + 255) / 256 : 1; }
-// out[0 .. 2 LS_TRIALS): (central sum of squares, violations) per trial; out[2 LS_TRIALS ..): dual sum of squares
+// out[0 .. 2 LS_TRIALS): (central sum of squares, violations) per trial; out[2 LS_TRIALS ..): dual sum of squares;
+// with equality rows (p > 0, solve_withEQs :531-534) out[3 LS_TRIALS ..): the primal residual |A x_s - b|^2 =
+// |(A x - b) + s (A dx)|^2 per trial, the column kernel over the p rows.
 void launch_pd_trials(hipStream_t s, const double* c, const double* e, const double* ub, const double* lam,
                       const double* dlam, int m, const double* R0, const double* R1, int n, double sbase, double beta,
-                      double t, double* part_rows, double* part_cols, double* out, const double* f, const double* R2) {
+                      double t, double* part_rows, double* part_cols, double* out, const double* f, const double* R2,
+                      const double* rp, const double* adx, int p, double* part_eq) {
   const int br = pd_row_blocks(m), bc = (n + 255) / 256;
   k_pd_trials_rows<<<br, 256, 0, s>>>(c, e, ub, lam, dlam, m, sbase, beta, t, part_rows, f);
   k_pd_trials_cols<<<bc, 256, 0, s>>>(R0, R1, n, sbase, beta, part_cols, R2);
   launch_sum_chunks(s, part_rows, br, 2 * LS_TRIALS, out);
   launch_sum_chunks(s, part_cols, bc, LS_TRIALS, out + 2 * LS_TRIALS);
+  if (p > 0) {
+    const int be = (p + 255) / 256;
+    k_pd_trials_cols<<<be, 256, 0, s>>>(rp, adx, p, sbase, beta, part_eq, nullptr);
+    launch_sum_chunks(s, part_eq, be, LS_TRIALS, out + 3 * LS_TRIALS);
+  }
+}
+
+// The central residual r_cent = -l (c - ub) - 1/t at (x, lambda) (:97-106; k_pd_dlambda's expression), 0 on padded
+// rows: the state's |r_t| after a step (solve_withEQs :606).
+__global__ void k_pd_central(const double* __restrict__ c, const double* __restrict__ ub,
+                             const double* __restrict__ lam, double t, int m, int mp, double* __restrict__ rc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= mp) return;
+  rc[i] = (i < m) ? -lam[i] * (c[i] - ub[i]) - 1.0 / t : 0.0;
+}
+void launch_pd_central(hipStream_t s, const double* c, const double* ub, const double* lam, double t, int m, int mp,
+                       double* rc) {
+  k_pd_central<<<(mp + 255) / 256, 256, 0, s>>>(c, ub, lam, t, m, mp, rc);
 }
 
 }  // namespace cvxg

@@ -136,7 +136,10 @@ void launch_pd_reset_s0(hipStream_t s, DevCtrl* ctrl);
 void launch_pd_trials(hipStream_t s, const double* c, const double* e, const double* ub, const double* lam,
                       const double* dlam, int m, const double* R0, const double* R1, int n, double sbase, double beta,
                       double t, double* part_rows, double* part_cols, double* out, const double* f = nullptr,
-                      const double* R2 = nullptr);
+                      const double* R2 = nullptr, const double* rp = nullptr, const double* adx = nullptr, int p = 0,
+                      double* part_eq = nullptr);
+void launch_pd_central(hipStream_t s, const double* c, const double* ub, const double* lam, double t, int m, int mp,
+                       double* rc);
 
 // ---- MFMA SYRK (k_syrk.hip) -----------------------------------------------------------------------
 // H = t*P + A' diag(w) A over the lower tile list; split-K when nsplit > 1 (partials + ordered reduce).

@@ -230,7 +230,7 @@ class Engine:
         self._check(self.lib.cvxg_centering(self.h, C.byref(ps), float(t), C.byref(info)))
         return info
 
-    # --- primal-dual solver (PrimalDualSolver.scala, no equalities) -------------------------------
+    # --- primal-dual solver (PrimalDualSolver.scala) ------------------------------------------------
     def pd_direction(self, pars, t: float, x, lam):
         """(dx, dlambda, info) of one primal-dual KKT solve at (t, x, lambda) (cvxg_pd_direction)."""
         x, lam = _f64(x), _f64(lam)
@@ -241,16 +241,36 @@ class Engine:
                                                C.byref(info)))
         return dx, dlam, info
 
-    def pd_solve(self, pars) -> L.cvxg_pd_solution:
+    def pd_direction_eq(self, pars, t: float, x, lam, nu):
+        """(dx, dlambda, dnu, info) of one solve_withEQs KKT solve at (t, x, lambda, nu) (cvxg_pd_direction_eq)."""
+        x, lam, nu = _f64(x), _f64(lam), _f64(nu)
+        dx, dlam, dnu = np.zeros(self.n), np.zeros(self.m), np.zeros(max(self.p, 1))
+        info = L.cvxg_pd_step_info()
+        ps = params_struct(pars)
+        self._check(self.lib.cvxg_pd_direction_eq(self.h, C.byref(ps), float(t), _dp(x), _dp(lam), _dp(nu), _dp(dx),
+                                                  _dp(dlam), _dp(dnu), C.byref(info)))
+        return dx, dlam, dnu[:self.p], info
+
+    def pd_solve(self, pars, partial: bool = False):
+        """cvxg_pd_solve.  partial=True returns (status, solution) instead of raising: the solution then describes
+        the last accepted iterate (solve_withEQs fails in its line search like the reference)."""
         sol = L.cvxg_pd_solution()
         ps = params_struct(pars)
-        self._check(self.lib.cvxg_pd_solve(self.h, C.byref(ps), C.byref(sol)))
+        rc = self.lib.cvxg_pd_solve(self.h, C.byref(ps), C.byref(sol))
+        if partial:
+            return rc, sol
+        self._check(rc)
         return sol
 
     def get_lambda(self) -> np.ndarray:
         lam = np.zeros(self.m)
         self._check(self.lib.cvxg_get_lambda(self.h, _dp(lam)))
         return lam
+
+    def get_nu(self) -> np.ndarray:
+        nu = np.zeros(self.p)
+        self._check(self.lib.cvxg_get_nu(self.h, _dp(nu)))
+        return nu
 
     def barrier_solve(self, pars, termination: int = 0) -> L.cvxg_solution:
         sol = L.cvxg_solution()

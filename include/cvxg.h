@@ -227,14 +227,17 @@ typedef struct cvxg_pd_step_info {
   int regularized;          /* regularizedCholesky used Q + 1e-10 I */
 } cvxg_pd_step_info;
 
-/* Solution of PrimalDualSolver.solve (PrimalDualSolver.scala:455-459). */
+/* Solution of PrimalDualSolver.solve (PrimalDualSolver.scala:455-459; with equality rows :615-620).  Filled after
+ * every completed iteration, so after a failed one (CVXG_E_LINESEARCH) it describes the last accepted iterate. */
 typedef struct cvxg_pd_solution {
   double duality_gap;       /* surrogate gap -h(x).lambda (:289-297) */
-  double norm_dual_residual;/* |grad f + Dg' lambda| (:63-71) */
+  double norm_dual_residual;/* |grad f + Dg' lambda| (:63-71); with equality rows the whole |r_t(x, lambda, nu)|
+                               (residual_withEqs :133-145, as solve_withEQs reports it, :606) */
   double objective;         /* objF.valueAt(x) */
   int iter;                 /* iterations - 1 (reference semantics, :458) */
-  int maxed_out;            /* iter == 2000/mu */
+  int maxed_out;            /* iter == 2000/mu (1500/mu with equality rows, :577) */
   int newton_steps;         /* KKT solves performed (instrumentation) */
+  double equality_gap;      /* |A x - b| with equality rows (:603), 0 without */
 } cvxg_pd_solution;
 
 /* The primal-dual search direction at (t, x, lambda) (PrimalDualSolver.scala:216-261, 184-209): the KKT
@@ -245,16 +248,31 @@ typedef struct cvxg_pd_solution {
 int cvxg_pd_direction(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, const double* lambda,
                       double* dx, double* dlambda, cvxg_pd_step_info* info);
 
+/* The search direction of solve_withEQs (PrimalDualSolver.scala:590-593) at (t, x, lambda, nu) for a context with
+ * p > 0 equality rows (cvxg_set_eq): kktSystem_withEqs (:271-285) = KKTSystem(H_pd, A, q = rhs1 + A'nu, b - A x)
+ * solved as KKTSystem.solve does for the barrier's equality step (KKTSystem.scala:43-66: solvePD, solvePD on
+ * H + A'A, kktSymSolve), giving dx (n) and dnu (p), then deltaLambda (m).  With p == 0 nu / dnu are ignored and this
+ * is cvxg_pd_direction.  Output pointers may be NULL. */
+int cvxg_pd_direction_eq(cvxg_ctx* ctx, const cvxg_params* pars, double t, const double* x, const double* lambda,
+                         const double* nu, double* dx, double* dlambda, double* dnu, cvxg_pd_step_info* info);
+
 /* PrimalDualSolver.solve (PrimalDualSolver.scala:628-633 -> solve_noEQs :381-460) from the current iterate
  * (cvxg_set_x: a strictly feasible point): lambda0 = -1/h(x0) (ConstraintSet.scala:116-120), t = mu m / gap,
  * residual-norm backtracking line search (:311-374), stop when gap < tolSolver and |r_dual| < tolSolver.
- * The reference's solve_withEQs is not built (CVXG_E_UNSUPPORTED for p > 0): it passes q = rhs1 + A'nu to
- * KKTSystem, which solves H dx + A'dnu = -q, the opposite sign of its own no-equality system ("FIX ME",
- * PrimalDualSolver.scala:284), and its line search fails on the reference's known-answer problems. */
+ * With equality rows (p > 0) solve_withEQs (:550-621) as written: nu0 = 0, the direction of cvxg_pd_direction_eq,
+ * lineSearch_withEQs (:478-543) on |(r_dual + A'nu, r_central, A x - b)|, at most 1500/mu iterations.  The reference
+ * passes q = rhs1 + A'nu to KKTSystem, which solves H dx + A'dnu = -q: the opposite sign of its own no-equality
+ * system ("FIX ME", :284).  Its line search then fails after a few iterations on every problem we ran (the
+ * reference's known-answer problems and random QPs, tests/test_oracle_known_answers.py); the engine reproduces the
+ * same trajectory and returns CVXG_E_LINESEARCH at the same iteration, where the reference throws
+ * LineSearchFailedException (sol and the iterate then hold the last accepted step). */
 int cvxg_pd_solve(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_pd_solution* sol);
 
 /* The dual iterate lambda (m entries) after cvxg_pd_solve. */
 int cvxg_get_lambda(cvxg_ctx* ctx, double* lambda);
+
+/* The equality multipliers nu (p entries) after cvxg_pd_solve with equality rows. */
+int cvxg_get_nu(cvxg_ctx* ctx, double* nu);
 
 /* ---- affine re-parametrisation x = z0 + F u (BarrierSolver.affineTransformed / reduced) ----------- */
 

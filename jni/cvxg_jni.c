@@ -18,6 +18,7 @@
 #include <jni.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "cvxg.h"
 
@@ -474,19 +475,65 @@ JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_pdDirection(JNIEnv* env, jclass c
   return rc;
 }
 
-/* pdSolve(h, maxIter, params[6], out[6]) -> PrimalDualSolver.solve on the device (cvxg_pd_solve) */
+/* pdDirectionEq(h, maxIter, params[6], t, x[n], lambda[m], nu[p], dx[n], dlambda[m], dnu[p] (outputs nullable),
+ * info[9] (nullable)): the solve_withEQs search direction (cvxg_pd_direction_eq), info as pdDirection */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_pdDirectionEq(JNIEnv* env, jclass cls, jlong h, jint maxIter,
+                                                             jdoubleArray jp, jdouble t, jdoubleArray x,
+                                                             jdoubleArray lambda, jdoubleArray nu, jdoubleArray dx,
+                                                             jdoubleArray dlambda, jdoubleArray dnu,
+                                                             jdoubleArray info) {
+  (void)cls;
+  int ok = 1;
+  cvxg_params p;
+  cvxg_pd_step_info si;
+  fill_params(env, jp, maxIter, &p);
+  double* px = din(env, x, &ok);
+  double* pl = din(env, lambda, &ok);
+  double* pn = din(env, nu, &ok);
+  double* pd = dout(env, dx, &ok);
+  double* pdl = dout(env, dlambda, &ok);
+  double* pdn = dout(env, dnu, &ok);
+  jint rc = ok ? cvxg_pd_direction_eq(CTX(h), &p, t, px, pl, pn, pd, pdl, pdn, &si) : CVXG_E_ARG;
+  dput(env, dnu, pdn, rc);
+  dput(env, dlambda, pdl, rc);
+  dput(env, dx, pd, rc);
+  dfree(pn);
+  dfree(pl);
+  dfree(px);
+  if (rc == CVXG_OK && info) {
+    double o[9] = {si.t, si.s0, si.step, si.norm_residual, si.rel_err, (double)si.backtracks, (double)si.fallback,
+                   (double)si.ruiz_sweeps, (double)si.regularized};
+    (*env)->SetDoubleArrayRegion(env, info, 0, 9, o);
+  }
+  return rc;
+}
+
+/* pdSolve(h, maxIter, params[6], out[7]) -> PrimalDualSolver.solve on the device (cvxg_pd_solve; solve_withEQs when
+ * the context has equality rows).  out = {gap, normResidual, objective, iter, maxedOut, newtonSteps, equalityGap},
+ * also written on CVXG_E_LINESEARCH (the last accepted iterate; the Scala side throws LineSearchFailedException). */
 JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_pdSolve(JNIEnv* env, jclass cls, jlong h, jint maxIter, jdoubleArray jp,
                                                        jdoubleArray out) {
   (void)cls;
   cvxg_params p;
   cvxg_pd_solution s;
+  memset(&s, 0, sizeof(s));
   fill_params(env, jp, maxIter, &p);
   jint rc = cvxg_pd_solve(CTX(h), &p, &s);
-  if (rc == CVXG_OK) {
-    double o[6] = {s.duality_gap, s.norm_dual_residual, s.objective, (double)s.iter, (double)s.maxed_out,
-                   (double)s.newton_steps};
-    (*env)->SetDoubleArrayRegion(env, out, 0, 6, o);
+  if (rc == CVXG_OK || rc == CVXG_E_LINESEARCH) {
+    double o[7] = {s.duality_gap, s.norm_dual_residual, s.objective, (double)s.iter, (double)s.maxed_out,
+                   (double)s.newton_steps, s.equality_gap};
+    (*env)->SetDoubleArrayRegion(env, out, 0, 7, o);
   }
+  return rc;
+}
+
+/* getNu(h, nu[p]) -> the equality multipliers after pdSolve (cvxg_get_nu) */
+JNIEXPORT jint JNICALL Java_cvx_gpu_CvxgNative_getNu(JNIEnv* env, jclass cls, jlong h, jdoubleArray nu) {
+  (void)cls;
+  int ok = 1;
+  double* pn = dout(env, nu, &ok);
+  jint rc = ok ? cvxg_get_nu(CTX(h), pn) : CVXG_E_ARG;
+  dput(env, nu, pn, rc);
   return rc;
 }
 

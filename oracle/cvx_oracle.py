@@ -1239,12 +1239,31 @@ def pd_solve(pb: Problem, x0: np.ndarray, pars: SolverParams, record: bool = Fal
                       maxedOut=it == maxIter, records=records)
 
 
+def pd_residual_eq(pb: Problem, t: float, x: np.ndarray, lam: np.ndarray, nu: np.ndarray) -> np.ndarray:
+    """residual_withEqs (:133-145) = (r_dual + A'nu (:76-90), r_central, A x - b (:111-120))."""
+    A, b = pb.Aeq, pb.beq
+    return np.concatenate([pd_dual_residual(pb, x, lam) + A.T @ nu, pd_central_residual(pb, t, x, lam), A @ x - b])
+
+
+def pd_direction_eq(pb: Problem, t: float, x: np.ndarray, lam: np.ndarray, nu: np.ndarray, tolEqSolve: float,
+                    info: Optional[dict] = None):
+    """One KKT solve of solve_withEQs (:590-593): kktSystem_withEqs (:271-285) = KKTSystem(H_pd, A, q = rhs1 + A'nu,
+    -(A x - b)), KKTSystem.solve (H dx + A'dnu = -q), then deltaLambda.  Returns (dx, dlambda, dnu)."""
+    A, b = pb.Aeq, pb.beq
+    H = pd_kkt_matrix(pb, x, lam)
+    q = pd_rhs1(pb, t, x) + A.T @ nu
+    dx, dnu = kkt_solve(H, A, q, -(A @ x - b), tolEqSolve, info)
+    return dx, pd_delta_lambda(pb, t, x, dx, lam), dnu
+
+
 def pd_solve_with_eqs(pb: Problem, x0: np.ndarray, pars: SolverParams, record: bool = False):
     """PrimalDualSolver.solve_withEQs (:550-621) as written: KKTSystem(H, A, q = rhs1 + A'nu, b = -(Ax - b))
     (:271-285, the reference's own 'FIX ME: check this!'); KKTSystem solves H dx + A' w = -q, the OPPOSITE sign
     of the no-equality system H dx = rhs1.  lineSearch_withEQs (:478-543) on the full residual
     (r_dual + A'nu, r_central, Ax - b); normDualResidual is the norm of that full residual; <= 1500/mu
-    iterations.  Returns (x, lambda, nu, gap, normResidual, iter, maxedOut) or raises like the reference."""
+    iterations.  Returns (x, lambda, nu, gap, normResidual, iter, maxedOut[, records]) or raises like the
+    reference: LineSearchFailedException, with .records (record=True) and .state = (x, lambda, nu, gap,
+    normResidual, equalityGap, completed iterations) of the last accepted iterate."""
     A, b = pb.Aeq, pb.beq
     tol, mu, m = pars.tolSolver, 10.0, pb.m
     x = x0.copy()
@@ -1252,30 +1271,28 @@ def pd_solve_with_eqs(pb: Problem, x0: np.ndarray, pars: SolverParams, record: b
     nu = np.zeros(A.shape[0])
     gap = -float(np.dot(pd_constraint_function(pb, x), lam))
     normRes = float("inf")
+    eqGap = float("inf")
     t = mu * m / gap
-
-    def residual(t_, x_, l_, n_):
-        return np.concatenate([pd_dual_residual(pb, x_, l_) + A.T @ n_, pd_central_residual(pb, t_, x_, l_),
-                               A @ x_ - b])
-
     maxIter = 1500 / mu
     it = 0
+    records = []
     while not (gap < tol and normRes < tol) and it < maxIter:
-        H = pd_kkt_matrix(pb, x, lam)
-        q = pd_rhs1(pb, t, x) + A.T @ nu
-        dx, dnu = kkt_solve(H, A, q, -(A @ x - b), pars.tolEqSolve)
-        dlam = pd_delta_lambda(pb, t, x, dx, lam)
+        info = {}
+        dx, dlam, dnu = pd_direction_eq(pb, t, x, lam, nu, pars.tolEqSolve, info)
+        rec = dict(t=t, x=x.copy(), lam=lam.copy(), nu=nu.copy(), dx=dx, dlam=dlam, dnu=dnu,
+                   fallback=info.get("fallback", 0))
         s0 = 1.0
         for i in range(m):
             if dlam[i] < 0 and -lam[i] / dlam[i] < s0:
                 s0 = -lam[i] / dlam[i]
         s = 0.99 * s0
-        norm_rt = float(np.linalg.norm(residual(t, x, lam, nu)))
+        norm_rt = float(np.linalg.norm(pd_residual_eq(pb, t, x, lam, nu)))
+        rec.update(s0=s0, norm_rt=norm_rt)
 
         def trial(s_):
             x_s, l_s, n_s = x + dx * s_, lam + dlam * s_, nu + dnu * s_
             ok = all(is_satisfied_strictly(pb, i, x_s) for i in range(m))
-            dec = float(np.linalg.norm(residual(t, x_s, l_s, n_s))) < (1 - pars.alpha * s_) * norm_rt
+            dec = float(np.linalg.norm(pd_residual_eq(pb, t, x_s, l_s, n_s))) < (1 - pars.alpha * s_) * norm_rt
             return ok and dec, (x_s, l_s, n_s)
 
         good, u = trial(s)
@@ -1285,11 +1302,21 @@ def pd_solve_with_eqs(pb: Problem, x0: np.ndarray, pars: SolverParams, record: b
             s *= pars.beta
             good, u = trial(s)
             k += 1
+        rec.update(step=s, backtracks=k)
+        if record:
+            records.append(rec)
         if k >= maxLS:
-            raise LineSearchFailedException("Line search unsuccessful.")
+            e = LineSearchFailedException("Line search unsuccessful.")
+            e.records = records
+            e.state = (x, lam, nu, gap, normRes, eqGap, it)
+            raise e
         x, lam, nu = u
         gap = -float(np.dot(pd_constraint_function(pb, x), lam))
-        normRes = float(np.linalg.norm(residual(t, x, lam, nu)))
-        t = mu * m / gap
+        normRes = float(np.linalg.norm(pd_residual_eq(pb, t, x, lam, nu)))
+        eqGap = float(np.linalg.norm(A @ x - b))
+        with np.errstate(divide="ignore"):
+            t = float(np.float64(mu * m) / np.float64(gap))
         it += 1
+    if record:
+        return x, lam, nu, gap, normRes, it - 1, it == maxIter, records
     return x, lam, nu, gap, normRes, it - 1, it == maxIter

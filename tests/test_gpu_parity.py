@@ -1093,15 +1093,94 @@ def test_pd_known_minimizers_on_gpu(mods, spec_fn):
     prob.solver.engine.close()
 
 
-def test_pd_with_equalities_is_unsupported(mods):
+@pytest.mark.parametrize("n,m,p", [(40, 96, 3), (300, 500, 6), (200, 300, 70)])
+def test_pd_direction_eq_vs_oracle(mods, n, m, p):
+    """One solve_withEQs KKT solve (kktSystem_withEqs + KKTSystem.solve + deltaLambda, PrimalDualSolver.scala:271-285,
+    590-593) from identical (t, x, lambda, nu), nu != 0: dx, dlambda and dnu within 1e-8 of the oracle, the same s0
+    and KKT fallback.  p = 70: the wide KKT path (p + 1 > MAX_RHS, the dataflow Schur complement)."""
     Z, SP, Engine, O = mods
-    spec = Z.joptP2()
+    spec = Z.random_qp_eq(n, m, p, instance=5)
+    pb = _opb(O, spec)
     eng = _engine(Engine, spec)
-    eng.set_x(np.array([0.5, 0.5]))
-    from cvx_amd.engine import CvxgError
-    with pytest.raises(CvxgError):
-        eng.pd_solve(SP.standardParams())
+    pars = SP.standardParams()
+    x = spec["x0"]
+    lam = -1.0 / O.pd_constraint_function(pb, x)
+    nu = np.random.default_rng(7).uniform(-1.0, 1.0, size=p)
+    for t in (10.0, 1e3, 1e5):
+        dx, dlam, dnu, info = eng.pd_direction_eq(pars, t, x, lam, nu)
+        ref_info = {}
+        dxr, dlr, dnr = O.pd_direction_eq(pb, t, x, lam, nu, pars.tolEqSolve, ref_info)
+        assert np.linalg.norm(dx - dxr) <= 1e-8 * np.linalg.norm(dxr), t
+        assert np.linalg.norm(dlam - dlr) <= 1e-8 * np.linalg.norm(dlr), t
+        assert np.linalg.norm(dnu - dnr) <= 1e-8 * np.linalg.norm(dnr), t
+        s0 = 1.0
+        for i in range(pb.m):
+            if dlr[i] < 0 and -lam[i] / dlr[i] < s0:
+                s0 = -lam[i] / dlr[i]
+        assert info.s0 == pytest.approx(s0, rel=1e-10)
+        assert info.fallback == ref_info.get("fallback", 0)
     eng.close()
+
+
+def _pd_eq_cases(Z, O):
+    pars = O.standard_params()
+    for spec in (Z.joptP2(), Z.rank_one_problem_simplex(10)):
+        pb = _opb(O, spec)
+        yield spec["id"], spec, pb, O.with_feasible_point(pb, spec["x_where_defined"], pars)
+    for (n, m, p, inst) in ((20, 40, 2, 0), (40, 96, 3, 1), (60, 100, 5, 2), (30, 60, 1, 3), (100, 200, 8, 4)):
+        spec = Z.random_qp_eq(n, m, p, instance=inst)
+        yield spec["id"], spec, _opb(O, spec), spec["x0"]
+
+
+def test_pd_solve_with_equalities_fails_like_the_reference(mods):
+    """PrimalDualSolver.solve_withEQs (PrimalDualSolver.scala:550-621) as the reference writes it: its KKT
+    right-hand side has the opposite sign of the no-equality system ("FIX ME", :284) and its line search throws
+    LineSearchFailedException (:538-541) after a few iterations on every problem here (the reference's
+    equality-constrained known-answer problems and random QPs).  The engine runs the same iterations: it fails at
+    the same iteration (CVXG_E_LINESEARCH), and the last accepted (x, lambda, nu), gap, |r_t| and |A x - b| match
+    the oracle's (1e-6)."""
+    Z, SP, Engine, O = mods
+    from cvx_amd import _lib as L
+    pars = SP.standardParams()
+    for name, spec, pb, x0 in _pd_eq_cases(Z, O):
+        with pytest.raises(O.LineSearchFailedException) as ei:
+            O.pd_solve_with_eqs(pb, x0, O.standard_params(), record=True)
+        xr, lr, nr, gap, nres, egap, done = ei.value.state
+        p = spec["Aeq"].shape[0]
+        eng = Engine(x0.shape[0], spec["A"].shape[0], p)
+        eng.load_problem(spec)
+        eng.set_x(x0)
+        rc, sol = eng.pd_solve(pars, partial=True)
+        assert rc == L.CVXG_E_LINESEARCH, (name, rc)
+        assert sol.newton_steps == done, (name, sol.newton_steps, done)
+        x, lam, nu = eng.get_x(), eng.get_lambda(), eng.get_nu()
+        eng.close()
+        tol = lambda ref: 1e-6 * max(1.0, np.linalg.norm(ref))
+        assert np.linalg.norm(x - xr) <= tol(xr), name
+        assert np.linalg.norm(lam - lr) <= tol(lr), name
+        assert np.linalg.norm(nu - nr) <= tol(nr), name
+        if done > 0:
+            assert sol.duality_gap == pytest.approx(gap, rel=1e-6, abs=1e-12), name
+            assert sol.norm_dual_residual == pytest.approx(nres, rel=1e-6, abs=1e-12), name
+            assert sol.equality_gap == pytest.approx(egap, rel=1e-6, abs=1e-10), name
+        print(f"{name}: LineSearchFailedException after {done} iterations on both sides")
+
+
+def test_pd_with_equalities_api_raises_line_search_failed(mods):
+    """OptimizationProblem.apply(..., "PD") with an EqualityConstraint (OptimizationProblem.scala:154 ->
+    PrimalDualSolver.solve -> solve_withEQs): LineSearchFailedException, its .solution the last accepted iterate."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import LineSearchFailedException, OptimizationProblem, problem_from_spec
+    spec = Z.random_qp_eq(40, 96, 3, instance=1)
+    objF, cs, eqs = problem_from_spec(spec)
+    assert eqs is not None
+    pars = SP.standardParams()
+    prob = OptimizationProblem.apply(spec["id"], objF, cs.addFeasiblePoint(spec["x0"]), eqs, "PD", pars)
+    with pytest.raises(LineSearchFailedException) as ei:
+        prob.solve()
+    sol = ei.value.solution
+    assert sol.nu is not None and sol.nu.shape == (3,) and sol.equalityGap is not None
+    prob.solver.engine.close()
 
 
 # ---- QuadraticConstraint rows (QuadraticConstraint.scala) in the barrier path -------------------------------------
