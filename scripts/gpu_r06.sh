@@ -25,6 +25,12 @@ for st in ${STAGES:-smoke tests ab}; do
         done
       done
       python scripts/ab_summary.py $O > $O/ab_summary.txt 2>&1 ;;
+    abfull)  # whole C3 solves (regularized steps: the speculative pair) with each library, in rotation
+      for r in $(seq 1 ${ROUNDS:-2}); do
+        for v in ${LIBS:-}; do
+          CVXG_LIB=$R/cvx_amd/libcvxg_$v.so timeout -k 10 300 python bench.py --workload C3FULL > $O/full_$v$r.json 2>$O/full_$v$r.err; chk $? full_$v$r
+        done
+      done ;;
     bench) timeout -k 10 500 python bench.py ${BENCH_ARGS:-} > $O/bench.log 2>&1; chk $? bench ;;
     full) timeout -k 10 300 python bench.py --workload C3FULL > $O/bench_full.log 2>&1; chk $? full ;;
     ruizloop)  # the one-launch Ruiz loop against the launch pairs at C2 and C4
