@@ -178,6 +178,21 @@ PMC_TRAFFIC = latest_profile("pmc_traffic.json")
 TRACE_ROOFLINE = latest_profile("trace_roofline.json")
 
 
+def committed_whole_solve():
+    """The newest committed C3FULL line (one complete C3 barrier solve with the standard parameters, `bench.py
+    --workload C3FULL`): the whole-job rate, regularized steps included, beside the t = 1 window `value` times."""
+    path = latest_profile("bench_c3full.json")
+    try:
+        d = json.loads(open(path).read().strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError):
+        return None
+    return {"source": os.path.relpath(path, ROOT), "note": "a committed C3FULL line, not measured by this run",
+            "steps_per_s": d.get("value"), "newton_steps": d.get("steps"),
+            "steps_per_centering": d.get("steps_per_centering"),
+            "regularized_refactorizations": d.get("regularized_refactorizations"),
+            "cholesky_ms_per_step": (d.get("phases_ms_per_occurrence_timed_solve") or {}).get("cholesky_fused_fwd")}
+
+
 def trace_roofline():
     try:
         d = json.load(open(TRACE_ROOFLINE))
@@ -440,6 +455,7 @@ def run_rank(args, engine_cls=None, backend: str = "nccl", device=None):
         "ruiz_lookahead_reruns": ruiz_reruns,
         "ls_full_steps": full_steps,
         "steady_state": steady,
+        "whole_solve_committed": committed_whole_solve() if wl == "C3" else None,
         "gathered_ranks": len(gathered),
     }
     return out, gathered
