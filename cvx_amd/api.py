@@ -618,15 +618,15 @@ class LineSearchFailedException(NotConvergedException):
 
 class GpuPrimalDualSolver:
     """PrimalDualSolver (PrimalDualSolver.scala:18-621) on the MI355X engine: each iteration's KKT matrix, its
-    solve, dlambda and the residual line-search trials run on the device (cvxg_pd_solve).  Quadratic or linear
-    objective, LinearConstraint and QuadraticConstraint members; with equality constraints solve_withEQs as the
+    solve, dlambda and the residual line-search trials run on the device (cvxg_pd_solve).  Quadratic, linear or KL
+    primal objective, LinearConstraint and QuadraticConstraint members; with equality constraints solve_withEQs as the
     reference writes it (its KKT right-hand side "FIX ME", :284), whose line search fails like the reference's
     (LineSearchFailedException, see include/cvxg.h)."""
 
     def __init__(self, objF: ObjectiveFunction, cnts: ConstraintSet, eqs: Optional[EqualityConstraint],
                  pars: SolverParams, device: int = 0):
-        if not isinstance(objF, (QuadraticObjectiveFunction, LinearObjectiveFunction)):
-            raise TypeError("GPU primal-dual engine: objective must be Quadratic- or LinearObjectiveFunction")
+        if not isinstance(objF, (QuadraticObjectiveFunction, LinearObjectiveFunction, KLPrimalObjectiveFunction)):
+            raise TypeError("GPU primal-dual engine: objective must be Quadratic-, Linear- or KLPrimalObjectiveFunction")
         if cnts.feasiblePoint is None:
             raise ValueError("ConstraintSet with FeasiblePoint required (use withFeasiblePoint)")
         self.objF, self.cnts, self.eqs, self.pars = objF, cnts, eqs, pars
@@ -636,7 +636,10 @@ class GpuPrimalDualSolver:
         A, r, ub = cnts.packed()
         p = eqs.A.shape[0] if eqs is not None else 0
         self.engine = Engine(cnts.dim, A.shape[0], p, device)
-        self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
+        if isinstance(objF, KLPrimalObjectiveFunction):  # Dist_KL.objectiveFunction (Dist_KL.scala:223-239)
+            self.engine.set_objective_kl_primal(objF.n)
+        else:
+            self.engine.set_objective(objF.a, objF.r, getattr(objF, "P", None))
         self.engine.set_ineq(A, r, ub)
         if eqs is not None:
             self.engine.set_eq(eqs.A, eqs.b)
@@ -784,15 +787,12 @@ class Dist_KL(OptimizationProblem):
         return solD
 
     def solve(self, debugLevel: int = 0) -> Solution:
-        """The direct solve (Dist_KL.scala:309-312): BarrierSolver(objF, ineqsWithFeasiblePoint, Some(eqs)) on the
-        engine's KL primal objective.  "PD" builds the reference's PrimalDualSolver with equalities (solve_withEQs)
-        over the KL objective, which the device primal-dual solver does not take (quadratic or linear objectives
-        only, include/cvxg.h)."""
-        if self.solverType == "PD":
-            raise TypeError("GPU primal-dual engine: the KL primal objective is not supported (solverType \"PD\")")
+        """The direct solve (Dist_KL.scala:309-315) on the engine's KL primal objective: "BR" builds
+        BarrierSolver(objF, ineqsWithFeasiblePoint, Some(eqs)), "PD" PrimalDualSolver(C, objF, ineqsWithFeasiblePoint,
+        Some(eqs)), whose solve_withEQs raises LineSearchFailedException like the reference's (include/cvxg.h)."""
         if self.solver is None:
-            self.solver = BarrierSolver.apply(self.objectiveFunction, self.ineqsWithFeasiblePoint, self.eqs, self.pars,
-                                              self.device)
+            build = PrimalDualSolver.apply if self.solverType == "PD" else BarrierSolver.apply
+            self.solver = build(self.objectiveFunction, self.ineqsWithFeasiblePoint, self.eqs, self.pars, self.device)
         return self.solver.solve(debugLevel)
 
 

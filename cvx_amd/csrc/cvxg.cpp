@@ -2653,8 +2653,8 @@ int cvxg_get_phase_stats(cvxg_ctx* ctx, double* ms, int* occurrences, int count)
 // ------------------------------------------------------------------------------------------------
 static int pd_check(cvxg_ctx* ctx) {
   CHK(check_ready(ctx));
-  if (ctx->kl || ctx->klp)
-    return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: quadratic or linear objective only");
+  if (ctx->kl)
+    return set_err(ctx, CVXG_E_UNSUPPORTED, "primal-dual engine: quadratic, linear or KL primal objective only");
   if (ctx->m == 0) return set_err(ctx, CVXG_E_ARG, "primal-dual solver needs inequality constraints");
   if (ctx->lam) return CVXG_OK;
   const size_t np = ctx->np, mp = ctx->mp;
@@ -2672,6 +2672,12 @@ static int pd_check(cvxg_ctx* ctx) {
   }
   HIPC(ctx, hipHostMalloc((void**)&ctx->pd_hout, 4 * LS_TRIALS * sizeof(double), hipHostMallocDefault));
   return CVXG_OK;
+}
+
+// The objective gradient's x-dependent part at the evaluated x for the dual residual: P x, or the KL primal's
+// (1 + log x) + log n (klp_g0; a0 = 0 there).
+static const double* pd_grad_term(cvxg_ctx* ctx) {
+  return ctx->klp ? ctx->klp_g0 : (ctx->hasP ? ctx->Px : nullptr);
 }
 
 // grad f(x) + Dg' v into out (the dual residual, :63-71): A' v, plus sum_k (P_k x) v_k over the QuadraticConstraint
@@ -2771,8 +2777,7 @@ static int pd_delta_lambda(cvxg_ctx* ctx, double t) {
 static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg_pd_step_info* info) {
   hipStream_t s = ctx->s;
   const int n = ctx->n, np = ctx->np, p = ctx->p;
-  const double* Px = ctx->hasP ? ctx->Px : nullptr;
-  pd_dual_residual(ctx, ctx->lam, ctx->a0, Px, ctx->pd_R0);                      // r_dual(x, lambda)
+  pd_dual_residual(ctx, ctx->lam, ctx->a0, pd_grad_term(ctx), ctx->pd_R0);       // r_dual(x, lambda)
   if (ctx->hasP) launch_rowdot(s, ctx->P, np, np, np, ctx->dx, ctx->pd_tmp);     // P dx
   pd_dual_residual(ctx, ctx->dlam, nullptr, ctx->hasP ? ctx->pd_tmp : nullptr, ctx->pd_R1);
   if (ctx->nq > 0) {  // Dg(x + s dx)'(l + s dl): + s sum_k (P_k dx) l_k, + s^2 sum_k (P_k dx) dl_k
@@ -2790,7 +2795,17 @@ static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg
     R0 = ctx->pd_R0e;
     R1 = ctx->pd_R1e;
   }
-  launch_dot(s, R0, nullptr, p > 0 ? n : np, ctx->ctrl, SC_RES2);
+  launch_dot(s, R0, nullptr, p > 0 ? n : np, ctx->ctrl, SC_RES2);  // |r_dual(x, lambda) (+ A'nu)|^2
+  const double* R0t = R0;  // the trials' constant term: with the KL primal objective only the constraint part (A'l
+  if (ctx->klp) {          // (+ A'nu)); the objective's gradient at x_s is formed per trial
+    pd_dual_residual(ctx, ctx->lam, nullptr, nullptr, ctx->pd_tmp);  // (no P with this objective: pd_tmp is free)
+    if (p > 0) {  // (pd_rhs, rhs1 of this step's direction, is free after the solve)
+      launch_btw_plus(s, ctx->Aeq, np, p, ctx->pd_nu, ctx->pd_tmp, n, ctx->pd_rhs);
+      R0t = ctx->pd_rhs;
+    } else {
+      R0t = ctx->pd_tmp;
+    }
+  }
   launch_dot(s, ctx->pd_rc, nullptr, ctx->mp, ctx->ctrl, SC_RES2B);
   HIPC(ctx, hipGetLastError());
   CHK(sync_ctrl(ctx));
@@ -2808,9 +2823,10 @@ static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg
   double sK = 0.0;
   const int nout = p > 0 ? 4 : 3;
   while (K < 0) {
-    launch_pd_trials(s, ctx->c, ctx->e, ctx->ub, ctx->lam, ctx->dlam, ctx->m, R0, R1, ctx->n, sbase, beta, t,
+    launch_pd_trials(s, ctx->c, ctx->e, ctx->ub, ctx->lam, ctx->dlam, ctx->m, R0t, R1, ctx->n, sbase, beta, t,
                      ctx->pd_part_rows, ctx->pd_part_cols, ctx->pd_out, ctx->nq > 0 ? ctx->qf : nullptr,
-                     ctx->nq > 0 ? ctx->pd_R2 : nullptr, ctx->pd_rp, ctx->pd_adx, p, ctx->pd_part_eq);
+                     ctx->nq > 0 ? ctx->pd_R2 : nullptr, ctx->pd_rp, ctx->pd_adx, p, ctx->pd_part_eq,
+                     ctx->klp ? ctx->x : nullptr, ctx->klp ? ctx->dx : nullptr, ctx->klp_n);
     HIPC(ctx, hipGetLastError());
     CHK(copy_sync(ctx, ctx->pd_hout, ctx->pd_out, nout * LS_TRIALS * sizeof(double), hipMemcpyDeviceToHost));
     double sk = sbase;
@@ -2844,7 +2860,7 @@ static int pd_line_search(cvxg_ctx* ctx, const cvxg_params* pars, double t, cvxg
 static int pd_state(cvxg_ctx* ctx, double t, double* gap, double* norm_dual, double* eq_gap) {
   CHK(eval_at_x(ctx));
   const int p = ctx->p;
-  pd_dual_residual(ctx, ctx->lam, ctx->a0, ctx->hasP ? ctx->Px : nullptr, ctx->pd_R0);
+  pd_dual_residual(ctx, ctx->lam, ctx->a0, pd_grad_term(ctx), ctx->pd_R0);
   const double* R0 = ctx->pd_R0;
   if (p > 0) {
     launch_btw_plus(ctx->s, ctx->Aeq, ctx->np, p, ctx->pd_nu, ctx->pd_R0, ctx->n, ctx->pd_R0e);

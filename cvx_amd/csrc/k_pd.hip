@@ -140,18 +140,24 @@ __global__ __launch_bounds__(256) void k_pd_trials_rows(const double* __restrict
   }
 }
 // ... and over the variables, the dual residual grad f(x_s) + Dg(x_s)' l_s = R0 + s R1 (+ s^2 R2 with
-// QuadraticConstraint rows, whose gradients a + P x_s move with the step).
+// QuadraticConstraint rows, whose gradients a + P x_s move with the step).  With the KL primal objective (x != NULL)
+// grad f(x_s) is evaluated afresh per trial, (1 + log(x_j + dx_j s)) + log n (Dist_KL.scala:228-229), and R0 / R1
+// carry only the constraint terms; a trial outside the domain gives NaN, which no acceptance test passes.
 __global__ __launch_bounds__(256) void k_pd_trials_cols(const double* __restrict__ R0, const double* __restrict__ R1,
                                                         int n, double sbase, double beta, double* __restrict__ part,
-                                                        const double* __restrict__ R2) {
+                                                        const double* __restrict__ R2, const double* __restrict__ x,
+                                                        const double* __restrict__ dx, double nd) {
   __shared__ double sd[4][LS_TRIALS];
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool valid = j < n;
   const double r0 = valid ? R0[j] : 0.0, r1 = valid ? R1[j] : 0.0, r2 = (valid && R2) ? R2[j] : 0.0;
+  const double xj = (valid && x) ? x[j] : 1.0, dxj = (valid && x) ? dx[j] : 0.0;
+  const double logn = x ? log(nd) : 0.0;  // (as k_klp_eval forms it)
   double s = sbase;
   for (int k = 0; k < LS_TRIALS; ++k) {
-    const double v = R2 ? (r0 + s * r1) + (s * s) * r2 : r0 + s * r1;
+    double v = R2 ? (r0 + s * r1) + (s * s) * r2 : r0 + s * r1;
+    if (x && valid) v = ((1.0 + log(xj + dxj * s)) + logn) + v;
     const double sv = wave_sum(v * v);
     if (lane == 0) sd[wid][k] = sv;
     s *= beta;
@@ -169,15 +175,16 @@ int pd_row_blocks(int m) { return m > 0 ? (m + 255) / 256 : 1; }
 void launch_pd_trials(hipStream_t s, const double* c, const double* e, const double* ub, const double* lam,
                       const double* dlam, int m, const double* R0, const double* R1, int n, double sbase, double beta,
                       double t, double* part_rows, double* part_cols, double* out, const double* f, const double* R2,
-                      const double* rp, const double* adx, int p, double* part_eq) {
+                      const double* rp, const double* adx, int p, double* part_eq, const double* klx,
+                      const double* kldx, double klp_n) {
   const int br = pd_row_blocks(m), bc = (n + 255) / 256;
   k_pd_trials_rows<<<br, 256, 0, s>>>(c, e, ub, lam, dlam, m, sbase, beta, t, part_rows, f);
-  k_pd_trials_cols<<<bc, 256, 0, s>>>(R0, R1, n, sbase, beta, part_cols, R2);
+  k_pd_trials_cols<<<bc, 256, 0, s>>>(R0, R1, n, sbase, beta, part_cols, R2, klx, kldx, klp_n);
   launch_sum_chunks(s, part_rows, br, 2 * LS_TRIALS, out);
   launch_sum_chunks(s, part_cols, bc, LS_TRIALS, out + 2 * LS_TRIALS);
   if (p > 0) {
     const int be = (p + 255) / 256;
-    k_pd_trials_cols<<<be, 256, 0, s>>>(rp, adx, p, sbase, beta, part_eq, nullptr);
+    k_pd_trials_cols<<<be, 256, 0, s>>>(rp, adx, p, sbase, beta, part_eq, nullptr, nullptr, nullptr, 1.0);
     launch_sum_chunks(s, part_eq, be, LS_TRIALS, out + 3 * LS_TRIALS);
   }
 }

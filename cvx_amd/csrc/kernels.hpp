@@ -137,7 +137,8 @@ void launch_pd_trials(hipStream_t s, const double* c, const double* e, const dou
                       const double* dlam, int m, const double* R0, const double* R1, int n, double sbase, double beta,
                       double t, double* part_rows, double* part_cols, double* out, const double* f = nullptr,
                       const double* R2 = nullptr, const double* rp = nullptr, const double* adx = nullptr, int p = 0,
-                      double* part_eq = nullptr);
+                      double* part_eq = nullptr, const double* klx = nullptr, const double* kldx = nullptr,
+                      double klp_n = 0.0);
 void launch_pd_central(hipStream_t s, const double* c, const double* ub, const double* lam, double t, int m, int mp,
                        double* rc);
 

@@ -129,8 +129,9 @@ int cvxg_set_objective_kl(cvxg_ctx* ctx, const double* B, int ldB, int row_major
 /* Dist_KL.objectiveFunction(n) (Dist_KL.scala:223-239), the KL distance from the uniform distribution on nout outcomes
  * (nout = the context's n for Dist_KL's own problems):
  *   valueAt(x) = x . log(x * nout),  gradientAt(x)_j = (1 + log x_j) + log nout,  hessianAt(x) = diag(1 / x).
- * Defined for x > 0 (Dist_KL's allCoordinatesPositive rows keep the iterates there).  The barrier path only: the
- * primal-dual solver and cvxg_affine_from return CVXG_E_UNSUPPORTED for it. */
+ * Defined for x > 0 (Dist_KL's allCoordinatesPositive rows keep the iterates there).  The barrier solver and the
+ * primal-dual solver (Dist_KL.scala:309-315, solverType "PD": its line-search residual takes the gradient afresh at
+ * every trial point) run on it; cvxg_affine_from returns CVXG_E_UNSUPPORTED. */
 int cvxg_set_objective_kl_primal(cvxg_ctx* ctx, int nout);
 
 /* The LinearConstraint list r_i + a_i.x <= ub_i (LinearConstraint.scala:7-32), A row i = a_i in LIST

@@ -1130,6 +1130,13 @@ def _pd_eq_cases(Z, O):
     for (n, m, p, inst) in ((20, 40, 2, 0), (40, 96, 3, 1), (60, 100, 5, 2), (30, 60, 1, 3), (100, 200, 8, 4)):
         spec = Z.random_qp_eq(n, m, p, instance=inst)
         yield spec["id"], spec, _opb(O, spec), spec["x0"]
+    # Dist_KL's direct problems with solverType "PD" (Dist_KL.scala:313-314; the reference's Runner runs kl_2A this
+    # way, Runner.scala:31, 48): the KL primal objective, its gradient taken afresh at every line-search trial
+    for (kind, n) in (("kl_1", 20), ("kl_2", 20), ("kl_1", 64), ("kl_2", 64), ("kl_2", 200)):
+        spec = Z.kl_primal_spec(n, kind)
+        pb = O.Problem(a0=spec["a0"], r0=0.0, P=None, A=spec["A"], r=spec["r"], ub=spec["ub"], Aeq=spec["Aeq"],
+                       beq=spec["beq"], klp_n=n)
+        yield spec["id"], spec, pb, spec["x0"]
 
 
 def test_pd_solve_with_equalities_fails_like_the_reference(mods):
@@ -1164,6 +1171,34 @@ def test_pd_solve_with_equalities_fails_like_the_reference(mods):
             assert sol.norm_dual_residual == pytest.approx(nres, rel=1e-6, abs=1e-12), name
             assert sol.equality_gap == pytest.approx(egap, rel=1e-6, abs=1e-10), name
         print(f"{name}: LineSearchFailedException after {done} iterations on both sides")
+
+
+def test_dist_kl_pd_raises_line_search_failed_like_the_reference(mods):
+    """Dist_KL.apply(..., "PD") (Dist_KL.scala:270-315: phase I, then PrimalDualSolver with Some(eqs)) and solve:
+    the reference's solve_withEQs over the KL primal objective throws LineSearchFailedException; so does the engine,
+    at the oracle's iteration, from the same phase-I point."""
+    Z, SP, Engine, O = mods
+    from cvx_amd.api import Dist_KL, LineSearchFailedException
+    n = 40
+    j = np.arange(n)
+    H = np.vstack([-(j < 3).astype(float), (j >= n // 2).astype(float)])  # kl_1A's rows: P(A) >= 0.36, P(B) <= 0.1
+    u = np.array([-0.36, 0.1])
+    pars = SP.standardParams()
+    prob = Dist_KL.apply("dist_KL_1A", n, H, u, None, None, "PD", pars)
+    x0 = prob.ineqsWithFeasiblePoint.feasiblePoint.copy()
+    with pytest.raises(LineSearchFailedException) as ei:
+        prob.solve()
+    sol = ei.value.solution
+    prob.solver.engine.close()
+    A = np.vstack([H, -np.eye(n)])
+    pb = O.Problem(a0=np.zeros(n), r0=0.0, P=None, A=A, r=np.zeros(A.shape[0]),
+                   ub=np.concatenate([u, np.zeros(n)]), Aeq=np.ones((1, n)), beq=np.ones(1), klp_n=n)
+    with pytest.raises(O.LineSearchFailedException) as eo:
+        O.pd_solve_with_eqs(pb, x0, O.standard_params())
+    xr, done = eo.value.state[0], eo.value.state[6]
+    assert sol.newtonSteps == done
+    assert np.linalg.norm(sol.x - xr) <= 1e-6 * max(1.0, np.linalg.norm(xr))
+    print(f"Dist_KL kl_1A n={n} PD: LineSearchFailedException after {done} iterations on both sides")
 
 
 def test_pd_with_equalities_api_raises_line_search_failed(mods):

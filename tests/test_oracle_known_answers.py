@@ -250,6 +250,20 @@ def test_primal_dual_with_equalities_fails_like_the_reference(spec):
         O.pd_solve_with_eqs(pb, x0, pars)
 
 
+@pytest.mark.parametrize("kind", ["kl_1", "kl_2"])
+def test_primal_dual_with_equalities_on_the_kl_primal_fails_like_the_reference(kind):
+    """Dist_KL with solverType "PD" (Dist_KL.scala:313-314, the reference Runner's configuration, Runner.scala:31, 48)
+    runs solve_withEQs over the KL primal objective: its line search fails there too (a trial's log of a negative
+    coordinate gives NaN, which no acceptance test passes)."""
+    n = 20
+    spec = Z.kl_primal_spec(n, kind)
+    pb = O.Problem(a0=spec["a0"], r0=0.0, P=None, A=spec["A"], r=spec["r"], ub=spec["ub"], Aeq=spec["Aeq"],
+                   beq=spec["beq"], klp_n=n)
+    with np.errstate(invalid="ignore"), pytest.raises(O.LineSearchFailedException) as ei:
+        O.pd_solve_with_eqs(pb, spec["x0"], O.standard_params(), record=True)
+    assert ei.value.state[6] >= 1 and len(ei.value.records) == ei.value.state[6] + 1
+
+
 # ---- QuadraticConstraint problems (SimpleOptimizationProblems.scala:266-300, 347-377, 464-561) ------------------
 
 def _qproblem(spec):
