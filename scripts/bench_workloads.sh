@@ -15,7 +15,7 @@ run() {  # $1 = label, rest = env + args
 }
 run C2 python bench.py --workload C2 --no-cpu-baseline --steps 50 --warmup 5
 run C3B python bench.py --workload C3B --no-cpu-baseline --steps 10 --warmup 2
-run C3B_dense CVXG_SPARSE_ROWS=0 python bench.py --workload C3B --no-cpu-baseline --steps 10 --warmup 2
+run C3B_dense python bench.py --workload C3B --no-cpu-baseline --steps 10 --warmup 2 --opt sparse_rows=0
 run C4 python bench.py --workload C4 --no-cpu-baseline --steps 50 --warmup 5
 run C2PD python bench.py --workload C2PD --no-cpu-baseline --steps 50
 run C3PD python bench.py --workload C3PD --no-cpu-baseline --steps 20
