@@ -97,8 +97,8 @@ struct cvxg_ctx {
   double *cabs = nullptr, *eabs = nullptr, *Pxa = nullptr, *Psa = nullptr;
   double *xtr = nullptr, *Pxtr = nullptr, *c_tr = nullptr, *d_tr = nullptr, *invd_tr = nullptr, *w_tr = nullptr,
          *logd_tr = nullptr;
-  // the speculative evaluation at x1 = x + dx (k_ls_setup_eval), swapped with c/d/invd/w/logd/cabs when the line
-  // search accepts t = 1
+  // the speculative evaluation at x1 = x + dx t (k_ls_setup_eval, t = spec_t below), swapped with c/d/invd/w/logd/cabs
+  // when the line search accepts that t
   double *x1 = nullptr, *c1 = nullptr, *d1 = nullptr, *invd1 = nullptr, *w1 = nullptr, *logd1 = nullptr,
          *cabs1 = nullptr;
   int* tiles = nullptr;
@@ -213,6 +213,9 @@ struct cvxg_ctx {
   // spec_eval_*: the setup's sweep over A also evaluated the constraints at x + dx (linear rows only)
   bool spec_eval_launched = false, spec_eval_have = false;
   double spec_beta = 0.5;
+  // the step the speculative evaluation assumes: the previous step's accepted t (1 at a centering's start); late in
+  // the path the line search takes the same beta^k step after step, early on mostly t = 1
+  double spec_t = 1.0, spec_t_used = 1.0;
   double* spart = nullptr;  // SYRK split-K partials (ctx->part belongs to the evaluation's A'(1/d))
   // affine re-parametrisation (cvxg_affine_from): x = z0 + F u with F (aff_n x n, column-major, ld aff_n)
   double *aff_F = nullptr, *aff_z0 = nullptr;
@@ -651,8 +654,8 @@ static bool step_h_full(const cvxg_ctx* ctx) { return !(ctx->p == 0 && ctx->h_lo
 static bool spec_eval_ok(const cvxg_ctx* ctx) {
   return ls_certified(ctx) && ctx->nq == 0 && !ctx->kl && !ctx->klp && ctx->p == 0;
 }
-// taken: the line search accepted t = 1 along s = dx, and the speculative evaluation at x1 = x + dx (bitwise the
-// x + s t of the step) is the constraint evaluation at the new x
+// taken: the line search accepted the speculated t along s = dx, and the speculative evaluation at x1 = x + dx t
+// (bitwise the x + s t of the step) is the constraint evaluation at the new x
 // ahead: the prefetched assembly belongs to the next step (the end-of-step prefetch, timed in ring slot tick + 1) or
 // to this one (a step that starts without an evaluation, slot tick)
 static int eval_at_x(cvxg_ctx* ctx, bool prefetch = false, bool taken = false, bool ahead = true) {
@@ -1132,7 +1135,9 @@ static int cholesky_solve(cvxg_ctx* ctx, double tol, cvxg_step_info* info) {
     if (se) {
       epi.x = ctx->x;
       epi.x1 = ctx->x1;
+      epi.t1 = ctx->spec_t;
       epi.sctrl = ctx->ctrl;
+      ctx->spec_t_used = ctx->spec_t;
     }
     backward_solve(ctx, 1, epi);
     // relativeSize(H*x - b, b, tol), b = -grad  (MatrixUtils.scala:437-442, 496)
@@ -2368,6 +2373,7 @@ int cvxg_centering_begin(cvxg_ctx* ctx, double t) {
   CHK(set_t(ctx, t));
   ctx->iter = 0;
   ctx->trust = NAN;
+  ctx->spec_t = 1.0;
   ctx->began = 1;
   CHK(eval_at_x(ctx));  // y = objF.gradientAt(x); normGrad; eqDiff   (UnconstrainedSolver.scala:44-46)
   ctx->nd = std::numeric_limits<double>::infinity();  // set to tol + 1 by the first cvxg_newton_step
@@ -2381,6 +2387,7 @@ int cvxg_centering_resume(cvxg_ctx* ctx, double t, int iter, double trust_radius
   CHK(set_t(ctx, t));
   ctx->iter = iter;
   ctx->trust = iter == 0 ? NAN : trust_radius;
+  ctx->spec_t = 1.0;
   ctx->began = 1;
   CHK(eval_at_x(ctx));
   if (grad) {  // the host's y (UnconstrainedSolver.scala:44,131): replaces the engine's gradient for this iteration
@@ -2455,9 +2462,10 @@ int cvxg_newton_step(cvxg_ctx* ctx, const cvxg_params* pars, cvxg_step_info* inf
     info->ls_ties = ties;
     tstop(ctx, 4);
     if (rc != CVXG_OK) return rc;
-    const bool taken = use_spec && spec_eval && tacc == 1.0;
-    if (taken) std::swap(ctx->x, ctx->x1);  // x1 = x + s*1, formed (bitwise as below) before the host read
+    const bool taken = use_spec && spec_eval && tacc == ctx->spec_t_used;
+    if (taken) std::swap(ctx->x, ctx->x1);  // x1 = x + s*t, formed (bitwise as below) before the host read
     else launch_axpy(ctx->s, ctx->x, ctx->sdir, tacc, ctx->np, ctx->x);  // x = x + s*t
+    ctx->spec_t = scale == 1.0 ? tacc : 1.0;  // the next step's guess (s = dx there)
     HIPC(ctx, hipGetLastError());
     info->step = tacc;
     info->backtracks_c = kc;

@@ -116,13 +116,13 @@ __global__ __launch_bounds__(256) void k_bwd_dataflow(const double* __restrict__
       gr.st2(2 * ((b * NB + c) * nrhs + rho), f64x2{s, tag});  // the hand-off granule first
       out[(size_t)(b * NB + c) * nrhs + rho] = s;              // the solution (read after the launch)
     }
-    if (epi.d) {  // Newton step (nrhs = 1): dx = d :* u, and the line search's s = dx, x1 = x + s*1 (k_scale_vec,
+    if (epi.d) {  // Newton step (nrhs = 1): dx = d :* u, and the line search's s = dx, x1 = x + s*t1 (k_scale_vec,
                   // k_spec_prep fused)
       const int i = b * NB + c;
       const double v = epi.d[i] * out[i];
       epi.dx[i] = v;
       if (epi.s) epi.s[i] = v;
-      if (epi.x1) epi.x1[i] = epi.x[i] + v * 1.0;
+      if (epi.x1) epi.x1[i] = epi.x[i] + v * epi.t1;
     }
   }
   if (epi.sctrl && b == 0 && threadIdx.x == 0) {

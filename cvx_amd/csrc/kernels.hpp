@@ -179,7 +179,8 @@ struct BwdEpilogue {
   double* dx = nullptr;
   double* s = nullptr;
   const double* x = nullptr;
-  double* x1 = nullptr;
+  double* x1 = nullptr;  // x1 = x + s t1: the speculative next point (t1: the step the line search is expected to take)
+  double t1 = 1.0;
   DevCtrl* sctrl = nullptr;
 };
 // The second factorization of a speculative pair (regularized_cholesky_spec): used instead of L / Linv / rhs when
